@@ -1,0 +1,378 @@
+"""audio-network_amd — MI355X-native acoustic-FSK demodulator (host mirror).
+
+Thin ctypes mirror of the C ABI in include/demod.h (libfskdemod.so built
+in-tree from audio-network_amd/csrc). Names, argument meaning and error
+behaviour follow the C entry points one-for-one, which in turn mirror the
+Opus-decoder-shaped API at the reference's PCM insertion point
+(hardware/src/playback.cpp:67-74,115-122).
+
+Every compute call runs the HIP kernels on a gfx950 GPU. There is no CPU
+fallback: if libfskdemod.so is missing, :func:`load_library` raises, and if no
+MI355X is visible, :class:`Demodulator` raises DemodError(DEMOD_NO_DEVICE).
+The frame/packing helpers are host byte work and need no GPU.
+
+Load this package by path (the directory name has a hyphen), e.g.
+``importlib.util.spec_from_file_location("audio_network_amd", ".../__init__.py")``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+from typing import Optional, Sequence, Tuple
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libfskdemod.so")
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "demod.h")
+
+DEMOD_OK = 0
+DEMOD_BAD_ARG = -1
+DEMOD_BUFFER_TOO_SMALL = -2
+DEMOD_INTERNAL_ERROR = -3
+DEMOD_INVALID_PACKET = -4
+DEMOD_UNIMPLEMENTED = -5
+DEMOD_INVALID_STATE = -6
+DEMOD_ALLOC_FAIL = -7
+DEMOD_DEVICE_ERROR = -8
+DEMOD_NO_DEVICE = -9
+DEMOD_FRAME_TOO_LARGE = -10
+
+DEMOD_MAX_TONES = 16
+DEMOD_MAX_FRAME_PAYLOAD = 4096
+
+CH_LEFT, CH_RIGHT, CH_DOWNMIX = 0, 1, 2
+METHOD_AUTO, METHOD_GOERTZEL, METHOD_FFT = 0, 1, 2
+
+FSK2_FREQS = (1500.0, 3000.0)                              # SURVEY §8 tone plan
+FSK8_FREQS = tuple(1500.0 + 375.0 * i for i in range(8))
+BENCH_SEED = 0x2C5DA044
+
+
+class DemodCfg(ctypes.Structure):
+    """Mirror of ``demod_cfg_t`` (include/demod.h)."""
+    _fields_ = [
+        ("fs", ctypes.c_double),
+        ("n", ctypes.c_uint32),
+        ("hop", ctypes.c_uint32),
+        ("k", ctypes.c_uint32),
+        ("channels", ctypes.c_uint32),
+        ("channel_mode", ctypes.c_int32),
+        ("device", ctypes.c_int32),
+        ("method", ctypes.c_int32),
+        ("reserved", ctypes.c_uint32),
+        ("freqs", ctypes.c_double * DEMOD_MAX_TONES),
+    ]
+
+
+class DemodError(RuntimeError):
+    def __init__(self, code: int, what: str = ""):
+        self.code = code
+        msg = strerror(code) if _lib is not None else str(code)
+        super().__init__(f"{what}: {msg} ({code})" if what else f"{msg} ({code})")
+
+
+_lib: Optional[ctypes.CDLL] = None
+
+_P = ctypes.c_void_p
+_SZ = ctypes.c_size_t
+
+
+def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load libfskdemod.so (raises FileNotFoundError if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise FileNotFoundError(
+            f"{path} not built: run `make -C audio-network_amd/csrc` "
+            "(or __graft_entry__.build()); there is no CPU fallback")
+    try:
+        # Bind the HIP runtime once: torch ships its own libamdhip64.so.7; if it
+        # is imported after this library, a second runtime would be loaded.
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+    lib = ctypes.CDLL(path)
+    sig = {
+        "demod_cfg_default": (None, [ctypes.POINTER(DemodCfg)]),
+        "demod_create": (_P, [ctypes.POINTER(DemodCfg), ctypes.POINTER(ctypes.c_int)]),
+        "demod_destroy": (None, [_P]),
+        "demod_reset": (ctypes.c_int, [_P]),
+        "demod_pending": (ctypes.c_int, [_P]),
+        "demod_max_symbols": (ctypes.c_int, [_P, _SZ]),
+        "demodulate": (ctypes.c_int, [_P, _P, _SZ, _P, _SZ]),
+        "demodulate_mags": (ctypes.c_int, [_P, _P, _SZ, _P, _P, _SZ]),
+        "demod_batch": (ctypes.c_int, [_P, _P, _SZ, _P, _P]),
+        "demod_batch_async": (ctypes.c_int, [_P, _P, _SZ, _P, _P, _P]),
+        "demod_frame_size": (_SZ, [_SZ]),
+        "demod_frame_encode": (ctypes.c_int, [_P, _SZ, _P, _SZ]),
+        "demod_frame_decode": (ctypes.c_int, [_P, _SZ, ctypes.POINTER(ctypes.c_void_p),
+                                              ctypes.POINTER(_SZ), ctypes.POINTER(_SZ)]),
+        "demod_bits_per_symbol": (ctypes.c_int, [ctypes.c_uint32]),
+        "demod_pack_symbols": (ctypes.c_int, [_P, _SZ, ctypes.c_int, _P, _SZ]),
+        "demod_unpack_symbols": (ctypes.c_int, [_P, _SZ, ctypes.c_int, _P, _SZ]),
+        "demod_frame_symbols": (ctypes.c_longlong, [_P, _SZ, ctypes.c_int, _SZ, _P, _SZ]),
+        "demod_synth_fsk": (ctypes.c_int, [ctypes.POINTER(DemodCfg), ctypes.c_uint64,
+                                           ctypes.c_uint64, _SZ, ctypes.c_int, ctypes.c_int,
+                                           _P, _P, _P]),
+        "demod_strerror": (ctypes.c_char_p, [ctypes.c_int]),
+        "demod_version_string": (ctypes.c_char_p, []),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def header_exports(path: str = HEADER_PATH) -> list:
+    """Function names declared in include/demod.h."""
+    src = open(path).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    names = re.findall(r"\b([a-z_][a-z0-9_]*)\s*\(", src)
+    skip = {"defined", "sizeof"}
+    decl = []
+    for m in re.finditer(r"^[^#\n][^;{}]*?\b([a-z_][a-z0-9_]*)\s*\([^;{}]*\)\s*;", src, flags=re.M):
+        if m.group(1) not in skip:
+            decl.append(m.group(1))
+    return sorted(set(decl)) if decl else sorted(set(names) - skip)
+
+
+def strerror(code: int) -> str:
+    return load_library().demod_strerror(code).decode()
+
+
+def version_string() -> str:
+    return load_library().demod_version_string().decode()
+
+
+def make_cfg(fs: float = 48000.0, n: int = 1024, hop: Optional[int] = None,
+             freqs: Sequence[float] = FSK2_FREQS, channels: int = 1,
+             channel_mode: int = CH_LEFT, device: int = 0,
+             method: int = METHOD_AUTO) -> DemodCfg:
+    cfg = DemodCfg()
+    load_library().demod_cfg_default(ctypes.byref(cfg))
+    cfg.fs = float(fs)
+    cfg.n = int(n)
+    cfg.hop = int(n if hop is None else hop)
+    if len(freqs) > DEMOD_MAX_TONES:
+        raise DemodError(DEMOD_BAD_ARG, "too many tones")
+    cfg.k = len(freqs)
+    cfg.channels = int(channels)
+    cfg.channel_mode = int(channel_mode)
+    cfg.device = int(device)
+    cfg.method = int(method)
+    for i in range(DEMOD_MAX_TONES):
+        cfg.freqs[i] = float(freqs[i]) if i < len(freqs) else 0.0
+    return cfg
+
+
+def _ptr(a) -> int:
+    """Address of a numpy array or a torch tensor (host or device)."""
+    if a is None:
+        return 0
+    if isinstance(a, np.ndarray):
+        return a.ctypes.data
+    return int(a.data_ptr())
+
+
+class Demodulator:
+    """One demod_t handle (not thread-safe within a handle, like libopus)."""
+
+    def __init__(self, cfg: Optional[DemodCfg] = None, **kw):
+        self._lib = load_library()
+        self.cfg = cfg if cfg is not None else make_cfg(**kw)
+        err = ctypes.c_int(0)
+        h = self._lib.demod_create(ctypes.byref(self.cfg), ctypes.byref(err))
+        if not h:
+            raise DemodError(err.value, "demod_create")
+        self._h = h
+
+    @property
+    def k(self) -> int:
+        return int(self.cfg.k)
+
+    @property
+    def n(self) -> int:
+        return int(self.cfg.n)
+
+    @property
+    def hop(self) -> int:
+        return int(self.cfg.hop)
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._lib.demod_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def reset(self) -> None:
+        rc = self._lib.demod_reset(self._h)
+        if rc < 0:
+            raise DemodError(rc, "demod_reset")
+
+    def pending(self) -> int:
+        return int(self._lib.demod_pending(self._h))
+
+    def max_symbols(self, n_frames: int) -> int:
+        return int(self._lib.demod_max_symbols(self._h, n_frames))
+
+    def demodulate(self, pcm: np.ndarray, mags: bool = False, max_symbols: Optional[int] = None):
+        """Streaming demodulate(pcm, n): pcm is int16, interleaved if stereo."""
+        pcm = np.ascontiguousarray(pcm, dtype=np.int16)
+        ch = int(self.cfg.channels)
+        if pcm.size % ch:
+            raise DemodError(DEMOD_BAD_ARG, "pcm length not a multiple of channels")
+        n_frames = pcm.size // ch
+        cap = self.max_symbols(n_frames) if max_symbols is None else int(max_symbols)
+        sym = np.empty(max(cap, 1), dtype=np.uint8)
+        mag = np.empty((max(cap, 1), self.k), dtype=np.float32) if mags else None
+        rc = self._lib.demodulate_mags(self._h, _ptr(pcm), n_frames, _ptr(sym), _ptr(mag), cap)
+        if rc < 0:
+            raise DemodError(rc, "demodulate")
+        return (sym[:rc], mag[:rc]) if mags else sym[:rc]
+
+    def batch(self, pcm, n_windows: Optional[int] = None, mags: bool = False):
+        """Batch hot path on host numpy windows [W][n] (or hop-strided)."""
+        pcm = np.ascontiguousarray(pcm, dtype=np.int16)
+        flat = pcm.reshape(-1)
+        if n_windows is None:
+            if pcm.ndim == 2 and self.hop == self.n:
+                n_windows = pcm.shape[0]
+            else:
+                n_windows = 0 if flat.size < self.n else (flat.size - self.n) // self.hop + 1
+        if n_windows and (n_windows - 1) * self.hop + self.n > flat.size:
+            raise DemodError(DEMOD_BAD_ARG, "pcm shorter than n_windows")
+        buf = flat
+        if flat.ctypes.data % 16:
+            buf = np.empty(flat.size + 8, dtype=np.int16)
+            off = (-buf.ctypes.data % 16) // 2
+            buf = buf[off:off + flat.size]
+            buf[:] = flat
+        sym = np.empty(max(n_windows, 1), dtype=np.uint8)
+        mag = np.empty((max(n_windows, 1), self.k), dtype=np.float32) if mags else None
+        rc = self._lib.demod_batch(self._h, _ptr(buf), n_windows, _ptr(sym), _ptr(mag))
+        if rc < 0:
+            raise DemodError(rc, "demod_batch")
+        return (sym[:rc], mag[:rc]) if mags else sym[:rc]
+
+    def batch_device(self, d_pcm, n_windows: int, d_sym, d_mag=None) -> int:
+        """Synchronous batch on device pointers/tensors."""
+        rc = self._lib.demod_batch(self._h, _ptr(d_pcm), n_windows, _ptr(d_sym), _ptr(d_mag))
+        if rc < 0:
+            raise DemodError(rc, "demod_batch")
+        return rc
+
+    def batch_async(self, d_pcm, n_windows: int, d_sym, d_mag=None, stream: int = 0) -> int:
+        """Enqueue on a HIP stream (raw hipStream_t as int; 0 = handle stream)."""
+        rc = self._lib.demod_batch_async(self._h, _ptr(d_pcm), n_windows, _ptr(d_sym),
+                                         _ptr(d_mag), stream or None)
+        if rc < 0:
+            raise DemodError(rc, "demod_batch_async")
+        return rc
+
+
+def synth_fsk(cfg: DemodCfg, seed: int, n_windows: int, amplitude: int, sigma: int,
+              d_pcm, d_sym=None, stream: int = 0, w0: int = 0) -> None:
+    """Device generator of the seeded FSK test signal into device buffers."""
+    rc = load_library().demod_synth_fsk(ctypes.byref(cfg), ctypes.c_uint64(seed),
+                                         ctypes.c_uint64(w0), n_windows,
+                                         amplitude, sigma, _ptr(d_pcm), _ptr(d_sym),
+                                         stream or None)
+    if rc < 0:
+        raise DemodError(rc, "demod_synth_fsk")
+
+
+# ---- ip.proto framing (host) ---------------------------------------------
+
+def frame_size(payload_len: int) -> int:
+    return int(load_library().demod_frame_size(payload_len))
+
+
+def frame_encode(payload: bytes) -> bytes:
+    lib = load_library()
+    src = (ctypes.c_uint8 * max(len(payload), 1)).from_buffer_copy(payload or b"\0")
+    cap = lib.demod_frame_size(len(payload))
+    out = (ctypes.c_uint8 * cap)()
+    rc = lib.demod_frame_encode(src, len(payload), out, cap)
+    if rc < 0:
+        raise DemodError(rc, "demod_frame_encode")
+    return bytes(out[:rc])
+
+
+def frame_decode(buf: bytes) -> Tuple[bytes, int]:
+    """Decode one delimited ToReceiver frame -> (payload, bytes consumed)."""
+    lib = load_library()
+    src = (ctypes.c_uint8 * max(len(buf), 1)).from_buffer_copy(buf or b"\0")
+    pl = ctypes.c_void_p()
+    pl_len = _SZ()
+    used = _SZ()
+    rc = lib.demod_frame_decode(src, len(buf), ctypes.byref(pl), ctypes.byref(pl_len),
+                                ctypes.byref(used))
+    if rc < 0:
+        raise DemodError(rc, "demod_frame_decode")
+    off = (pl.value or ctypes.addressof(src)) - ctypes.addressof(src)
+    return bytes(buf[off:off + pl_len.value]), int(used.value)
+
+
+def bits_per_symbol(k: int) -> int:
+    return int(load_library().demod_bits_per_symbol(k))
+
+
+def pack_symbols(symbols: np.ndarray, bits: int) -> bytes:
+    sym = np.ascontiguousarray(symbols, dtype=np.uint8)
+    cap = (sym.size * bits + 7) // 8
+    out = np.empty(max(cap, 1), dtype=np.uint8)
+    rc = load_library().demod_pack_symbols(_ptr(sym), sym.size, bits, _ptr(out), cap)
+    if rc < 0:
+        raise DemodError(rc, "demod_pack_symbols")
+    return out[:rc].tobytes()
+
+
+def unpack_symbols(data: bytes, n: int, bits: int) -> np.ndarray:
+    src = np.frombuffer(data, dtype=np.uint8).copy() if data else np.zeros(1, np.uint8)
+    if len(data) * 8 < n * bits:
+        raise DemodError(DEMOD_BAD_ARG, "not enough packed bytes")
+    out = np.empty(max(n, 1), dtype=np.uint8)
+    rc = load_library().demod_unpack_symbols(_ptr(src), n, bits, _ptr(out), n)
+    if rc < 0:
+        raise DemodError(rc, "demod_unpack_symbols")
+    return out[:n]
+
+
+def frame_symbols(symbols: np.ndarray, bits: int,
+                  max_payload: int = DEMOD_MAX_FRAME_PAYLOAD) -> bytes:
+    """Symbols -> consecutive delimited ToReceiver frames (rank-0 framing)."""
+    sym = np.ascontiguousarray(symbols, dtype=np.uint8)
+    per = max_payload * 8 // bits
+    nframes = (sym.size + per - 1) // per
+    cap = nframes * frame_size(max_payload) + 16
+    out = np.empty(cap, dtype=np.uint8)
+    rc = load_library().demod_frame_symbols(_ptr(sym), sym.size, bits, max_payload,
+                                            _ptr(out), cap)
+    if rc < 0:
+        raise DemodError(int(rc), "demod_frame_symbols")
+    return out[:rc].tobytes()
+
+
+def iter_frames(stream: bytes):
+    """Yield payloads of consecutive delimited frames (network.cpp:409-430 loop)."""
+    pos = 0
+    while pos < len(stream):
+        payload, used = frame_decode(stream[pos:])
+        yield payload
+        pos += used

@@ -1,0 +1,439 @@
+// demod_api.cpp — C ABI host layer of libfskdemod.so (include/demod.h).
+//
+// Handle lifecycle mirrors the Opus decoder the reference receiver drives
+// (opus_decoder_create/destroy, hardware/src/playback.cpp:67-74); streaming
+// intake mirrors the per-packet call at playback.cpp:115-122, where
+// demodulate(pcm, nSamplesDecoded) would consume opus_decode's output.
+// Errors are returned (no abort(), unlike OPUS_ERROR_CHECK playback.cpp:16-22).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "../../include/demod.h"
+#include "demod_internal.h"
+
+using namespace fskd;
+
+struct demod {
+    demod_cfg_t cfg;
+    int device = 0;
+    int cus = 0;
+    int log2g = 0;
+    hipStream_t stream = nullptr;
+    float4 *d_rot = nullptr;    // [k][g]
+    float coef[kMaxTones] = {};
+    // staging for host-pointer calls
+    int16_t *d_in = nullptr;
+    size_t d_in_cap = 0;        // samples
+    uint8_t *d_sym = nullptr;
+    float *d_mag = nullptr;
+    size_t d_out_cap = 0;       // windows
+    int16_t *h_in = nullptr;    // pinned
+    size_t h_in_cap = 0;
+    uint8_t *h_sym = nullptr;   // pinned
+    float *h_mag = nullptr;     // pinned
+    size_t h_out_cap = 0;
+    // streaming carry (mono samples not yet consumed by a complete window)
+    std::vector<int16_t> carry;
+    std::vector<int16_t> scratch;
+    // synth
+    int16_t *d_lut = nullptr;
+};
+
+#define HIP_TRY(x)                                                 \
+    do {                                                           \
+        hipError_t _e = (x);                                       \
+        if (_e != hipSuccess) {                                    \
+            std::fprintf(stderr, "fskdemod: %s failed: %s\n", #x,  \
+                         hipGetErrorString(_e));                   \
+            return DEMOD_DEVICE_ERROR;                             \
+        }                                                          \
+    } while (0)
+
+extern "C" {
+
+void demod_cfg_default(demod_cfg_t *cfg)
+{
+    if (!cfg) return;
+    std::memset(cfg, 0, sizeof(*cfg));
+    cfg->fs = 48000.0;
+    cfg->n = 1024;
+    cfg->hop = 1024;
+    cfg->k = 2;
+    cfg->channels = 1;
+    cfg->channel_mode = DEMOD_CH_LEFT;
+    cfg->device = 0;
+    cfg->method = DEMOD_METHOD_AUTO;
+    cfg->freqs[0] = 1500.0;
+    cfg->freqs[1] = 3000.0;
+}
+
+static int validate(const demod_cfg_t *c)
+{
+    if (!c) return DEMOD_BAD_ARG;
+    if (!(c->fs > 0.0) || !std::isfinite(c->fs)) return DEMOD_BAD_ARG;
+    if (c->k < 1 || c->k > DEMOD_MAX_TONES) return DEMOD_BAD_ARG;
+    // Goertzel tiles: n = 64 * 2^j, 64 <= n <= 4096
+    if (c->n < 64 || c->n > 4096 || (c->n & (c->n - 1))) return DEMOD_BAD_ARG;
+    if (c->hop < 8 || c->hop > c->n || (c->hop % 8)) return DEMOD_BAD_ARG;
+    if (c->channels != 1 && c->channels != 2) return DEMOD_BAD_ARG;
+    if (c->channels == 2 && (c->channel_mode < 0 || c->channel_mode > 2)) return DEMOD_BAD_ARG;
+    if (c->method != DEMOD_METHOD_AUTO && c->method != DEMOD_METHOD_GOERTZEL)
+        return DEMOD_UNIMPLEMENTED;
+    if (c->reserved != 0) return DEMOD_BAD_ARG;
+    for (uint32_t i = 0; i < c->k; ++i)
+        if (!std::isfinite(c->freqs[i]) || c->freqs[i] < 0.0 || c->freqs[i] > c->fs / 2)
+            return DEMOD_BAD_ARG;
+    return DEMOD_OK;
+}
+
+static int init_device_state(demod_t *st)
+{
+    const demod_cfg_t &c = st->cfg;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+        (void)hipGetLastError();
+        return DEMOD_NO_DEVICE;
+    }
+    if (c.device < 0 || c.device >= ndev) return DEMOD_NO_DEVICE;
+    HIP_TRY(hipSetDevice(c.device));
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, c.device));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+        std::fprintf(stderr, "fskdemod: device %d is %s, need gfx950 (MI355X)\n",
+                     c.device, prop.gcnArchName);
+        return DEMOD_NO_DEVICE;
+    }
+    st->device = c.device;
+    st->cus = prop.multiProcessorCount;
+    HIP_TRY(hipStreamCreateWithFlags(&st->stream, hipStreamNonBlocking));
+
+    int g = (int)(c.n / 64), lg = 0;
+    while ((1 << lg) < g) ++lg;
+    st->log2g = lg;
+    // Rotation of each lane segment j (samples [64j, 64j+64)) into window phase:
+    // A = e^{-jw(64j+63)}, B = e^{-jw(64j+64)}; X += A s1 - B s2.
+    std::vector<float4> rot((size_t)c.k * g);
+    for (uint32_t k = 0; k < c.k; ++k) {
+        const double w = 2.0 * M_PI * c.freqs[k] / c.fs;
+        st->coef[k] = (float)(2.0 * std::cos(w));
+        for (int j = 0; j < g; ++j) {
+            const double a = -w * (64.0 * j + 63.0), b = -w * (64.0 * j + 64.0);
+            rot[(size_t)k * g + j] = make_float4((float)std::cos(a), (float)std::sin(a),
+                                                 (float)std::cos(b), (float)std::sin(b));
+        }
+    }
+    HIP_TRY(hipMalloc(&st->d_rot, rot.size() * sizeof(float4)));
+    HIP_TRY(hipMemcpy(st->d_rot, rot.data(), rot.size() * sizeof(float4), hipMemcpyHostToDevice));
+    return DEMOD_OK;
+}
+
+static void free_state(demod_t *st)
+{
+    if (st->stream) (void)hipStreamSynchronize(st->stream);
+    if (st->d_rot) (void)hipFree(st->d_rot);
+    if (st->d_in) (void)hipFree(st->d_in);
+    if (st->d_sym) (void)hipFree(st->d_sym);
+    if (st->d_mag) (void)hipFree(st->d_mag);
+    if (st->h_in) (void)hipHostFree(st->h_in);
+    if (st->h_sym) (void)hipHostFree(st->h_sym);
+    if (st->h_mag) (void)hipHostFree(st->h_mag);
+    if (st->d_lut) (void)hipFree(st->d_lut);
+    if (st->stream) (void)hipStreamDestroy(st->stream);
+}
+
+demod_t *demod_create(const demod_cfg_t *cfg, int *error)
+{
+    int rc = validate(cfg);
+    if (rc != DEMOD_OK) {
+        if (error) *error = rc;
+        return nullptr;
+    }
+    demod_t *st = new (std::nothrow) demod();
+    if (!st) {
+        if (error) *error = DEMOD_ALLOC_FAIL;
+        return nullptr;
+    }
+    st->cfg = *cfg;
+    rc = init_device_state(st);
+    if (rc != DEMOD_OK) {
+        free_state(st);
+        delete st;
+        if (error) *error = rc;
+        return nullptr;
+    }
+    st->carry.reserve(cfg->n);
+    if (error) *error = DEMOD_OK;
+    return st;
+}
+
+void demod_destroy(demod_t *st)
+{
+    if (!st) return;
+    (void)hipSetDevice(st->device);
+    free_state(st);
+    delete st;
+}
+
+int demod_reset(demod_t *st)
+{
+    if (!st) return DEMOD_BAD_ARG;
+    st->carry.clear();
+    return DEMOD_OK;
+}
+
+int demod_pending(const demod_t *st)
+{
+    if (!st) return DEMOD_BAD_ARG;
+    return (int)st->carry.size();
+}
+
+static size_t windows_for(const demod_t *st, size_t total)
+{
+    if (total < st->cfg.n) return 0;
+    return (total - st->cfg.n) / st->cfg.hop + 1;
+}
+
+int demod_max_symbols(const demod_t *st, size_t n_frames)
+{
+    if (!st) return DEMOD_BAD_ARG;
+    size_t w = windows_for(st, st->carry.size() + n_frames);
+    return w > 0x7FFFFFFF ? 0x7FFFFFFF : (int)w;
+}
+
+// Enqueue the Goertzel kernel on device-resident windows.
+static int enqueue_batch(demod_t *st, const int16_t *d_pcm, size_t n_windows, uint8_t *d_sym,
+                         float *d_mag, hipStream_t s)
+{
+    if (n_windows == 0) return 0;
+    GoertzelParams p;
+    std::memset(&p, 0, sizeof(p));
+    p.pcm = d_pcm;
+    p.n_windows = (long long)n_windows;
+    p.hop = st->cfg.hop;
+    p.log2g = st->log2g;
+    p.k = (int)st->cfg.k;
+    p.rot = st->d_rot;
+    p.sym = d_sym;
+    p.mag = d_mag;
+    for (uint32_t k = 0; k < st->cfg.k; ++k) p.coef[k] = st->coef[k];
+    const int grid = goertzel_grid(p.k, p.n_windows, p.log2g, st->device, st->cus);
+    HIP_TRY(launch_goertzel(p, grid, s));
+    return (int)n_windows;
+}
+
+static int ensure_dev(demod_t *st, size_t samples, size_t windows, bool mags)
+{
+    if (samples > st->d_in_cap) {
+        if (st->d_in) (void)hipFree(st->d_in);
+        st->d_in = nullptr;
+        st->d_in_cap = 0;
+        size_t cap = samples + samples / 4 + 64;
+        HIP_TRY(hipMalloc(&st->d_in, cap * sizeof(int16_t)));
+        st->d_in_cap = cap;
+    }
+    if (windows > st->d_out_cap || (mags && !st->d_mag)) {
+        if (st->d_sym) (void)hipFree(st->d_sym);
+        if (st->d_mag) (void)hipFree(st->d_mag);
+        st->d_sym = nullptr;
+        st->d_mag = nullptr;
+        st->d_out_cap = 0;
+        size_t cap = windows + windows / 4 + 16;
+        HIP_TRY(hipMalloc(&st->d_sym, cap));
+        HIP_TRY(hipMalloc(&st->d_mag, cap * st->cfg.k * sizeof(float)));
+        st->d_out_cap = cap;
+    }
+    return DEMOD_OK;
+}
+
+static int ensure_host(demod_t *st, size_t samples, size_t windows)
+{
+    if (samples > st->h_in_cap) {
+        if (st->h_in) (void)hipHostFree(st->h_in);
+        st->h_in = nullptr;
+        st->h_in_cap = 0;
+        size_t cap = samples + samples / 4 + 64;
+        HIP_TRY(hipHostMalloc(&st->h_in, cap * sizeof(int16_t), hipHostMallocDefault));
+        st->h_in_cap = cap;
+    }
+    if (windows > st->h_out_cap) {
+        if (st->h_sym) (void)hipHostFree(st->h_sym);
+        if (st->h_mag) (void)hipHostFree(st->h_mag);
+        st->h_sym = nullptr;
+        st->h_mag = nullptr;
+        st->h_out_cap = 0;
+        size_t cap = windows + windows / 4 + 16;
+        HIP_TRY(hipHostMalloc(&st->h_sym, cap, hipHostMallocDefault));
+        HIP_TRY(hipHostMalloc(&st->h_mag, cap * st->cfg.k * sizeof(float), hipHostMallocDefault));
+        st->h_out_cap = cap;
+    }
+    return DEMOD_OK;
+}
+
+static bool is_device_ptr(const void *p)
+{
+    if (!p) return false;
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged;
+}
+
+// Host samples [n_samples] -> device, kernel, results -> host (synchronous).
+static int run_host(demod_t *st, const int16_t *pcm, size_t n_samples, size_t n_windows,
+                    uint8_t *symbols, float *mags)
+{
+    int rc;
+    if ((rc = ensure_dev(st, n_samples, n_windows, mags != nullptr)) != DEMOD_OK) return rc;
+    if ((rc = ensure_host(st, n_samples, n_windows)) != DEMOD_OK) return rc;
+    std::memcpy(st->h_in, pcm, n_samples * sizeof(int16_t));
+    HIP_TRY(hipMemcpyAsync(st->d_in, st->h_in, n_samples * sizeof(int16_t),
+                           hipMemcpyHostToDevice, st->stream));
+    rc = enqueue_batch(st, st->d_in, n_windows, st->d_sym, mags ? st->d_mag : nullptr, st->stream);
+    if (rc < 0) return rc;
+    HIP_TRY(hipMemcpyAsync(st->h_sym, st->d_sym, n_windows, hipMemcpyDeviceToHost, st->stream));
+    if (mags)
+        HIP_TRY(hipMemcpyAsync(st->h_mag, st->d_mag, n_windows * st->cfg.k * sizeof(float),
+                               hipMemcpyDeviceToHost, st->stream));
+    HIP_TRY(hipStreamSynchronize(st->stream));
+    std::memcpy(symbols, st->h_sym, n_windows);
+    if (mags) std::memcpy(mags, st->h_mag, n_windows * st->cfg.k * sizeof(float));
+    return (int)n_windows;
+}
+
+int demod_batch(demod_t *st, const int16_t *pcm, size_t n_windows, uint8_t *symbols, float *mags)
+{
+    if (!st || (!pcm && n_windows) || (!symbols && n_windows)) return DEMOD_BAD_ARG;
+    if (n_windows > 0x7FFFFFFF) return DEMOD_BAD_ARG;
+    if (n_windows == 0) return 0;
+    if (((uintptr_t)pcm & 15) != 0) return DEMOD_BAD_ARG;
+    HIP_TRY(hipSetDevice(st->device));
+    const size_t n_samples = (n_windows - 1) * st->cfg.hop + st->cfg.n;
+    const bool din = is_device_ptr(pcm), dsym = is_device_ptr(symbols);
+    const bool dmag = mags ? is_device_ptr(mags) : dsym;
+    if (din && dsym && dmag) {
+        int rc = enqueue_batch(st, pcm, n_windows, symbols, mags, st->stream);
+        if (rc < 0) return rc;
+        HIP_TRY(hipStreamSynchronize(st->stream));
+        return rc;
+    }
+    if (!din && !dsym && !dmag) return run_host(st, pcm, n_samples, n_windows, symbols, mags);
+    return DEMOD_BAD_ARG;  // mixed host/device pointers
+}
+
+int demod_batch_async(demod_t *st, const int16_t *d_pcm, size_t n_windows, uint8_t *d_symbols,
+                      float *d_mags, void *stream)
+{
+    if (!st || (!d_pcm && n_windows) || (!d_symbols && n_windows)) return DEMOD_BAD_ARG;
+    if (n_windows > 0x7FFFFFFF) return DEMOD_BAD_ARG;
+    if (((uintptr_t)d_pcm & 15) != 0) return DEMOD_BAD_ARG;
+    hipStream_t s = stream ? (hipStream_t)stream : st->stream;
+    return enqueue_batch(st, d_pcm, n_windows, d_symbols, d_mags, s);
+}
+
+int demodulate_mags(demod_t *st, const int16_t *pcm, size_t n_frames, uint8_t *symbols,
+                    float *mags, size_t max_symbols)
+{
+    if (!st || (!pcm && n_frames)) return DEMOD_BAD_ARG;
+    const demod_cfg_t &c = st->cfg;
+    const size_t have = st->carry.size();
+    const size_t total = have + n_frames;
+    const size_t W = windows_for(st, total);
+    if (W > max_symbols) return DEMOD_BUFFER_TOO_SMALL;
+    if (W && !symbols) return DEMOD_BAD_ARG;
+    if (W > 0x7FFFFFFF) return DEMOD_BAD_ARG;
+    // Mono view: carried samples followed by the new frames' selected channel.
+    std::vector<int16_t> &m = st->scratch;
+    m.resize(total);
+    if (have) std::memcpy(m.data(), st->carry.data(), have * sizeof(int16_t));
+    int16_t *dst = m.data() + have;
+    if (c.channels == 1) {
+        if (n_frames) std::memcpy(dst, pcm, n_frames * sizeof(int16_t));
+    } else if (c.channel_mode == DEMOD_CH_DOWNMIX) {
+        for (size_t i = 0; i < n_frames; ++i)
+            dst[i] = (int16_t)(((int32_t)pcm[2 * i] + (int32_t)pcm[2 * i + 1]) >> 1);
+    } else {
+        const int ch = c.channel_mode == DEMOD_CH_RIGHT ? 1 : 0;
+        for (size_t i = 0; i < n_frames; ++i) dst[i] = pcm[2 * i + ch];
+    }
+    if (W) {
+        HIP_TRY(hipSetDevice(st->device));
+        const size_t used = (W - 1) * c.hop + c.n;
+        int rc = run_host(st, m.data(), used, W, symbols, mags);
+        if (rc < 0) return rc;  // nothing consumed on failure
+    }
+    const size_t consumed = W * c.hop;
+    st->carry.assign(m.begin() + consumed, m.end());
+    return (int)W;
+}
+
+int demodulate(demod_t *st, const int16_t *pcm, size_t n_frames, uint8_t *symbols,
+               size_t max_symbols)
+{
+    return demodulate_mags(st, pcm, n_frames, symbols, nullptr, max_symbols);
+}
+
+int demod_synth_fsk(const demod_cfg_t *cfg, uint64_t seed, uint64_t w0, size_t n_windows,
+                    int amplitude, int sigma, int16_t *d_pcm, uint8_t *d_symbols, void *stream)
+{
+    if (!cfg || cfg->k < 1 || cfg->k > DEMOD_MAX_TONES || cfg->n < 8 || (cfg->n % 8)) return DEMOD_BAD_ARG;
+    if (!(cfg->fs > 0.0) || !d_pcm || ((uintptr_t)d_pcm & 15)) return DEMOD_BAD_ARG;
+    if (amplitude < 0 || amplitude > 32767 || sigma < 0 || sigma > 32767) return DEMOD_BAD_ARG;
+    if (n_windows == 0) return DEMOD_OK;
+    static int16_t *d_lut[64] = {nullptr};
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    if (dev < 0 || dev >= 64) return DEMOD_BAD_ARG;
+    if (!d_lut[dev]) {
+        std::vector<int16_t> lut(16384);
+        for (int i = 0; i < 16384; ++i)
+            lut[i] = (int16_t)std::lrint(32767.0 * std::sin(2.0 * M_PI * (double)i / 16384.0));
+        HIP_TRY(hipMalloc(&d_lut[dev], lut.size() * sizeof(int16_t)));
+        HIP_TRY(hipMemcpy(d_lut[dev], lut.data(), lut.size() * sizeof(int16_t), hipMemcpyHostToDevice));
+    }
+    SynthParams p;
+    std::memset(&p, 0, sizeof(p));
+    p.seed = seed;
+    p.w0 = w0;
+    p.n_windows = (long long)n_windows;
+    p.n = (int)cfg->n;
+    p.k = (int)cfg->k;
+    p.amplitude = amplitude;
+    p.sigma = sigma;
+    p.lut = d_lut[dev];
+    p.pcm = d_pcm;
+    p.sym = d_symbols;
+    for (uint32_t t = 0; t < cfg->k; ++t)
+        p.inc[t] = (uint32_t)((unsigned long long)std::llround(cfg->freqs[t] / cfg->fs * 4294967296.0) &
+                              0xFFFFFFFFULL);
+    HIP_TRY(launch_synth(p, (hipStream_t)stream));
+    return DEMOD_OK;
+}
+
+const char *demod_strerror(int error)
+{
+    switch (error) {
+    case DEMOD_OK: return "success";
+    case DEMOD_BAD_ARG: return "invalid argument";
+    case DEMOD_BUFFER_TOO_SMALL: return "buffer too small";
+    case DEMOD_INTERNAL_ERROR: return "internal error";
+    case DEMOD_INVALID_PACKET: return "corrupted frame";
+    case DEMOD_UNIMPLEMENTED: return "request not implemented";
+    case DEMOD_INVALID_STATE: return "invalid state";
+    case DEMOD_ALLOC_FAIL: return "memory allocation failed";
+    case DEMOD_DEVICE_ERROR: return "HIP device error";
+    case DEMOD_NO_DEVICE: return "no gfx950 (MI355X) device available";
+    case DEMOD_FRAME_TOO_LARGE: return "encoded frame exceeds max size";
+    default: return "unknown error";
+    }
+}
+
+const char *demod_version_string(void) { return "fskdemod 0.1.0 (gfx950 HIP)"; }
+
+}  // extern "C"

@@ -1,0 +1,213 @@
+// goertzel.hip — per-window Goertzel tone bank, |X_k|^2 and argmax on gfx950.
+//
+// The north-star hot path. The reference has no such
+// kernel; the math restates the textbook recurrence that
+// oracle/fsk_oracle.c:goertzel_window_d evaluates sequentially in double.
+//
+// Work decomposition:
+//   * a wave owns a TILE of 64 lane-segments x 64 samples (8 KiB of int16);
+//     a window of n = 64*G samples spans G consecutive lanes, so one tile
+//     holds 64/G windows (4 at n = 1024);
+//   * the tile is read from HBM with coalesced 16 B/lane non-temporal buffer
+//     loads (8 x 1 KiB per wave; the per-tile descriptor's record count
+//     bounds the last tile), prefetched one tile ahead in registers, then
+//     transposed through a wave-private LDS slice (segment stride 144 B, so
+//     every ds_read_b128 lane group hits 16 distinct bank slots);
+//   * each lane runs the Goertzel recurrence over its own 64 contiguous
+//     samples for all K tones (K independent chains interleave in the VALU);
+//   * the segment's partial DFT is rotated into window phase,
+//       X_k += A_seg s1 - B_seg s2,  A = e^{-jw(n0+63)}, B = e^{-jw(n0+64)},
+//     and summed over the G lanes of the window with DPP row operations;
+//   * every lane of the window then holds X_k; P_k = Re^2 + Im^2, argmax with
+//     ties to the lowest k, one lane stores the symbol, lanes store P_k.
+// 64-sample chains keep the fp32 error <= ~3e-6 of max_k P (a single
+// 1024-sample chain reaches ~2e-5, over the 1e-5 bar).
+#include "demod_internal.h"
+
+namespace fskd {
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v)
+{
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+
+// Sum over aligned groups of 2^log2g lanes; every lane of a group gets the
+// bit-identical total (each step adds the same two operands in both lanes).
+__device__ __forceinline__ float group_sum(float v, int log2g)
+{
+    if (log2g > 0) v += dpp_f<0xB1>(v);   // quad_perm [1,0,3,2]: lane ^ 1
+    if (log2g > 1) v += dpp_f<0x4E>(v);   // quad_perm [2,3,0,1]: lane ^ 2
+    if (log2g > 2) v += dpp_f<0x141>(v);  // row_half_mirror: other quad of the 8
+    if (log2g > 3) v += dpp_f<0x140>(v);  // row_mirror: other half of the row
+    if (log2g > 4) v += __shfl_xor(v, 16);
+    if (log2g > 5) v += __shfl_xor(v, 32);
+    return v;
+}
+
+// LOG2G >= 0: lane-group size fixed at compile time (4 <=> n = 1024);
+// LOG2G == -1: taken from p.log2g at run time.
+template <int K, int LOG2G>
+__global__ __launch_bounds__(256) void goertzel_tile_kernel(GoertzelParams p)
+{
+    __shared__ __attribute__((aligned(16))) unsigned char lds[kWavesPerBlock * kLdsWaveBytes];
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    unsigned char *wl = lds + wave * kLdsWaveBytes;
+    const int log2g = LOG2G >= 0 ? LOG2G : p.log2g;
+    const int g = 1 << log2g;
+    const int n = 64 << log2g;
+    const int seg = lane & (g - 1);          // segment index inside the window
+    const int win_in_tile = lane >> log2g;
+    const long long wins_per_tile = 64 >> log2g;
+    const long long n_tiles = (p.n_windows + wins_per_tile - 1) / wins_per_tile;
+
+    float4 r[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) r[k] = p.rot[k * g + seg];
+
+    // Byte offset (from the tile's first window) of this lane's 16-byte chunk
+    // i: chunk q = 64 i + lane is chunk (q mod 8G) of tile window q / 8G.
+    const int cpw_log2 = 3 + log2g;
+    int goff[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int q = 64 * i + lane;
+        goff[i] = (int)(((long long)(q >> cpw_log2) * p.hop +
+                         (long long)(q & ((1 << cpw_log2) - 1)) * 8) * 2);
+    }
+    // LDS write slot of chunk i: segment 8i + lane/8, chunk lane%8
+    const int wr_off = (lane >> 3) * kLdsSegStride + (lane & 7) * 16;
+    const int rd_off = lane * kLdsSegStride;
+
+    const long long stride = (long long)gridDim.x * kWavesPerBlock;
+    long long t = (long long)blockIdx.x * kWavesPerBlock + wave;
+
+    auto load_tile = [&](long long tt, u32x4 v[8]) {
+        const long long wbase = tt * wins_per_tile;
+        const long long left = p.n_windows - wbase;  // >= 1
+        long long bytes = ((left - 1) * p.hop + n) * 2;
+        if (bytes > 0x7FFFFFF0LL) bytes = 0x7FFFFFF0LL;
+        __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)(p.pcm + wbase * p.hop), (short)0, (int)bytes, 0x00020000);
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            v[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, goff[i], 0, 2 /*nt*/);
+    };
+
+    u32x4 v[8];
+    if (t < n_tiles) load_tile(t, v);
+
+    for (; t < n_tiles; t += stride) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            *reinterpret_cast<u32x4 *>(wl + wr_off + i * 8 * kLdsSegStride) = v[i];
+        const long long tn = t + stride;
+        if (tn < n_tiles) load_tile(tn, v);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+        float s1[K], s2[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) { s1[k] = 0.f; s2[k] = 0.f; }
+
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const u32x4 sj = *reinterpret_cast<const u32x4 *>(wl + rd_off + j * 16);
+            const uint32_t d4[4] = {sj.x, sj.y, sj.z, sj.w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t d = d4[q];
+                const float x0 = (float)(int)(short)(d & 0xFFFFu);
+                const float x1 = (float)((int)d >> 16);
+#pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    const float a = fmaf(p.coef[k], s1[k], x0 - s2[k]);
+                    s2[k] = s1[k];
+                    s1[k] = a;
+                }
+#pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    const float a = fmaf(p.coef[k], s1[k], x1 - s2[k]);
+                    s2[k] = s1[k];
+                    s1[k] = a;
+                }
+            }
+        }
+
+        float best = -1.f;
+        int arg = 0;
+        float P[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            float re = r[k].x * s1[k] - r[k].z * s2[k];
+            float im = r[k].y * s1[k] - r[k].w * s2[k];
+            re = group_sum(re, log2g);
+            im = group_sum(im, log2g);
+            P[k] = fmaf(re, re, im * im);
+            if (P[k] > best) { best = P[k]; arg = k; }
+        }
+
+        const long long w = t * wins_per_tile + win_in_tile;
+        if (w < p.n_windows) {
+            if (seg == 0) p.sym[w] = (uint8_t)arg;
+            if (p.mag) {
+#pragma unroll
+                for (int k = 0; k < K; ++k)
+                    if ((k & (g - 1)) == seg) p.mag[w * K + k] = P[k];
+            }
+        }
+    }
+}
+
+template <int K>
+static const void *kernel_for(int log2g)
+{
+    if (log2g == 4) return reinterpret_cast<const void *>(&goertzel_tile_kernel<K, 4>);
+    return reinterpret_cast<const void *>(&goertzel_tile_kernel<K, -1>);
+}
+
+static const void *kernel_ptr(int k, int log2g)
+{
+    switch (k) {
+#define FSKD_CASE(K) case K: return kernel_for<K>(log2g);
+        FSKD_CASE(1) FSKD_CASE(2) FSKD_CASE(3) FSKD_CASE(4)
+        FSKD_CASE(5) FSKD_CASE(6) FSKD_CASE(7) FSKD_CASE(8)
+        FSKD_CASE(9) FSKD_CASE(10) FSKD_CASE(11) FSKD_CASE(12)
+        FSKD_CASE(13) FSKD_CASE(14) FSKD_CASE(15) FSKD_CASE(16)
+#undef FSKD_CASE
+    default: return nullptr;
+    }
+}
+
+int goertzel_grid(int k, long long n_windows, int log2g, int device, int device_cus)
+{
+    const long long wins_per_tile = 64 >> log2g;
+    const long long n_tiles = (n_windows + wins_per_tile - 1) / wins_per_tile;
+    long long blocks = (n_tiles + kWavesPerBlock - 1) / kWavesPerBlock;
+    // Persistent grid: exactly the co-resident blocks, so no block waits for
+    // a second dispatch round (that tail would cost a whole extra pass).
+    int per_cu = 0;
+    const void *f = kernel_ptr(k, log2g);
+    (void)device;
+    if (!f || hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, 64 * kWavesPerBlock, 0) !=
+                  hipSuccess || per_cu < 1)
+        per_cu = 1;
+    const long long cap = (long long)device_cus * per_cu;
+    if (blocks > cap) blocks = cap;
+    if (blocks < 1) blocks = 1;
+    return (int)blocks;
+}
+
+hipError_t launch_goertzel(const GoertzelParams &p, int grid, hipStream_t s)
+{
+    const void *f = kernel_ptr(p.k, p.log2g);
+    if (!f) return hipErrorInvalidValue;
+    void *args[] = {const_cast<GoertzelParams *>(&p)};
+    return hipLaunchKernel(f, dim3(grid), dim3(64 * kWavesPerBlock), args, 0, s);
+}
+
+}  // namespace fskd

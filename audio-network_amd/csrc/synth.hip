@@ -1,0 +1,67 @@
+// synth.hip — device generator of the seeded FSK test signal.
+//
+// Same integer-exact function as oracle/fsk_oracle.c:oracle_synth_fsk
+// (DESIGN.md §Synthetic input), evaluated 8 samples per thread: splitmix64 is
+// counter-based, so any sample is generated independently and the bytes are
+// identical to the CPU generator's (tests/test_gpu_parity.py checks this).
+#include "demod_internal.h"
+
+namespace fskd {
+
+__device__ __forceinline__ uint64_t mix64(uint64_t z)
+{
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(256) void synth_kernel(SynthParams p)
+{
+    const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long long total8 = p.n_windows * (long long)p.n / 8;
+    if (gid >= total8) return;
+    const long long base = gid * 8;
+    const long long w = base / p.n;
+    const int s0 = (int)(base - w * p.n);
+    const uint64_t gamma = 0x9E3779B97F4A7C15ULL;
+    const uint64_t rw = mix64(p.seed + (p.w0 + (uint64_t)w + 1) * gamma);
+    const uint32_t sym = (uint32_t)(((rw >> 32) * (uint64_t)p.k) >> 32);
+    const uint32_t phase0 = (uint32_t)rw;
+    const uint64_t ns = mix64(rw ^ 0xA0761D6478BD642FULL);
+    uint32_t inc = 0;
+#pragma unroll
+    for (int t = 0; t < kMaxTones; ++t)
+        if ((uint32_t)t == sym) inc = p.inc[t];
+
+    int16_t out[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+        const uint32_t s = (uint32_t)(s0 + r);
+        const uint32_t ph = phase0 + s * inc;
+        const int32_t tone = (p.amplitude * (int32_t)p.lut[ph >> 18] + 16384) >> 15;
+        const uint64_t d = mix64(ns + ((uint64_t)s + 1) * gamma);
+        const int64_t u = (int64_t)((d & 0xFFFF) + ((d >> 16) & 0xFFFF) +
+                                    ((d >> 32) & 0xFFFF) + (d >> 48));
+        const int64_t noise = ((u - 131070) * (int64_t)p.sigma * 113512) >> 32;
+        int64_t v = (int64_t)tone + noise;
+        v = v > 32767 ? 32767 : (v < -32768 ? -32768 : v);
+        out[r] = (int16_t)v;
+    }
+    uint4 pk;
+    pk.x = (uint16_t)out[0] | ((uint32_t)(uint16_t)out[1] << 16);
+    pk.y = (uint16_t)out[2] | ((uint32_t)(uint16_t)out[3] << 16);
+    pk.z = (uint16_t)out[4] | ((uint32_t)(uint16_t)out[5] << 16);
+    pk.w = (uint16_t)out[6] | ((uint32_t)(uint16_t)out[7] << 16);
+    *reinterpret_cast<uint4 *>(p.pcm + base) = pk;
+    if (s0 == 0 && p.sym) p.sym[w] = (uint8_t)sym;
+}
+
+hipError_t launch_synth(const SynthParams &p, hipStream_t s)
+{
+    const long long total8 = p.n_windows * (long long)p.n / 8;
+    const long long blocks = (total8 + 255) / 256;
+    hipLaunchKernelGGL(synth_kernel, dim3((unsigned)blocks), dim3(256), 0, s, p);
+    return hipGetLastError();
+}
+
+}  // namespace fskd

@@ -1,0 +1,186 @@
+/*
+ * demod.h — C ABI of the MI355X acoustic-FSK demodulator (libfskdemod.so).
+ *
+ * This is the drop-in boundary for the north-star path.
+ * The reference (tmarsteel/audio-network) has no demodulator; every entry
+ * point below mirrors the shape of the C API that sits at the insertion
+ * point in the reference receiver, right after `opus_decode`
+ * (hardware/src/playback.cpp:118):
+ *
+ *   - an opaque handle created/destroyed like an Opus decoder
+ *       opus_decoder_create / opus_decoder_destroy
+ *       (hardware/lib/libopus/src/opus.h:423,512; playback.cpp:67-74);
+ *   - caller-owned buffers, `int` return = count on success or a negative
+ *     error code (opus_decode, opus.h:462; codes opus_defines.h:46-60);
+ *   - errors are returned, never abort()ed (the reference call site aborts
+ *     via OPUS_ERROR_CHECK, playback.cpp:16-22 — deliberately not copied);
+ *   - frame bytes follow protocol/ip.proto:32-36,63-65 (ToReceiver{AudioData})
+ *     with the varint32 length prefix of nanopb pb_encode_delimited /
+ *     protobuf-java writeDelimitedTo (network.cpp:389-403,411;
+ *     transmitter protobuf_async.kt:69-80,110-114).
+ *
+ * Threading: re-entrant across handles, not within one handle (one handle
+ * serves one consumer, like the single playback task, playback.cpp:157-165).
+ *
+ * Every compute entry point runs on the GPU (HIP, gfx950). There is no CPU
+ * fallback: without a visible MI355X, demod_create() fails with
+ * DEMOD_NO_DEVICE. The framing / packing helpers are pure host byte work.
+ */
+#ifndef FSKDEMOD_DEMOD_H
+#define FSKDEMOD_DEMOD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- error codes (same numbering as opus_defines.h:46-60 where they overlap) */
+#define DEMOD_OK                 0
+#define DEMOD_BAD_ARG           -1  /* OPUS_BAD_ARG */
+#define DEMOD_BUFFER_TOO_SMALL  -2  /* OPUS_BUFFER_TOO_SMALL */
+#define DEMOD_INTERNAL_ERROR    -3  /* OPUS_INTERNAL_ERROR */
+#define DEMOD_INVALID_PACKET    -4  /* OPUS_INVALID_PACKET: malformed frame bytes */
+#define DEMOD_UNIMPLEMENTED     -5  /* OPUS_UNIMPLEMENTED */
+#define DEMOD_INVALID_STATE     -6  /* OPUS_INVALID_STATE */
+#define DEMOD_ALLOC_FAIL        -7  /* OPUS_ALLOC_FAIL */
+#define DEMOD_DEVICE_ERROR      -8  /* a HIP runtime call failed */
+#define DEMOD_NO_DEVICE         -9  /* no gfx950 device visible */
+#define DEMOD_FRAME_TOO_LARGE  -10  /* payload > max encoded frame (network.cpp:24,223) */
+
+#define DEMOD_MAX_TONES         16
+#define DEMOD_MAX_FRAME_PAYLOAD 4096 /* MAX_ENCODED_FRAME_SIZE, network.cpp:24 */
+
+/* channel handling for interleaved input (channels == 2) */
+#define DEMOD_CH_LEFT     0   /* use channel 0 */
+#define DEMOD_CH_RIGHT    1   /* use channel 1 */
+#define DEMOD_CH_DOWNMIX  2   /* x = (L + R) >> 1 (arithmetic shift) */
+
+/* detector selection */
+#define DEMOD_METHOD_AUTO      0 /* GOERTZEL (plain tone bank) */
+#define DEMOD_METHOD_GOERTZEL  1 /* per-window Goertzel tone bank */
+#define DEMOD_METHOD_FFT       2 /* full-spectrum N-point real FFT, argmax over tone bins */
+
+typedef struct demod_cfg {
+    double   fs;                     /* sample rate, Hz (48000) */
+    uint32_t n;                      /* window length N in samples (1024) */
+    uint32_t hop;                    /* window advance; == n for non-overlapping */
+    uint32_t k;                      /* number of tones, 1..DEMOD_MAX_TONES */
+    uint32_t channels;               /* 1 = mono, 2 = interleaved stereo */
+    int32_t  channel_mode;           /* DEMOD_CH_* (ignored for mono) */
+    int32_t  device;                 /* HIP device ordinal */
+    int32_t  method;                 /* DEMOD_METHOD_* */
+    uint32_t reserved;               /* must be 0 */
+    double   freqs[DEMOD_MAX_TONES]; /* tone frequencies, Hz; symbol i <-> freqs[i] */
+} demod_cfg_t;
+
+typedef struct demod demod_t;
+
+/* Fill cfg with the 2-FSK defaults of SURVEY.md §8: fs 48 kHz, N = hop = 1024,
+ * tones {1500, 3000} Hz, mono. */
+void demod_cfg_default(demod_cfg_t *cfg);
+
+/* Replaces opus_decoder_create (opus.h:423). NULL on failure, *error set. */
+demod_t *demod_create(const demod_cfg_t *cfg, int *error);
+
+/* Replaces opus_decoder_destroy (opus.h:512). NULL is accepted. */
+void demod_destroy(demod_t *st);
+
+/* Drop carried samples; the next demodulate() starts a new stream.
+ * Mirrors playback_start_new_stream (playback.cpp:67-74). */
+int demod_reset(demod_t *st);
+
+/* Number of mono samples currently carried between demodulate() calls. */
+int demod_pending(const demod_t *st);
+
+/* Upper bound on symbols the next demodulate(st, ., n_frames, ...) emits. */
+int demod_max_symbols(const demod_t *st, size_t n_frames);
+
+/*
+ * Streaming entry point: demodulate(pcm, n) -> symbols.
+ * pcm: host pointer to n_frames frames of `channels` interleaved int16
+ * samples (48 kHz int16 LE, the format opus_decode writes at
+ * playback.cpp:118). Samples are appended to the handle's carry buffer;
+ * one symbol is emitted per complete window (advance `hop`).
+ * Returns the number of symbols written to symbols[0..], or a negative code.
+ * If max_symbols is too small nothing is consumed and
+ * DEMOD_BUFFER_TOO_SMALL is returned.
+ * mags (nullable, host): receives k floats |X_k|^2 per emitted symbol.
+ */
+int demodulate(demod_t *st, const int16_t *pcm, size_t n_frames,
+               uint8_t *symbols, size_t max_symbols);
+int demodulate_mags(demod_t *st, const int16_t *pcm, size_t n_frames,
+                    uint8_t *symbols, float *mags, size_t max_symbols);
+
+/*
+ * Batch entry point (the GPU hot path): W windows of mono int16.
+ * Window w starts at pcm + w * hop and is n samples long.
+ * Pointers may be host or device memory (detected per call); the call is
+ * synchronous. Returns W on success.
+ */
+int demod_batch(demod_t *st, const int16_t *pcm, size_t n_windows,
+                uint8_t *symbols, float *mags);
+
+/*
+ * Asynchronous batch on a caller stream (hipStream_t passed as void*;
+ * NULL = the handle's own stream). All pointers must be device pointers.
+ * Nothing is synchronised; returns W once the work is enqueued.
+ */
+int demod_batch_async(demod_t *st, const int16_t *d_pcm, size_t n_windows,
+                      uint8_t *d_symbols, float *d_mags, void *stream);
+
+/* ---- ip.proto framing (ToReceiver{AudioData{bytes}}, delimited) ------- */
+
+/* Bytes demod_frame_encode needs for a payload of len bytes. */
+size_t demod_frame_size(size_t payload_len);
+
+/* Encode varint32(len(msg)) || ToReceiver{audio_data{opus_encoded_frame =
+ * payload}}. Returns bytes written, DEMOD_BUFFER_TOO_SMALL, or
+ * DEMOD_FRAME_TOO_LARGE when len > DEMOD_MAX_FRAME_PAYLOAD. */
+int demod_frame_encode(const uint8_t *payload, size_t len,
+                       uint8_t *out, size_t cap);
+
+/* Decode one delimited ToReceiver frame from in[0..len). On success
+ * *payload points into `in`, *payload_len is its length, *consumed the
+ * bytes of the whole frame; returns DEMOD_OK. Returns DEMOD_BUFFER_TOO_SMALL
+ * when `in` holds only part of a frame (read more and retry),
+ * DEMOD_INVALID_PACKET on malformed bytes, DEMOD_FRAME_TOO_LARGE when the
+ * payload exceeds DEMOD_MAX_FRAME_PAYLOAD (network.cpp:223-227). */
+int demod_frame_decode(const uint8_t *in, size_t len, const uint8_t **payload,
+                       size_t *payload_len, size_t *consumed);
+
+/* Bits per symbol used for packing: ceil(log2(k)), at least 1. */
+int demod_bits_per_symbol(uint32_t k);
+
+/* Pack n symbols MSB-first into ceil(n*bits/8) bytes. Returns bytes. */
+int demod_pack_symbols(const uint8_t *symbols, size_t n, int bits,
+                       uint8_t *out, size_t cap);
+int demod_unpack_symbols(const uint8_t *in, size_t n, int bits,
+                         uint8_t *symbols, size_t cap);
+
+/* Frame a symbol stream into consecutive delimited ToReceiver frames,
+ * each payload <= max_payload (<= DEMOD_MAX_FRAME_PAYLOAD) bytes of packed
+ * symbols. Returns total bytes written. */
+long long demod_frame_symbols(const uint8_t *symbols, size_t n, int bits,
+                              size_t max_payload, uint8_t *out, size_t cap);
+
+/* ---- synthetic PCM (benchmarks / tests) -------------------------------- */
+
+/* Device generator of the seeded FSK test signal (DESIGN.md §Synthetic
+ * input): windows w0 .. w0+W-1 of the stream, cfg->n mono samples each,
+ * contiguous, symbols uniform
+ * over cfg->k, amplitude `amplitude`, Irwin–Hall noise of std `sigma`.
+ * d_pcm / d_symbols are device pointers; enqueued on `stream`. */
+int demod_synth_fsk(const demod_cfg_t *cfg, uint64_t seed, uint64_t w0,
+                    size_t n_windows, int amplitude, int sigma, int16_t *d_pcm,
+                    uint8_t *d_symbols, void *stream);
+
+/* ---- misc -------------------------------------------------------------- */
+const char *demod_strerror(int error);   /* mirrors opus_strerror */
+const char *demod_version_string(void);  /* mirrors opus_get_version_string */
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FSKDEMOD_DEMOD_H */

@@ -1,0 +1,64 @@
+"""The C-ABI library loads and exports what include/demod.h declares.
+
+No compute calls here (CPU container): argument validation happens before any
+device work, and without a GPU demod_create must fail loudly with
+DEMOD_NO_DEVICE — there is no CPU fallback.
+"""
+import ctypes
+import subprocess
+
+import pytest
+
+
+def test_library_exports_every_header_symbol(A):
+    lib = A.load_library()
+    declared = A.header_exports()
+    assert len(declared) >= 20
+    for name in declared:
+        assert hasattr(lib, name), name
+    out = subprocess.run(["nm", "-D", "--defined-only", A.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    exported = {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
+    assert set(declared) <= exported
+
+
+def test_library_targets_gfx950_only(A):
+    """The embedded code objects are gfx950 and nothing else."""
+    import re
+    blob = open(A.LIB_PATH, "rb").read()
+    targets = set(re.findall(rb"amdgcn-amd-amdhsa-+(gfx[0-9a-f]+)", blob))
+    assert targets == {b"gfx950"}, targets
+
+
+def test_cfg_struct_layout(A):
+    assert ctypes.sizeof(A.DemodCfg) == 8 + 4 * 8 + 8 * 16
+    cfg = A.make_cfg()
+    assert cfg.n == 1024 and cfg.hop == 1024 and cfg.k == 2 and cfg.fs == 48000.0
+    assert tuple(cfg.freqs[:2]) == (1500.0, 3000.0)
+
+
+@pytest.mark.parametrize("bad", [
+    dict(n=1000), dict(n=32), dict(n=8192), dict(hop=0), dict(hop=12), dict(hop=2048),
+    dict(channels=3), dict(freqs=()), dict(freqs=(30000.0,)), dict(freqs=(-1.0,)),
+    dict(fs=0.0), dict(channels=2, channel_mode=5),
+])
+def test_create_rejects_bad_config(A, bad):
+    kw = dict(bad)
+    with pytest.raises(A.DemodError) as e:
+        A.Demodulator(**kw)
+    assert e.value.code == A.DEMOD_BAD_ARG
+
+
+def test_create_without_gpu_fails_loudly(A):
+    torch = pytest.importorskip("torch")
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(A.DemodError) as e:
+        A.Demodulator()
+    assert e.value.code == A.DEMOD_NO_DEVICE
+
+
+def test_strerror_and_version(A):
+    assert A.strerror(A.DEMOD_NO_DEVICE).startswith("no gfx950")
+    assert A.strerror(12345) == "unknown error"
+    assert "gfx950" in A.version_string()
