@@ -43,7 +43,7 @@ DEMOD_MAX_TONES = 16
 DEMOD_MAX_FRAME_PAYLOAD = 4096
 
 CH_LEFT, CH_RIGHT, CH_DOWNMIX = 0, 1, 2
-METHOD_AUTO, METHOD_GOERTZEL, METHOD_FFT = 0, 1, 2
+METHOD_AUTO, METHOD_GOERTZEL, METHOD_FFT, METHOD_FOLDED = 0, 1, 2, 3
 
 FSK2_FREQS = (1500.0, 3000.0)                              # SURVEY §8 tone plan
 FSK8_FREQS = tuple(1500.0 + 375.0 * i for i in range(8))
@@ -101,6 +101,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "demod_destroy": (None, [_P]),
         "demod_reset": (ctypes.c_int, [_P]),
         "demod_pending": (ctypes.c_int, [_P]),
+        "demod_method": (ctypes.c_int, [_P]),
         "demod_max_symbols": (ctypes.c_int, [_P, _SZ]),
         "demodulate": (ctypes.c_int, [_P, _P, _SZ, _P, _SZ]),
         "demodulate_mags": (ctypes.c_int, [_P, _P, _SZ, _P, _P, _SZ]),
@@ -225,6 +226,11 @@ class Demodulator:
         if rc < 0:
             raise DemodError(rc, "demod_reset")
 
+    @property
+    def method(self) -> int:
+        """Detector in use: METHOD_GOERTZEL, METHOD_FOLDED or METHOD_FFT."""
+        return int(self._lib.demod_method(self._h))
+
     def pending(self) -> int:
         return int(self._lib.demod_pending(self._h))
 
@@ -278,7 +284,8 @@ class Demodulator:
         return rc
 
     def batch_async(self, d_pcm, n_windows: int, d_sym, d_mag=None, stream: int = 0) -> int:
-        """Enqueue on a HIP stream (raw hipStream_t as int; 0 = handle stream)."""
+        """Enqueue on a HIP stream (raw hipStream_t as int; 0 = default stream,
+        e.g. torch.cuda.current_stream().cuda_stream)."""
         rc = self._lib.demod_batch_async(self._h, _ptr(d_pcm), n_windows, _ptr(d_sym),
                                          _ptr(d_mag), stream or None)
         if rc < 0:

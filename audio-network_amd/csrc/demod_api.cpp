@@ -7,6 +7,7 @@
 // Errors are returned (no abort(), unlike OPUS_ERROR_CHECK playback.cpp:16-22).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -23,6 +24,7 @@ struct demod {
     int device = 0;
     int cus = 0;
     int log2g = 0;
+    int detector = kDetGoertzel;
     hipStream_t stream = nullptr;
     float4 *d_rot = nullptr;    // [k][g]
     float coef[kMaxTones] = {};
@@ -72,6 +74,18 @@ void demod_cfg_default(demod_cfg_t *cfg)
     cfg->freqs[1] = 3000.0;
 }
 
+// Every tone on an integer bin that is a multiple of 8 (fold.hip's identity).
+static bool fold_eligible(const demod_cfg_t &c)
+{
+    for (uint32_t i = 0; i < c.k; ++i) {
+        const double b = c.freqs[i] * c.n / c.fs;
+        const double r = std::nearbyint(b);
+        if (std::fabs(b - r) > 1e-9 * std::max(1.0, b)) return false;
+        if (((long long)r) % 8 != 0) return false;
+    }
+    return true;
+}
+
 static int validate(const demod_cfg_t *c)
 {
     if (!c) return DEMOD_BAD_ARG;
@@ -82,9 +96,11 @@ static int validate(const demod_cfg_t *c)
     if (c->hop < 8 || c->hop > c->n || (c->hop % 8)) return DEMOD_BAD_ARG;
     if (c->channels != 1 && c->channels != 2) return DEMOD_BAD_ARG;
     if (c->channels == 2 && (c->channel_mode < 0 || c->channel_mode > 2)) return DEMOD_BAD_ARG;
-    if (c->method != DEMOD_METHOD_AUTO && c->method != DEMOD_METHOD_GOERTZEL)
+    if (c->method != DEMOD_METHOD_AUTO && c->method != DEMOD_METHOD_GOERTZEL &&
+        c->method != DEMOD_METHOD_FOLDED)
         return DEMOD_UNIMPLEMENTED;
     if (c->reserved != 0) return DEMOD_BAD_ARG;
+    if (c->method == DEMOD_METHOD_FOLDED && !fold_eligible(*c)) return DEMOD_BAD_ARG;
     for (uint32_t i = 0; i < c->k; ++i)
         if (!std::isfinite(c->freqs[i]) || c->freqs[i] < 0.0 || c->freqs[i] > c->fs / 2)
             return DEMOD_BAD_ARG;
@@ -115,14 +131,21 @@ static int init_device_state(demod_t *st)
     int g = (int)(c.n / 64), lg = 0;
     while ((1 << lg) < g) ++lg;
     st->log2g = lg;
-    // Rotation of each lane segment j (samples [64j, 64j+64)) into window phase:
-    // A = e^{-jw(64j+63)}, B = e^{-jw(64j+64)}; X += A s1 - B s2.
+    const bool eligible = fold_eligible(c);
+    st->detector = (c.method == DEMOD_METHOD_FOLDED || (c.method == DEMOD_METHOD_AUTO && eligible &&
+                                                        c.k >= 3))
+                       ? kDetFolded
+                       : kDetGoertzel;
+    // Rotation of each lane's piece into window phase, X += A s1 - B s2:
+    //   Goertzel: segment j = samples [64j, 64j+64): A = e^{-jw(64j+63)}, B = e^{-jw(64j+64)}
+    //   Folded:   folded samples [8j, 8j+8):         A = e^{-jw(8j+7)},   B = e^{-jw(8j+8)}
+    const double span = st->detector == kDetFolded ? 8.0 : 64.0;
     std::vector<float4> rot((size_t)c.k * g);
     for (uint32_t k = 0; k < c.k; ++k) {
         const double w = 2.0 * M_PI * c.freqs[k] / c.fs;
         st->coef[k] = (float)(2.0 * std::cos(w));
         for (int j = 0; j < g; ++j) {
-            const double a = -w * (64.0 * j + 63.0), b = -w * (64.0 * j + 64.0);
+            const double a = -w * (span * j + span - 1.0), b = -w * (span * j + span);
             rot[(size_t)k * g + j] = make_float4((float)std::cos(a), (float)std::sin(a),
                                                  (float)std::cos(b), (float)std::sin(b));
         }
@@ -186,6 +209,12 @@ int demod_reset(demod_t *st)
     return DEMOD_OK;
 }
 
+int demod_method(const demod_t *st)
+{
+    if (!st) return DEMOD_BAD_ARG;
+    return st->detector == kDetFolded ? DEMOD_METHOD_FOLDED : DEMOD_METHOD_GOERTZEL;
+}
+
 int demod_pending(const demod_t *st)
 {
     if (!st) return DEMOD_BAD_ARG;
@@ -221,8 +250,7 @@ static int enqueue_batch(demod_t *st, const int16_t *d_pcm, size_t n_windows, ui
     p.sym = d_sym;
     p.mag = d_mag;
     for (uint32_t k = 0; k < st->cfg.k; ++k) p.coef[k] = st->coef[k];
-    const int grid = goertzel_grid(p.k, p.n_windows, p.log2g, st->device, st->cus);
-    HIP_TRY(launch_goertzel(p, grid, s));
+    HIP_TRY(launch_detector(st->detector, p, s));
     return (int)n_windows;
 }
 
@@ -333,8 +361,7 @@ int demod_batch_async(demod_t *st, const int16_t *d_pcm, size_t n_windows, uint8
     if (!st || (!d_pcm && n_windows) || (!d_symbols && n_windows)) return DEMOD_BAD_ARG;
     if (n_windows > 0x7FFFFFFF) return DEMOD_BAD_ARG;
     if (((uintptr_t)d_pcm & 15) != 0) return DEMOD_BAD_ARG;
-    hipStream_t s = stream ? (hipStream_t)stream : st->stream;
-    return enqueue_batch(st, d_pcm, n_windows, d_symbols, d_mags, s);
+    return enqueue_batch(st, d_pcm, n_windows, d_symbols, d_mags, (hipStream_t)stream);
 }
 
 int demodulate_mags(demod_t *st, const int16_t *pcm, size_t n_frames, uint8_t *symbols,

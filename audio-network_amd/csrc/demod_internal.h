@@ -24,7 +24,21 @@ struct GoertzelParams {
     uint8_t *sym;            // [n_windows]
     float *mag;              // [n_windows][k] or nullptr
     float coef[kMaxTones];   // 2 cos(w_k)
+    int xcd_swizzle;         // 1: blocks b, b+8, b+16.. (one XCD) take adjacent tiles
 };
+
+// Tile-group index of this block. Blocks are dealt round-robin to the 8 XCDs
+// (MI355X_MICROARCH.md §Workgroup dispatch), so with the swizzle each XCD
+// walks one contiguous 1/8 of the tiles and every output line is written by a
+// single XCD's L2. Placement only affects speed, never correctness.
+__device__ __forceinline__ long long tile_block(int swz)
+{
+    const long long b = blockIdx.x, nb = gridDim.x;
+    if (!swz) return b;
+    const long long per = nb / 8, full = per * 8;
+    if (b >= full) return b;
+    return (b % 8) * per + b / 8;
+}
 
 struct SynthParams {
     uint64_t seed;
@@ -40,8 +54,12 @@ struct SynthParams {
     uint32_t inc[kMaxTones];  // phase increment per sample, 2^32 / cycle
 };
 
-hipError_t launch_goertzel(const GoertzelParams &p, int grid, hipStream_t s);
-int goertzel_grid(int k, long long n_windows, int log2g, int device, int device_cus);
+// Detectors (the kernels behind DEMOD_METHOD_*).
+constexpr int kDetGoertzel = 1;  // goertzel.hip: 64-sample lane segments
+constexpr int kDetFolded = 3;    // fold.hip: Goertzel on the N/8-folded window
+
+hipError_t launch_detector(int detector, const GoertzelParams &p, hipStream_t s);
+int tile_grid(long long n_windows, int log2g);
 hipError_t launch_synth(const SynthParams &p, hipStream_t s);
 
 }  // namespace fskd

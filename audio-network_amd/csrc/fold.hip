@@ -1,0 +1,153 @@
+// fold.hip — Goertzel tone bank on the period-folded window (integer-bin tones).
+//
+// Identity (exact): for tone bins b_k that are all multiples of 8,
+// e^{-j 2 pi b_k (n + N/8) / N} = e^{-j 2 pi b_k n / N}, so
+//     X_k = sum_{n<N} x[n] W^{b_k n} = sum_{r<N/8} xf[r] W^{b_k r},
+//     xf[r] = sum_{m<8} x[r + m N/8]           (integer sums, exact).
+// The Goertzel recurrence then runs over the N/8 folded samples instead of N;
+// P_k and the argmax are the same quantities the plain tone bank computes
+// (oracle/fsk_oracle.c:goertzel_window_d), to fp32 rounding.
+//
+// Layout: a window of N = 64 G samples = 8 G chunks of 8 samples; lane j of
+// the window's G-lane group loads chunks j + G m (m = 0..7) — per wave
+// instruction each window contributes G consecutive 16-byte chunks, i.e. whole
+// 128-byte lines, so the loads are coalesced without any LDS transpose —
+// folds them into xf[8j .. 8j+7], runs the K recurrences over those 8 values,
+// rotates into window phase (A = e^{-jw(8j+7)}, B = e^{-jw(8j+8)}) and sums
+// over the group with DPP, exactly as goertzel.hip does for 64-sample segments.
+// VALU per sample drops from ~(1 + 2K) to ~(1 + 2K/8 + epilogue), which makes
+// 8-FSK HBM-bound.
+#include "demod_internal.h"
+
+namespace fskd {
+
+typedef unsigned int u32x4f __attribute__((ext_vector_type(4)));
+
+template <int CTRL>
+__device__ __forceinline__ float dppf_(float v)
+{
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+
+__device__ __forceinline__ float group_sum_f(float v, int log2g)
+{
+    if (log2g > 0) v += dppf_<0xB1>(v);
+    if (log2g > 1) v += dppf_<0x4E>(v);
+    if (log2g > 2) v += dppf_<0x141>(v);
+    if (log2g > 3) v += dppf_<0x140>(v);
+    if (log2g > 4) v += __shfl_xor(v, 16);
+    if (log2g > 5) v += __shfl_xor(v, 32);
+    return v;
+}
+
+//   ROTLDS: keep the per-lane rotation constants in a block LDS table instead
+//           of 4K VGPRs (raises occupancy for large K).
+template <int K, int LOG2G, bool NT = true, int WPB = 4, bool ROTLDS = false>
+__global__ __launch_bounds__(64 * WPB) void fold_tile_kernel(GoertzelParams p)
+{
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int log2g = LOG2G >= 0 ? LOG2G : p.log2g;
+    const int g = 1 << log2g;
+    const int n = 64 << log2g;
+    const int j = lane & (g - 1);
+    const int win_in_tile = lane >> log2g;
+    const long long wins_per_tile = 64 >> log2g;
+    const long long n_tiles = (p.n_windows + wins_per_tile - 1) / wins_per_tile;
+
+    float4 r[ROTLDS ? 1 : K];
+    __shared__ float4 rot_lds[ROTLDS ? K * 64 : 1];
+    if (ROTLDS) {
+        for (int i = threadIdx.x; i < K * g; i += 64 * WPB) rot_lds[i] = p.rot[i];
+        __syncthreads();
+    } else {
+#pragma unroll
+        for (int k = 0; k < K; ++k) r[k] = p.rot[k * g + j];
+    }
+    int goff[8];
+#pragma unroll
+    for (int m = 0; m < 8; ++m)
+        goff[m] = (int)(((long long)win_in_tile * p.hop + (long long)(j + g * m) * 8) * 2);
+
+    const long long stride = (long long)gridDim.x * WPB;
+    for (long long t = tile_block(p.xcd_swizzle) * WPB + wave; t < n_tiles; t += stride) {
+        const long long wbase = t * wins_per_tile;
+        long long bytes = ((p.n_windows - wbase - 1) * p.hop + n) * 2;
+        if (bytes > 0x7FFFFFF0LL) bytes = 0x7FFFFFF0LL;
+        __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)(p.pcm + wbase * p.hop), (short)0, (int)bytes, 0x00020000);
+        u32x4f v[8];
+#pragma unroll
+        for (int m = 0; m < 8; ++m)
+            v[m] = __builtin_amdgcn_raw_buffer_load_b128(rs, goff[m], 0, NT ? 2 : 0);
+
+        int acc[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) acc[q] = 0;
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+            const uint32_t d4[4] = {v[m].x, v[m].y, v[m].z, v[m].w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                acc[2 * q] += (int)(short)(d4[q] & 0xFFFFu);
+                acc[2 * q + 1] += (int)d4[q] >> 16;
+            }
+        }
+        float xf[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) xf[q] = (float)acc[q];
+
+        float best = -1.f;
+        int arg = 0;
+        float P[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const float a = fmaf(p.coef[k], s1, xf[q] - s2);
+                s2 = s1;
+                s1 = a;
+            }
+            const float4 rk = ROTLDS ? rot_lds[k * g + j] : r[ROTLDS ? 0 : k];
+            float re = rk.x * s1 - rk.z * s2;
+            float im = rk.y * s1 - rk.w * s2;
+            re = group_sum_f(re, log2g);
+            im = group_sum_f(im, log2g);
+            P[k] = fmaf(re, re, im * im);
+            if (P[k] > best) { best = P[k]; arg = k; }
+        }
+
+        const long long w = wbase + win_in_tile;
+        if (w < p.n_windows) {
+            if (j == 0) p.sym[w] = (uint8_t)arg;
+            if (p.mag) {
+#pragma unroll
+                for (int k = 0; k < K; ++k)
+                    if ((k & (g - 1)) == j) p.mag[w * K + k] = P[k];
+            }
+        }
+    }
+}
+
+template <int K>
+static const void *fold_kernel_for(int log2g)
+{
+    if (log2g == 4) return reinterpret_cast<const void *>(&fold_tile_kernel<K, 4>);
+    return reinterpret_cast<const void *>(&fold_tile_kernel<K, -1>);
+}
+
+const void *fold_kernel_ptr(int k, int log2g)
+{
+    switch (k) {
+#define FSKD_CASE(K) case K: return fold_kernel_for<K>(log2g);
+        FSKD_CASE(1) FSKD_CASE(2) FSKD_CASE(3) FSKD_CASE(4)
+        FSKD_CASE(5) FSKD_CASE(6) FSKD_CASE(7) FSKD_CASE(8)
+        FSKD_CASE(9) FSKD_CASE(10) FSKD_CASE(11) FSKD_CASE(12)
+        FSKD_CASE(13) FSKD_CASE(14) FSKD_CASE(15) FSKD_CASE(16)
+#undef FSKD_CASE
+    default: return nullptr;
+    }
+}
+
+}  // namespace fskd

@@ -49,10 +49,18 @@ __device__ __forceinline__ float group_sum(float v, int log2g)
 
 // LOG2G >= 0: lane-group size fixed at compile time (4 <=> n = 1024);
 // LOG2G == -1: taken from p.log2g at run time.
-template <int K, int LOG2G>
-__global__ __launch_bounds__(256) void goertzel_tile_kernel(GoertzelParams p)
+// Tunables (defaults are the shipped configuration, chosen by scripts/probe):
+//   PF  tiles prefetched per wave in registers (1 or 2),
+//   NT  non-temporal loads (the PCM is read exactly once),
+//   WPB waves per block (each wave owns a private LDS slice).
+//   DIRECT  no LDS: each lane loads its own 128-byte segment (8 x 16 B;
+//           per instruction 64 lines, each fully consumed over the 8).
+template <int K, int LOG2G, int PF = 1, bool NT = true, int WPB = kWavesPerBlock,
+          bool DIRECT = false>
+__global__ __launch_bounds__(64 * WPB) void goertzel_tile_kernel(GoertzelParams p)
 {
-    __shared__ __attribute__((aligned(16))) unsigned char lds[kWavesPerBlock * kLdsWaveBytes];
+    static_assert(PF == 1 || PF == 2, "prefetch depth");
+    __shared__ __attribute__((aligned(16))) unsigned char lds[DIRECT ? 16 : WPB * kLdsWaveBytes];
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     unsigned char *wl = lds + wave * kLdsWaveBytes;
@@ -75,15 +83,18 @@ __global__ __launch_bounds__(256) void goertzel_tile_kernel(GoertzelParams p)
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
         const int q = 64 * i + lane;
-        goff[i] = (int)(((long long)(q >> cpw_log2) * p.hop +
-                         (long long)(q & ((1 << cpw_log2) - 1)) * 8) * 2);
+        if (DIRECT)
+            goff[i] = (int)(((long long)win_in_tile * p.hop + seg * 64 + 8 * i) * 2);
+        else
+            goff[i] = (int)(((long long)(q >> cpw_log2) * p.hop +
+                             (long long)(q & ((1 << cpw_log2) - 1)) * 8) * 2);
     }
     // LDS write slot of chunk i: segment 8i + lane/8, chunk lane%8
     const int wr_off = (lane >> 3) * kLdsSegStride + (lane & 7) * 16;
     const int rd_off = lane * kLdsSegStride;
 
-    const long long stride = (long long)gridDim.x * kWavesPerBlock;
-    long long t = (long long)blockIdx.x * kWavesPerBlock + wave;
+    const long long stride = (long long)gridDim.x * WPB;
+    long long t = tile_block(p.xcd_swizzle) * WPB + wave;
 
     auto load_tile = [&](long long tt, u32x4 v[8]) {
         const long long wbase = tt * wins_per_tile;
@@ -94,21 +105,26 @@ __global__ __launch_bounds__(256) void goertzel_tile_kernel(GoertzelParams p)
             (void *)(p.pcm + wbase * p.hop), (short)0, (int)bytes, 0x00020000);
 #pragma unroll
         for (int i = 0; i < 8; ++i)
-            v[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, goff[i], 0, 2 /*nt*/);
+            v[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, goff[i], 0, NT ? 2 : 0);
     };
 
-    u32x4 v[8];
-    if (t < n_tiles) load_tile(t, v);
-
-    for (; t < n_tiles; t += stride) {
+    // One tile: stage v through LDS, refill v with tile `next`, then run the
+    // recurrences, the rotation + lane-group reduction and the decision.
+    auto do_tile = [&](long long tt, u32x4 v[8], long long next) {
+        u32x4 cur[8];
+        if (DIRECT) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i)
-            *reinterpret_cast<u32x4 *>(wl + wr_off + i * 8 * kLdsSegStride) = v[i];
-        const long long tn = t + stride;
-        if (tn < n_tiles) load_tile(tn, v);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            for (int i = 0; i < 8; ++i) cur[i] = v[i];
+            if (next < n_tiles) load_tile(next, v);
+        } else {
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+                *reinterpret_cast<u32x4 *>(wl + wr_off + i * 8 * kLdsSegStride) = v[i];
+            if (next < n_tiles) load_tile(next, v);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
 
         float s1[K], s2[K];
 #pragma unroll
@@ -116,7 +132,7 @@ __global__ __launch_bounds__(256) void goertzel_tile_kernel(GoertzelParams p)
 
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            const u32x4 sj = *reinterpret_cast<const u32x4 *>(wl + rd_off + j * 16);
+            const u32x4 sj = DIRECT ? cur[j] : *reinterpret_cast<const u32x4 *>(wl + rd_off + j * 16);
             const uint32_t d4[4] = {sj.x, sj.y, sj.z, sj.w};
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
@@ -151,7 +167,7 @@ __global__ __launch_bounds__(256) void goertzel_tile_kernel(GoertzelParams p)
             if (P[k] > best) { best = P[k]; arg = k; }
         }
 
-        const long long w = t * wins_per_tile + win_in_tile;
+        const long long w = tt * wins_per_tile + win_in_tile;
         if (w < p.n_windows) {
             if (seg == 0) p.sym[w] = (uint8_t)arg;
             if (p.mag) {
@@ -159,6 +175,21 @@ __global__ __launch_bounds__(256) void goertzel_tile_kernel(GoertzelParams p)
                 for (int k = 0; k < K; ++k)
                     if ((k & (g - 1)) == seg) p.mag[w * K + k] = P[k];
             }
+        }
+    };
+
+    if (PF == 1) {
+        u32x4 v[8];
+        if (t < n_tiles) load_tile(t, v);
+        for (; t < n_tiles; t += stride) do_tile(t, v, t + stride);
+    } else {
+        u32x4 va[8], vb[8];
+        if (t < n_tiles) load_tile(t, va);
+        if (t + stride < n_tiles) load_tile(t + stride, vb);
+        for (; t < n_tiles; t += 2 * stride) {
+            do_tile(t, va, t + 2 * stride);
+            if (t + stride >= n_tiles) break;
+            do_tile(t + stride, vb, t + 3 * stride);
         }
     }
 }
@@ -183,31 +214,28 @@ static const void *kernel_ptr(int k, int log2g)
     }
 }
 
-int goertzel_grid(int k, long long n_windows, int log2g, int device, int device_cus)
+// One tile per wave (grid = tiles / waves-per-block): measured 317 us vs
+// 363 us for a persistent grid-stride grid on 2^20 windows (profiles/,
+// DESIGN.md §Tuning) — the dispatcher keeps every CU fed to the last tile.
+int tile_grid(long long n_windows, int log2g)
 {
     const long long wins_per_tile = 64 >> log2g;
     const long long n_tiles = (n_windows + wins_per_tile - 1) / wins_per_tile;
     long long blocks = (n_tiles + kWavesPerBlock - 1) / kWavesPerBlock;
-    // Persistent grid: exactly the co-resident blocks, so no block waits for
-    // a second dispatch round (that tail would cost a whole extra pass).
-    int per_cu = 0;
-    const void *f = kernel_ptr(k, log2g);
-    (void)device;
-    if (!f || hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, 64 * kWavesPerBlock, 0) !=
-                  hipSuccess || per_cu < 1)
-        per_cu = 1;
-    const long long cap = (long long)device_cus * per_cu;
-    if (blocks > cap) blocks = cap;
+    if (blocks > 0x7FFFFFFFLL) blocks = 0x7FFFFFFFLL;  // kernels grid-stride beyond
     if (blocks < 1) blocks = 1;
     return (int)blocks;
 }
 
-hipError_t launch_goertzel(const GoertzelParams &p, int grid, hipStream_t s)
+const void *fold_kernel_ptr(int k, int log2g);
+
+hipError_t launch_detector(int detector, const GoertzelParams &p, hipStream_t s)
 {
-    const void *f = kernel_ptr(p.k, p.log2g);
+    const void *f = detector == kDetFolded ? fold_kernel_ptr(p.k, p.log2g) : kernel_ptr(p.k, p.log2g);
     if (!f) return hipErrorInvalidValue;
     void *args[] = {const_cast<GoertzelParams *>(&p)};
-    return hipLaunchKernel(f, dim3(grid), dim3(64 * kWavesPerBlock), args, 0, s);
+    return hipLaunchKernel(f, dim3(tile_grid(p.n_windows, p.log2g)), dim3(64 * kWavesPerBlock),
+                           args, 0, s);
 }
 
 }  // namespace fskd

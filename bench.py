@@ -95,6 +95,7 @@ def main():
     ap.add_argument("--config", choices=["fsk2", "fsk8"], default="fsk2")
     ap.add_argument("--windows", type=int, default=1 << 20, help="windows per GPU")
     ap.add_argument("--no-mags", action="store_true", help="symbols only")
+    ap.add_argument("--method", choices=["auto", "goertzel", "folded"], default="auto")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -116,7 +117,9 @@ def main():
     K = len(freqs)
     n = 1024
     W = int(args.windows)
-    cfg = A.make_cfg(freqs=freqs, n=n, device=local)
+    method = {"auto": A.METHOD_AUTO, "goertzel": A.METHOD_GOERTZEL,
+              "folded": A.METHOD_FOLDED}[args.method]
+    cfg = A.make_cfg(freqs=freqs, n=n, device=local, method=method)
     dev = torch.device("cuda", local)
     d_pcm = torch.empty((W, n), dtype=torch.int16, device=dev)
     d_true = torch.empty(W, dtype=torch.uint8, device=dev)
@@ -155,7 +158,8 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    kts = np.array([a.elapsed_time(b) for a, b in evs])
+    kernel_ms = float(kts.mean())
     ms_per_step = elapsed / args.steps * 1e3
 
     # correctness of the timed output: every symbol vs the transmitted one
@@ -198,6 +202,9 @@ def main():
                 "outputs": "symbols" + ("" if args.no_mags else " + |X_k|^2"),
                 "parallelism": f"dp{world} (independent window shards, RCCL symbol all-gather)",
             },
+            "detector": {A.METHOD_GOERTZEL: "goertzel", A.METHOD_FOLDED: "folded"}.get(
+                demod.method, str(demod.method)),
+            "kernel_ms_p10_p50_p90": [round(float(np.percentile(kts, q)), 4) for q in (10, 50, 90)],
             "symbol_errors": sym_err,
             "symbol_error_rate": sym_err / float(world * W),
             "kernel_ms": round(kernel_ms, 4),
@@ -209,7 +216,8 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBPS, 4),
                 "traffic": pmc_traffic(args.config, W),
                 "alg_bytes_per_launch": alg_bytes,
-                "kernel": "goertzel_tile_kernel<%d,4>" % K,
+                "kernel": ("fold_tile_kernel<%d,4>" if demod.method == A.METHOD_FOLDED
+                           else "goertzel_tile_kernel<%d,4>") % K,
             },
         }
         if framed:

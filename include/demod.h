@@ -58,9 +58,12 @@ extern "C" {
 #define DEMOD_CH_DOWNMIX  2   /* x = (L + R) >> 1 (arithmetic shift) */
 
 /* detector selection */
-#define DEMOD_METHOD_AUTO      0 /* GOERTZEL (plain tone bank) */
-#define DEMOD_METHOD_GOERTZEL  1 /* per-window Goertzel tone bank */
-#define DEMOD_METHOD_FFT       2 /* full-spectrum N-point real FFT, argmax over tone bins */
+#define DEMOD_METHOD_AUTO      0 /* FOLDED when eligible and k >= 3, else GOERTZEL */
+#define DEMOD_METHOD_GOERTZEL  1 /* per-window Goertzel tone bank over all n samples */
+#define DEMOD_METHOD_FFT       2 /* full-spectrum n-point real FFT, argmax over tone bins */
+#define DEMOD_METHOD_FOLDED    3 /* Goertzel over the window folded to n/8 samples:
+                                    exact when every tone is on a multiple of 8
+                                    bins (f*n/fs integer, divisible by 8) */
 
 typedef struct demod_cfg {
     double   fs;                     /* sample rate, Hz (48000) */
@@ -90,6 +93,9 @@ void demod_destroy(demod_t *st);
 /* Drop carried samples; the next demodulate() starts a new stream.
  * Mirrors playback_start_new_stream (playback.cpp:67-74). */
 int demod_reset(demod_t *st);
+
+/* Detector the handle runs (DEMOD_METHOD_GOERTZEL / _FOLDED / _FFT). */
+int demod_method(const demod_t *st);
 
 /* Number of mono samples currently carried between demodulate() calls. */
 int demod_pending(const demod_t *st);
@@ -123,9 +129,9 @@ int demod_batch(demod_t *st, const int16_t *pcm, size_t n_windows,
                 uint8_t *symbols, float *mags);
 
 /*
- * Asynchronous batch on a caller stream (hipStream_t passed as void*;
- * NULL = the handle's own stream). All pointers must be device pointers.
- * Nothing is synchronised; returns W once the work is enqueued.
+ * Asynchronous batch on a caller stream (hipStream_t passed as void*; NULL =
+ * the HIP default stream, as in the HIP runtime API). All pointers must be
+ * device pointers. Nothing is synchronised; returns W once enqueued.
  */
 int demod_batch_async(demod_t *st, const int16_t *d_pcm, size_t n_windows,
                       uint8_t *d_symbols, float *d_mags, void *stream);

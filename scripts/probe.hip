@@ -1,0 +1,290 @@
+// probe.hip — interleaved A/B timing of Goertzel kernel variants and of a
+// pure read-only HBM stream (the practical bandwidth ceiling of this box).
+//
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 scripts/probe.hip -o scripts/bin/probe
+//   scripts/bin/probe [windows=1048576] [rounds=5] [reps=10]
+//
+// All variants run in one process, round-robin, on the same seeded input
+// (cdna_hip_programming.md §5.4 rule 24); each reports min / median kernel
+// time from HIP events and the algorithmic GB/s. Outputs are cross-checked
+// against the default variant.
+#include "../audio-network_amd/csrc/goertzel.hip"
+#include "../audio-network_amd/csrc/synth.hip"
+#include "../audio-network_amd/csrc/fold.hip"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <string>
+#include <vector>
+
+using namespace fskd;
+
+#define CK(x)                                                                   \
+    do {                                                                        \
+        hipError_t e_ = (x);                                                    \
+        if (e_ != hipSuccess) {                                                 \
+            std::fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x,      \
+                         hipGetErrorString(e_));                                \
+            std::exit(1);                                                       \
+        }                                                                       \
+    } while (0)
+
+template <bool NT, int U>
+__global__ __launch_bounds__(256) void read_kernel(const u32x4 *__restrict__ p, long long n16,
+                                                   unsigned *out)
+{
+    long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+    const long long stride = (long long)gridDim.x * 256;
+    unsigned acc = 0;
+    for (; i + (U - 1) * stride < n16; i += U * stride) {
+        u32x4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            v[u] = NT ? __builtin_nontemporal_load(p + i + u * stride) : p[i + u * stride];
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+    }
+    for (; i < n16; i += stride) acc ^= p[i].x;
+    if (acc == 0x9E3779B9u) out[0] = acc;
+}
+
+// The same one-shot access pattern as the tile kernels (each wave reads one
+// contiguous 8 KiB tile with 8 coalesced 16 B/lane nt buffer loads) and no
+// compute: the practical HBM read ceiling for this shape.
+__global__ __launch_bounds__(256) void read_tile_kernel(const int16_t *p, long long n_tiles,
+                                                        unsigned *out)
+{
+    const int lane = threadIdx.x & 63;
+    const long long t = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (t >= n_tiles) return;
+    __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(p + t * 4096), (short)0, 8192, 0x00020000);
+    unsigned acc = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (64 * i + lane) * 16, 0, 2);
+        acc ^= v.x ^ v.y ^ v.z ^ v.w;
+    }
+    if (acc == 0x9E3779B9u) out[0] = acc;
+}
+
+struct Variant {
+    std::string name;
+    std::function<void(hipStream_t)> run;
+    double bytes;
+    std::vector<float> ms;
+    uint8_t *sym = nullptr;
+};
+
+static void add_variant(std::vector<Variant> &vs, const void *f, int wpb, const char *label,
+                        GoertzelParams p, int K, int cus, int tpw)
+{
+    // tpw = 0: persistent grid (co-resident blocks); tpw >= 1: tiles per wave
+    int per_cu = 0;
+    CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, 64 * wpb, 0));
+    const long long n_tiles = (p.n_windows + 3) / 4;
+    long long blocks = tpw ? (n_tiles + (long long)wpb * tpw - 1) / ((long long)wpb * tpw)
+                           : std::min<long long>((n_tiles + wpb - 1) / wpb, (long long)cus * per_cu);
+    uint8_t *sym;
+    CK(hipMalloc(&sym, p.n_windows));
+    p.sym = sym;
+    char name[200];
+    std::snprintf(name, sizeof name, "%s K=%d WPB=%d %s%d grid=%lld (%d/CU)", label, K, wpb,
+                  tpw ? "tpw=" : "persist", tpw, blocks, per_cu);
+    Variant v;
+    v.name = name;
+    v.bytes = (double)p.n_windows * (2048 + 1 + (p.mag ? 4 * K : 0));
+    v.sym = sym;
+    v.run = [f, p, blocks, wpb](hipStream_t s) {
+        void *args[] = {const_cast<GoertzelParams *>(&p)};
+        CK(hipLaunchKernel(f, dim3((unsigned)blocks), dim3(64 * wpb), args, 0, s));
+    };
+    vs.push_back(v);
+}
+
+#define GZ(K, PF, NT, WPB, DIRECT) \
+    reinterpret_cast<const void *>(&goertzel_tile_kernel<K, 4, PF, NT, WPB, DIRECT>)
+#define FD(K, WPB) reinterpret_cast<const void *>(&fold_tile_kernel<K, 4, true, WPB>)
+#define FDL(K, WPB) reinterpret_cast<const void *>(&fold_tile_kernel<K, 4, true, WPB, true>)
+
+int main(int argc, char **argv)
+{
+    const long long W = argc > 1 ? std::atoll(argv[1]) : (1LL << 20);
+    const int rounds = argc > 2 ? std::atoi(argv[2]) : 5;
+    const int reps = argc > 3 ? std::atoi(argv[3]) : 10;
+    hipDeviceProp_t prop;
+    CK(hipGetDeviceProperties(&prop, 0));
+    const int cus = prop.multiProcessorCount;
+    std::printf("device %s (%s), %d CUs, %lld windows (%.2f GiB)\n", prop.name, prop.gcnArchName,
+                cus, W, W * 2048.0 / (1 << 30));
+
+    // input: seeded FSK, identical to the product generator
+    int16_t *pcm, *lut;
+    CK(hipMalloc(&pcm, W * 2048));
+    std::vector<int16_t> hl(16384);
+    for (int i = 0; i < 16384; ++i) hl[i] = (int16_t)std::lrint(32767.0 * std::sin(2 * M_PI * i / 16384.0));
+    CK(hipMalloc(&lut, 16384 * 2));
+    CK(hipMemcpy(lut, hl.data(), 16384 * 2, hipMemcpyHostToDevice));
+    float *mag;
+    CK(hipMalloc(&mag, W * 8 * sizeof(float)));
+    unsigned *sink;
+    CK(hipMalloc(&sink, 64));
+
+    std::vector<Variant> vs;
+    // one input for all (2-FSK tones; the 8-FSK kernels read the same bytes)
+    {
+        SynthParams sp{};
+        sp.seed = 0x2C5DA044;
+        sp.n_windows = W;
+        sp.n = 1024;
+        sp.k = 2;
+        sp.amplitude = 8000;
+        sp.sigma = 400;
+        sp.lut = lut;
+        sp.pcm = pcm;
+        sp.inc[0] = 32u << 22;
+        sp.inc[1] = 64u << 22;
+        CK(launch_synth(sp, nullptr));
+        CK(hipDeviceSynchronize());
+    }
+
+    // rotation tables for K = 2 and 8 (freqs on bins 32.. as the bench)
+    auto make_rot = [&](int K, const double *bins, GoertzelParams &p) {
+        std::vector<float4> rot(K * 16);
+        for (int k = 0; k < K; ++k) {
+            const double w = 2 * M_PI * bins[k] / 1024.0;
+            p.coef[k] = (float)(2 * std::cos(w));
+            for (int j = 0; j < 16; ++j) {
+                const double a = -w * (64.0 * j + 63), b = -w * (64.0 * j + 64);
+                rot[k * 16 + j] = make_float4((float)std::cos(a), (float)std::sin(a),
+                                              (float)std::cos(b), (float)std::sin(b));
+            }
+        }
+        float4 *d;
+        CK(hipMalloc(&d, rot.size() * sizeof(float4)));
+        CK(hipMemcpy(d, rot.data(), rot.size() * sizeof(float4), hipMemcpyHostToDevice));
+        p.rot = d;
+    };
+    const double b2[2] = {32, 64}, b8[8] = {32, 40, 48, 56, 64, 72, 80, 88};
+    GoertzelParams p2{}, p8{};
+    p2.pcm = p8.pcm = pcm;
+    p2.n_windows = p8.n_windows = W;
+    p2.hop = p8.hop = 1024;
+    p2.log2g = p8.log2g = 4;
+    p2.k = 2;
+    p8.k = 8;
+    p2.mag = p8.mag = mag;
+    make_rot(2, b2, p2);
+    make_rot(8, b8, p8);
+
+    // fold rotation tables: lane j holds folded positions 8j..8j+7
+    GoertzelParams f2 = p2, f8 = p8;
+    auto make_fold_rot = [&](int K, const double *bins, GoertzelParams &p) {
+        std::vector<float4> rot(K * 16);
+        for (int k = 0; k < K; ++k) {
+            const double w = 2 * M_PI * bins[k] / 1024.0;
+            for (int j = 0; j < 16; ++j) {
+                const double a = -w * (8.0 * j + 7), b = -w * (8.0 * j + 8);
+                rot[k * 16 + j] = make_float4((float)std::cos(a), (float)std::sin(a),
+                                              (float)std::cos(b), (float)std::sin(b));
+            }
+        }
+        float4 *d;
+        CK(hipMalloc(&d, rot.size() * sizeof(float4)));
+        CK(hipMemcpy(d, rot.data(), rot.size() * sizeof(float4), hipMemcpyHostToDevice));
+        p.rot = d;
+    };
+    make_fold_rot(2, b2, f2);
+    make_fold_rot(8, b8, f8);
+
+    GoertzelParams p2s = p2, f2s = f2, f8s = f8, p2n = p2, f8n = f8;
+    p2s.xcd_swizzle = f2s.xcd_swizzle = f8s.xcd_swizzle = 1;
+    p2n.mag = f8n.mag = nullptr;
+    add_variant(vs, GZ(2, 1, true, 4, false), 4, "goertzel [default]", p2, 2, cus, 1);
+    add_variant(vs, GZ(2, 1, true, 4, false), 4, "goertzel XSWZ", p2s, 2, cus, 1);
+    add_variant(vs, GZ(2, 1, true, 4, false), 4, "goertzel nomag", p2n, 2, cus, 1);
+    add_variant(vs, FD(2, 4), 4, "fold", f2, 2, cus, 1);
+    add_variant(vs, FD(2, 4), 4, "fold XSWZ", f2s, 2, cus, 1);
+    add_variant(vs, FD(8, 4), 4, "fold [default]", f8, 8, cus, 1);
+    add_variant(vs, FD(8, 4), 4, "fold XSWZ", f8s, 8, cus, 1);
+    add_variant(vs, FD(8, 4), 4, "fold nomag", f8n, 8, cus, 1);
+    add_variant(vs, FD(8, 1), 1, "fold", f8, 8, cus, 1);
+    {
+        Variant v;
+        v.name = "read-only one-shot tile (8 KiB/wave, nt)";
+        v.bytes = (double)W * 2048;
+        const long long nt = W / 4;
+        v.run = [=](hipStream_t s) {
+            hipLaunchKernelGGL(read_tile_kernel, dim3((unsigned)((nt + 3) / 4)), dim3(256), 0, s,
+                               (const int16_t *)pcm, nt, sink);
+        };
+        vs.push_back(v);
+    }
+    {
+        const long long n16 = W * 2048 / 16;
+        for (int g : {2048, 4096, 8192}) {
+            Variant v;
+            v.name = "read-only dwordx4 nt U=4 grid=" + std::to_string(g);
+            v.bytes = (double)W * 2048;
+            v.run = [=](hipStream_t s) {
+                hipLaunchKernelGGL((read_kernel<true, 4>), dim3(g), dim3(256), 0, s,
+                                   (const u32x4 *)pcm, n16, sink);
+            };
+            vs.push_back(v);
+        }
+        Variant v;
+        v.name = "read-only dwordx4 plain U=4 grid=4096";
+        v.bytes = (double)W * 2048;
+        v.run = [=](hipStream_t s) {
+            hipLaunchKernelGGL((read_kernel<false, 4>), dim3(4096), dim3(256), 0, s,
+                               (const u32x4 *)pcm, n16, sink);
+        };
+        vs.push_back(v);
+    }
+
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    for (auto &v : vs) v.run(nullptr);  // warm
+    CK(hipDeviceSynchronize());
+    for (int r = 0; r < rounds; ++r)
+        for (auto &v : vs)
+            for (int i = 0; i < reps; ++i) {
+                CK(hipEventRecord(a, nullptr));
+                v.run(nullptr);
+                CK(hipEventRecord(b, nullptr));
+                CK(hipEventSynchronize(b));
+                float ms;
+                CK(hipEventElapsedTime(&ms, a, b));
+                v.ms.push_back(ms);
+            }
+    // cross-check symbols of every variant against the first variant of the same K
+    std::vector<std::pair<std::string, std::vector<uint8_t>>> refs;
+    std::vector<uint8_t> cur(W);
+    for (auto &v : vs) {
+        if (!v.sym) continue;
+        CK(hipMemcpy(cur.data(), v.sym, W, hipMemcpyDeviceToHost));
+        const size_t kp = v.name.find(" K=");
+        const std::string key = v.name.substr(kp, v.name.find(' ', kp + 1) - kp);
+        auto it = std::find_if(refs.begin(), refs.end(), [&](auto &r) { return r.first == key; });
+        if (it == refs.end()) {
+            refs.push_back({key, cur});
+            continue;
+        }
+        long long bad = 0;
+        for (long long i = 0; i < W; ++i) bad += cur[i] != it->second[i];
+        if (bad) std::printf("MISMATCH %s: %lld\n", v.name.c_str(), bad);
+    }
+    std::printf("%-72s %9s %9s %9s %7s\n", "variant", "min_us", "med_us", "GB/s(med)", "%peak");
+    for (auto &v : vs) {
+        std::sort(v.ms.begin(), v.ms.end());
+        const double mn = v.ms.front() * 1e3, md = v.ms[v.ms.size() / 2] * 1e3;
+        const double gbs = v.bytes / (md * 1e-6) / 1e9;
+        std::printf("%-72s %9.1f %9.1f %9.1f %6.1f%%\n", v.name.c_str(), mn, md, gbs, gbs / 80.0);
+    }
+    return 0;
+}

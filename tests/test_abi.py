@@ -41,6 +41,8 @@ def test_cfg_struct_layout(A):
     dict(n=1000), dict(n=32), dict(n=8192), dict(hop=0), dict(hop=12), dict(hop=2048),
     dict(channels=3), dict(freqs=()), dict(freqs=(30000.0,)), dict(freqs=(-1.0,)),
     dict(fs=0.0), dict(channels=2, channel_mode=5),
+    dict(method=3, freqs=(1500.0, 1546.875)),        # FOLDED needs multiples of 8 bins
+    dict(method=3, freqs=(1000.0,)),                  # non-integer bin
 ])
 def test_create_rejects_bad_config(A, bad):
     kw = dict(bad)
