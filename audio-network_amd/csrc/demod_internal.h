@@ -27,6 +27,16 @@ struct GoertzelParams {
     int xcd_swizzle;         // 1: blocks b, b+8, b+16.. (one XCD) take adjacent tiles
 };
 
+// Output store; NTS = non-temporal (streamed once, never re-read by the kernel).
+template <bool NTS, typename T>
+__device__ __forceinline__ void out_store(T *ptr, T v)
+{
+    if (NTS)
+        __builtin_nontemporal_store(v, ptr);
+    else
+        *ptr = v;
+}
+
 // Tile-group index of this block. Blocks are dealt round-robin to the 8 XCDs
 // (MI355X_MICROARCH.md §Workgroup dispatch), so with the swizzle each XCD
 // walks one contiguous 1/8 of the tiles and every output line is written by a

@@ -42,7 +42,8 @@ __device__ __forceinline__ float group_sum_f(float v, int log2g)
 
 //   ROTLDS: keep the per-lane rotation constants in a block LDS table instead
 //           of 4K VGPRs (raises occupancy for large K).
-template <int K, int LOG2G, bool NT = true, int WPB = 4, bool ROTLDS = false>
+//   NTS: non-temporal output stores.
+template <int K, int LOG2G, bool NT = true, int WPB = 4, bool ROTLDS = false, bool NTS = false>
 __global__ __launch_bounds__(64 * WPB) void fold_tile_kernel(GoertzelParams p)
 {
     const int lane = threadIdx.x & 63;
@@ -120,11 +121,11 @@ __global__ __launch_bounds__(64 * WPB) void fold_tile_kernel(GoertzelParams p)
 
         const long long w = wbase + win_in_tile;
         if (w < p.n_windows) {
-            if (j == 0) p.sym[w] = (uint8_t)arg;
+            if (j == 0) out_store<NTS>(p.sym + w, (uint8_t)arg);
             if (p.mag) {
 #pragma unroll
                 for (int k = 0; k < K; ++k)
-                    if ((k & (g - 1)) == j) p.mag[w * K + k] = P[k];
+                    if ((k & (g - 1)) == j) out_store<NTS>(p.mag + w * K + k, P[k]);
             }
         }
     }

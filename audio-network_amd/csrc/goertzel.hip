@@ -55,8 +55,9 @@ __device__ __forceinline__ float group_sum(float v, int log2g)
 //   WPB waves per block (each wave owns a private LDS slice).
 //   DIRECT  no LDS: each lane loads its own 128-byte segment (8 x 16 B;
 //           per instruction 64 lines, each fully consumed over the 8).
+//   NTS     non-temporal output stores.
 template <int K, int LOG2G, int PF = 1, bool NT = true, int WPB = kWavesPerBlock,
-          bool DIRECT = false>
+          bool DIRECT = false, bool NTS = false>
 __global__ __launch_bounds__(64 * WPB) void goertzel_tile_kernel(GoertzelParams p)
 {
     static_assert(PF == 1 || PF == 2, "prefetch depth");
@@ -169,11 +170,11 @@ __global__ __launch_bounds__(64 * WPB) void goertzel_tile_kernel(GoertzelParams 
 
         const long long w = tt * wins_per_tile + win_in_tile;
         if (w < p.n_windows) {
-            if (seg == 0) p.sym[w] = (uint8_t)arg;
+            if (seg == 0) out_store<NTS>(p.sym + w, (uint8_t)arg);
             if (p.mag) {
 #pragma unroll
                 for (int k = 0; k < K; ++k)
-                    if ((k & (g - 1)) == seg) p.mag[w * K + k] = P[k];
+                    if ((k & (g - 1)) == seg) out_store<NTS>(p.mag + w * K + k, P[k]);
             }
         }
     };

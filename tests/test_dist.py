@@ -1,0 +1,108 @@
+"""The sharded multi-GPU path (config 5) on CPU: world_size 2 over gloo.
+
+Each rank demodulates its contiguous shard of independent streams (here with
+the oracle standing in for the GPU kernel: this test covers the sharding,
+the symbol gather and rank-0 framing, not the kernel), gathers every rank's
+symbols and rank 0 frames them into ToReceiver messages; the reassembled
+stream must equal the single-process oracle result.
+"""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, n_streams, wps, k, q):
+    try:
+        _work(rank, world, port, n_streams, wps, k, q)
+    except BaseException:
+        import traceback
+        q.put(("error", traceback.format_exc()))
+        raise
+
+
+def _work(rank, world, port, n_streams, wps, k, q):
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import torch
+    import torch.distributed as dist
+    from conftest import load_pkg
+    from oracle import oracle as O
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    A = load_pkg()
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "audio_network_amd.dist", os.path.join(ROOT, "audio-network_amd", "dist.py"))
+    D = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(D)
+    freqs = A.FSK2_FREQS if k == 2 else A.FSK8_FREQS
+    first, count = D.shard_range(n_streams, rank, world)
+    pcm, _ = O.synth_fsk(freqs, 1024, count * wps, 0x2C5DA044, w0=first * wps)
+    sym, _ = O.goertzel(pcm, freqs, 1024)
+    full = D.gather_symbols(torch.from_numpy(sym), n_streams, world, unit=wps)
+    if rank == 0:
+        stream = D.frame_symbols(A, full.numpy(), k)
+        back = D.unframe_symbols(A, stream, n_streams * wps, k)
+        q.put((full.numpy().tobytes(), back.tobytes(), len(stream)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n_streams,k", [(2, 6, 2), (2, 7, 8), (3, 5, 2)])
+def test_sharded_demod_gather_and_framing(A, O, world, n_streams, k):
+    torch = pytest.importorskip("torch")
+    import torch.multiprocessing as mp
+    wps = 40  # windows per stream
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_streams, wps, k, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=240)
+    assert res[0] != "error", res[1]
+    full, back, nbytes = res
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    freqs = A.FSK2_FREQS if k == 2 else A.FSK8_FREQS
+    pcm, truth = O.synth_fsk(freqs, 1024, n_streams * wps, 0x2C5DA044)
+    ref, _ = O.goertzel(pcm, freqs, 1024)
+    got = np.frombuffer(full, np.uint8)
+    assert (got == ref).all() and (got == truth).all()
+    assert np.frombuffer(back, np.uint8).tolist() == ref.tolist()
+    assert nbytes > 0
+
+
+def test_shard_range_properties():
+    sys.path.insert(0, ROOT)
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "dist_mod", os.path.join(ROOT, "audio-network_amd", "dist.py"))
+    D = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(D)
+    for total in (0, 1, 7, 1024, 1025):
+        for world in (1, 2, 3, 8):
+            spans = [D.shard_range(total, r, world) for r in range(world)]
+            assert sum(c for _, c in spans) == total
+            pos = 0
+            for f, c in spans:
+                assert f == pos
+                pos += c
+            assert max(c for _, c in spans) - min(c for _, c in spans) <= 1
