@@ -107,6 +107,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "demodulate_mags": (ctypes.c_int, [_P, _P, _SZ, _P, _P, _SZ]),
         "demod_batch": (ctypes.c_int, [_P, _P, _SZ, _P, _P]),
         "demod_batch_async": (ctypes.c_int, [_P, _P, _SZ, _P, _P, _P]),
+        "demod_batch_spectrum_async": (ctypes.c_int, [_P, _P, _SZ, _P, _P, _P, _P]),
         "demod_frame_size": (_SZ, [_SZ]),
         "demod_frame_encode": (ctypes.c_int, [_P, _SZ, _P, _SZ]),
         "demod_frame_decode": (ctypes.c_int, [_P, _SZ, ctypes.POINTER(ctypes.c_void_p),
@@ -290,6 +291,15 @@ class Demodulator:
                                          _ptr(d_mag), stream or None)
         if rc < 0:
             raise DemodError(rc, "demod_batch_async")
+        return rc
+
+    def batch_spectrum_async(self, d_pcm, n_windows: int, d_sym, d_mag=None, d_spec=None,
+                             stream: int = 0) -> int:
+        """FFT handles: symbols, tone-bin |X|^2 and the full |X[b]|^2 spectrum."""
+        rc = self._lib.demod_batch_spectrum_async(self._h, _ptr(d_pcm), n_windows, _ptr(d_sym),
+                                                  _ptr(d_mag), _ptr(d_spec), stream or None)
+        if rc < 0:
+            raise DemodError(rc, "demod_batch_spectrum_async")
         return rc
 
 

@@ -27,6 +27,9 @@ struct demod {
     int detector = kDetGoertzel;
     hipStream_t stream = nullptr;
     float4 *d_rot = nullptr;    // [k][g]
+    float *d_tw512 = nullptr;   // FFT detector tables
+    float *d_tw1024 = nullptr;
+    int *d_bins = nullptr;
     float coef[kMaxTones] = {};
     // staging for host-pointer calls
     int16_t *d_in = nullptr;
@@ -97,8 +100,9 @@ static int validate(const demod_cfg_t *c)
     if (c->channels != 1 && c->channels != 2) return DEMOD_BAD_ARG;
     if (c->channels == 2 && (c->channel_mode < 0 || c->channel_mode > 2)) return DEMOD_BAD_ARG;
     if (c->method != DEMOD_METHOD_AUTO && c->method != DEMOD_METHOD_GOERTZEL &&
-        c->method != DEMOD_METHOD_FOLDED)
+        c->method != DEMOD_METHOD_FOLDED && c->method != DEMOD_METHOD_FFT)
         return DEMOD_UNIMPLEMENTED;
+    if (c->method == DEMOD_METHOD_FFT && c->n != 1024) return DEMOD_UNIMPLEMENTED;
     if (c->reserved != 0) return DEMOD_BAD_ARG;
     if (c->method == DEMOD_METHOD_FOLDED && !fold_eligible(*c)) return DEMOD_BAD_ARG;
     for (uint32_t i = 0; i < c->k; ++i)
@@ -136,6 +140,27 @@ static int init_device_state(demod_t *st)
                                                         c.k >= 3))
                        ? kDetFolded
                        : kDetGoertzel;
+    if (c.method == DEMOD_METHOD_FFT) {
+        st->detector = kDetFft;
+        std::vector<float> t1(1024), t2(1024);
+        for (int m = 0; m < 512; ++m) {
+            t1[2 * m] = (float)std::cos(-2.0 * M_PI * m / 512.0);
+            t1[2 * m + 1] = (float)std::sin(-2.0 * M_PI * m / 512.0);
+            t2[2 * m] = (float)std::cos(-2.0 * M_PI * m / 1024.0);
+            t2[2 * m + 1] = (float)std::sin(-2.0 * M_PI * m / 1024.0);
+        }
+        std::vector<int> bins(c.k);
+        for (uint32_t k = 0; k < c.k; ++k) {
+            long b = std::lround(c.freqs[k] * c.n / c.fs);
+            bins[k] = (int)std::min<long>(std::max<long>(b, 0), c.n / 2);
+        }
+        HIP_TRY(hipMalloc(&st->d_tw512, t1.size() * sizeof(float)));
+        HIP_TRY(hipMalloc(&st->d_tw1024, t2.size() * sizeof(float)));
+        HIP_TRY(hipMalloc(&st->d_bins, bins.size() * sizeof(int)));
+        HIP_TRY(hipMemcpy(st->d_tw512, t1.data(), t1.size() * sizeof(float), hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(st->d_tw1024, t2.data(), t2.size() * sizeof(float), hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(st->d_bins, bins.data(), bins.size() * sizeof(int), hipMemcpyHostToDevice));
+    }
     // Rotation of each lane's piece into window phase, X += A s1 - B s2:
     //   Goertzel: segment j = samples [64j, 64j+64): A = e^{-jw(64j+63)}, B = e^{-jw(64j+64)}
     //   Folded:   folded samples [8j, 8j+8):         A = e^{-jw(8j+7)},   B = e^{-jw(8j+8)}
@@ -159,6 +184,9 @@ static void free_state(demod_t *st)
 {
     if (st->stream) (void)hipStreamSynchronize(st->stream);
     if (st->d_rot) (void)hipFree(st->d_rot);
+    if (st->d_tw512) (void)hipFree(st->d_tw512);
+    if (st->d_tw1024) (void)hipFree(st->d_tw1024);
+    if (st->d_bins) (void)hipFree(st->d_bins);
     if (st->d_in) (void)hipFree(st->d_in);
     if (st->d_sym) (void)hipFree(st->d_sym);
     if (st->d_mag) (void)hipFree(st->d_mag);
@@ -212,7 +240,9 @@ int demod_reset(demod_t *st)
 int demod_method(const demod_t *st)
 {
     if (!st) return DEMOD_BAD_ARG;
-    return st->detector == kDetFolded ? DEMOD_METHOD_FOLDED : DEMOD_METHOD_GOERTZEL;
+    return st->detector == kDetFolded ? DEMOD_METHOD_FOLDED
+         : st->detector == kDetFft    ? DEMOD_METHOD_FFT
+                                      : DEMOD_METHOD_GOERTZEL;
 }
 
 int demod_pending(const demod_t *st)
@@ -234,11 +264,32 @@ int demod_max_symbols(const demod_t *st, size_t n_frames)
     return w > 0x7FFFFFFF ? 0x7FFFFFFF : (int)w;
 }
 
-// Enqueue the Goertzel kernel on device-resident windows.
+static int enqueue_fft(demod_t *st, const int16_t *d_pcm, size_t n_windows, uint8_t *d_sym,
+                       float *d_mag, float *d_spec, hipStream_t s)
+{
+    FftParams p;
+    std::memset(&p, 0, sizeof(p));
+    p.pcm = d_pcm;
+    p.n_windows = (long long)n_windows;
+    p.hop = st->cfg.hop;
+    p.k = (int)st->cfg.k;
+    p.xcd_swizzle = st->cfg.hop < st->cfg.n ? 1 : 0;  // overlapping windows: keep neighbours on one L2
+    p.tw512 = st->d_tw512;
+    p.tw1024 = st->d_tw1024;
+    p.bins = st->d_bins;
+    p.sym = d_sym;
+    p.mag = d_mag;
+    p.spec = d_spec;
+    HIP_TRY(launch_fft(p, s));
+    return (int)n_windows;
+}
+
+// Enqueue the detector kernel on device-resident windows.
 static int enqueue_batch(demod_t *st, const int16_t *d_pcm, size_t n_windows, uint8_t *d_sym,
                          float *d_mag, hipStream_t s)
 {
     if (n_windows == 0) return 0;
+    if (st->detector == kDetFft) return enqueue_fft(st, d_pcm, n_windows, d_sym, d_mag, nullptr, s);
     GoertzelParams p;
     std::memset(&p, 0, sizeof(p));
     p.pcm = d_pcm;
@@ -362,6 +413,17 @@ int demod_batch_async(demod_t *st, const int16_t *d_pcm, size_t n_windows, uint8
     if (n_windows > 0x7FFFFFFF) return DEMOD_BAD_ARG;
     if (((uintptr_t)d_pcm & 15) != 0) return DEMOD_BAD_ARG;
     return enqueue_batch(st, d_pcm, n_windows, d_symbols, d_mags, (hipStream_t)stream);
+}
+
+int demod_batch_spectrum_async(demod_t *st, const int16_t *d_pcm, size_t n_windows,
+                               uint8_t *d_symbols, float *d_mags, float *d_spectrum, void *stream)
+{
+    if (!st || (!d_pcm && n_windows) || (!d_symbols && n_windows)) return DEMOD_BAD_ARG;
+    if (st->detector != kDetFft) return DEMOD_UNIMPLEMENTED;
+    if (n_windows > 0x7FFFFFFF) return DEMOD_BAD_ARG;
+    if (((uintptr_t)d_pcm & 15) != 0) return DEMOD_BAD_ARG;
+    if (n_windows == 0) return 0;
+    return enqueue_fft(st, d_pcm, n_windows, d_symbols, d_mags, d_spectrum, (hipStream_t)stream);
 }
 
 int demodulate_mags(demod_t *st, const int16_t *pcm, size_t n_frames, uint8_t *symbols,

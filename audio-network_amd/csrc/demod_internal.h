@@ -50,6 +50,21 @@ __device__ __forceinline__ long long tile_block(int swz)
     return (b % 8) * per + b / 8;
 }
 
+// Full-spectrum detector (fft.hip), n = 1024.
+struct FftParams {
+    const int16_t *pcm;
+    long long n_windows;
+    long long hop;           // samples, even
+    int k;
+    int xcd_swizzle;
+    const float *tw512;      // [512][2]  e^{-2 pi i m / 512}
+    const float *tw1024;     // [512][2]  e^{-2 pi i k / 1024}
+    const int *bins;         // [k] tone bins round(f n / fs), device
+    uint8_t *sym;
+    float *mag;              // [n_windows][k] or nullptr
+    float *spec;             // [n_windows][513] or nullptr
+};
+
 struct SynthParams {
     uint64_t seed;
     uint64_t w0;             // index of the first generated window in the stream
@@ -66,10 +81,12 @@ struct SynthParams {
 
 // Detectors (the kernels behind DEMOD_METHOD_*).
 constexpr int kDetGoertzel = 1;  // goertzel.hip: 64-sample lane segments
+constexpr int kDetFft = 2;       // fft.hip: 1024-point real FFT, argmax over tone bins
 constexpr int kDetFolded = 3;    // fold.hip: Goertzel on the N/8-folded window
 
 hipError_t launch_detector(int detector, const GoertzelParams &p, hipStream_t s);
 int tile_grid(long long n_windows, int log2g);
 hipError_t launch_synth(const SynthParams &p, hipStream_t s);
+hipError_t launch_fft(const FftParams &p, hipStream_t s);
 
 }  // namespace fskd

@@ -1,0 +1,197 @@
+// fft.hip — full-spectrum detector: per window a
+// 1024-point real FFT, |X[b]|^2 for b = 0..512, symbol = argmax over the tone
+// bins b_k = round(f_k N / fs) (ties -> lowest k). Oracle:
+// oracle/fsk_oracle.c:oracle_fft_demod (double radix-2 FFT).
+//
+// One wave per window, everything in registers + a wave-private LDS slice:
+//   * real -> complex packing z[n] = x[2n] + i x[2n+1] (n < 512); lane j loads
+//     z[j + 64 r], r = 0..7 — one coalesced 256-byte dword load per r, which is
+//     exactly the input layout of the first Stockham stage;
+//   * 512-point complex FFT as three radix-8 Stockham stages (Ns = 1, 8, 64;
+//     lane j = butterfly j), DFT-8 in registers, per-lane stage twiddles held
+//     in registers, LDS exchange between stages (in place: one wave's LDS
+//     operations complete in order);
+//   * real-FFT post-pass: X[k] = Xe + W_1024^k Xo, X[k+512] = Xe - W_1024^k Xo
+//     with Xe/Xo from Z[k] and conj(Z[512-k]) (mirror read from LDS);
+//   * |X|^2 to LDS, tone-bin gather, argmax; optional full-spectrum store.
+// Cost ~350 VALU + ~60 LDS ops per lane per window: compute-bound.
+#include <algorithm>
+
+#include "demod_internal.h"
+
+namespace fskd {
+
+struct cf {
+    float x, y;
+};
+
+__device__ __forceinline__ cf cadd(cf a, cf b) { return {a.x + b.x, a.y + b.y}; }
+__device__ __forceinline__ cf csub(cf a, cf b) { return {a.x - b.x, a.y - b.y}; }
+__device__ __forceinline__ cf cmul(cf a, cf w)
+{
+    return {fmaf(a.x, w.x, -a.y * w.y), fmaf(a.x, w.y, a.y * w.x)};
+}
+__device__ __forceinline__ cf mul_mj(cf a) { return {a.y, -a.x}; }  // * (-i)
+__device__ __forceinline__ cf mul_pj(cf a) { return {-a.y, a.x}; }  // * (+i)
+
+// In-register forward DFT-8: X[k] = sum_n v[n] e^{-2 pi i n k / 8}.
+__device__ __forceinline__ void dft8(cf v[8])
+{
+    const float h = 0.70710678118654752f;
+    // DFT-4 of evens (v0, v2, v4, v6) and odds (v1, v3, v5, v7)
+    cf e0 = cadd(v[0], v[4]), e1 = csub(v[0], v[4]), e2 = cadd(v[2], v[6]), e3 = csub(v[2], v[6]);
+    cf E0 = cadd(e0, e2), E2 = csub(e0, e2), E1 = cadd(e1, mul_mj(e3)), E3 = csub(e1, mul_mj(e3));
+    cf o0 = cadd(v[1], v[5]), o1 = csub(v[1], v[5]), o2 = cadd(v[3], v[7]), o3 = csub(v[3], v[7]);
+    cf O0 = cadd(o0, o2), O2 = csub(o0, o2), O1 = cadd(o1, mul_mj(o3)), O3 = csub(o1, mul_mj(o3));
+    // twiddles W8^k on the odd half: W8^1 = h(1 - i), W8^2 = -i, W8^3 = h(-1 - i)
+    cf T1 = {h * (O1.x + O1.y), h * (O1.y - O1.x)};
+    cf T2 = mul_mj(O2);
+    cf T3 = {h * (O3.y - O3.x), -h * (O3.x + O3.y)};
+    v[0] = cadd(E0, O0);
+    v[4] = csub(E0, O0);
+    v[1] = cadd(E1, T1);
+    v[5] = csub(E1, T1);
+    v[2] = cadd(E2, T2);
+    v[6] = csub(E2, T2);
+    v[3] = cadd(E3, T3);
+    v[7] = csub(E3, T3);
+}
+
+// Persistent waves: the twiddles a lane needs depend only on its lane index
+// (stage 1: W_512^{8 (j%8) r}, stage 2: W_512^{j r}, post-pass: W_1024^{j+64r}),
+// so they are loaded once into registers and the LDS carries only the data
+// exchange; the next window's 8 input dwords are prefetched during the current
+// window's FFT.
+template <int WPB = 4>
+__global__ __launch_bounds__(64 * WPB) void fft1024_kernel(FftParams p)
+{
+    __shared__ __attribute__((aligned(16))) cf zbuf[WPB][512];   // per-wave exchange slice
+    __shared__ float pbuf[WPB][516];                             // per-wave |X|^2
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    cf *z = zbuf[wave];
+    float *pw = pbuf[wave];
+    const cf *t512 = reinterpret_cast<const cf *>(p.tw512);
+    const cf *t1024 = reinterpret_cast<const cf *>(p.tw1024);
+    cf ta[8], tb[8], tc[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+        ta[r] = t512[(8 * (lane & 7) * r) & 511];
+        tb[r] = t512[(lane * r) & 511];
+        tc[r] = t1024[lane + 64 * r];
+    }
+
+    const long long stride = (long long)gridDim.x * WPB;
+    long long w = tile_block(p.xcd_swizzle) * WPB + wave;
+    uint32_t nx[8];
+    auto load_win = [&](long long ww) {
+        const uint32_t *xw = reinterpret_cast<const uint32_t *>(p.pcm + ww * p.hop);
+#pragma unroll
+        for (int r = 0; r < 8; ++r) nx[r] = __builtin_nontemporal_load(xw + lane + 64 * r);
+    };
+    if (w < p.n_windows) load_win(w);
+    for (; w < p.n_windows; w += stride) {
+        // stage-0 operands: z[j + 64 r] = (x[2(j+64r)], x[2(j+64r)+1])
+        cf v[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r)
+            v[r] = {(float)(int)(short)(nx[r] & 0xFFFFu), (float)((int)nx[r] >> 16)};
+        if (w + stride < p.n_windows) load_win(w + stride);
+        // stage 0 (Ns = 1): no twiddles; out[8 j + r] (64 contiguous bytes per lane)
+        dft8(v);
+        {
+            float4 *z4 = reinterpret_cast<float4 *>(z + 8 * lane);
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                z4[r] = make_float4(v[2 * r].x, v[2 * r].y, v[2 * r + 1].x, v[2 * r + 1].y);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // stage 1 (Ns = 8): in[j + 64 r] * W_512^{8 (j%8) r}; out[(j/8) 64 + j%8 + 8 r]
+#pragma unroll
+        for (int r = 0; r < 8; ++r) v[r] = z[lane + 64 * r];
+#pragma unroll
+        for (int r = 1; r < 8; ++r) v[r] = cmul(v[r], ta[r]);
+        dft8(v);
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        {
+            const int base = (lane >> 3) * 64 + (lane & 7);
+#pragma unroll
+            for (int r = 0; r < 8; ++r) z[base + 8 * r] = v[r];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // stage 2 (Ns = 64): in[j + 64 r] * W_512^{j r}; result Z[j + 64 r] stays in v
+#pragma unroll
+        for (int r = 0; r < 8; ++r) v[r] = z[lane + 64 * r];
+#pragma unroll
+        for (int r = 1; r < 8; ++r) v[r] = cmul(v[r], tb[r]);
+        dft8(v);
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int r = 0; r < 8; ++r) z[lane + 64 * r] = v[r];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // real post-pass: k = j + 64 r; Zm = conj(Z[(512 - k) mod 512])
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            const int k = lane + 64 * r;
+            const cf zm = z[(512 - k) & 511];
+            const cf xe = {0.5f * (v[r].x + zm.x), 0.5f * (v[r].y - zm.y)};
+            const cf d = {0.5f * (v[r].x - zm.x), 0.5f * (v[r].y + zm.y)};
+            const cf t = cmul(mul_mj(d), tc[r]);  // W_1024^k (Z - conj Zm) / (2i)
+            const cf X = cadd(xe, t);
+            pw[k] = fmaf(X.x, X.x, X.y * X.y);
+            if (r == 0 && lane == 0) {
+                const cf X512 = csub(xe, t);
+                pw[512] = fmaf(X512.x, X512.x, X512.y * X512.y);
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (p.spec) {
+            float *so = p.spec + w * 513;
+#pragma unroll
+            for (int r = 0; r < 8; ++r) so[lane + 64 * r] = pw[lane + 64 * r];
+            if (lane == 0) so[512] = pw[512];
+        }
+        float mine = lane < p.k ? pw[p.bins[lane]] : -1.f;
+        if (p.mag && lane < p.k) p.mag[w * p.k + lane] = mine;
+        // argmax over lanes 0..k-1, ties -> lowest index (k <= 16: one DPP row)
+        int arg = lane;
+        float best = mine;
+#pragma unroll
+        for (int off = 1; off < 16; off <<= 1) {
+            const float ob = __shfl_xor(best, off, 16);
+            const int oa = __shfl_xor(arg, off, 16);
+            if (ob > best || (ob == best && oa < arg)) { best = ob; arg = oa; }
+        }
+        if (lane == 0) p.sym[w] = (uint8_t)arg;
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+hipError_t launch_fft(const FftParams &p, hipStream_t s)
+{
+    constexpr int WPB = 4;
+    int dev = 0, cus = 256, per_cu = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fft1024_kernel<WPB>, 64 * WPB, 0) !=
+            hipSuccess || per_cu < 1)
+        per_cu = 1;
+    long long blocks = (p.n_windows + WPB - 1) / WPB;
+    blocks = std::min<long long>(blocks, (long long)cus * per_cu);
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(fft1024_kernel<WPB>, dim3((unsigned)blocks), dim3(64 * WPB), 0, s, p);
+    return hipGetLastError();
+}
+
+}  // namespace fskd

@@ -63,32 +63,42 @@ def pmc_traffic(config: str, windows: int):
         return None
 
 
-def cpu_baseline(A, d_pcm, d_sym, d_mag, freqs, seconds: float, threads: int):
-    """Oracle (C, OpenMP) on a bounded sample of the timed windows."""
+def cpu_baseline(A, d_pcm, d_sym, d_mag, freqs, seconds: float, threads: int, fft: bool,
+                 hop: int):
+    """Oracle (C, OpenMP) on a bounded sample of the timed windows: the first
+    S stream windows (Goertzel) or the FFT windows over the first S*n samples."""
     sys.path.insert(0, ROOT)
     from oracle import oracle as O
 
     n = 1024
-    S = min(d_pcm.shape[0], 65536)
-    pcm = d_pcm[:S].cpu().numpy()
-    gsym = d_sym[:S].cpu().numpy()
-    gmag = d_mag[:S].cpu().numpy().astype(np.float64) if d_mag is not None else None
-    sym, P = O.goertzel(pcm, freqs, n, threads=threads)  # warm + parity reference
+    S = min(d_pcm.shape[0], 4096 if fft else 65536)
+    flat = d_pcm[:S].cpu().numpy().reshape(-1)
+    n_win = (S * n - n) // hop + 1
+    gsym = d_sym[:n_win].cpu().numpy()
+    gmag = d_mag[:n_win].cpu().numpy().astype(np.float64) if d_mag is not None else None
+
+    def run():
+        if fft:
+            return O.fft_demod(flat, freqs, n, hop, threads=threads)
+        return O.goertzel(flat, freqs, n, hop, threads=threads)
+
+    sym, P = run()  # warm + parity reference
     passes, t0 = 0, time.perf_counter()
     while True:
-        O.goertzel(pcm, freqs, n, threads=threads)
+        run()
         passes += 1
         el = time.perf_counter() - t0
         if el >= seconds:
             break
     msps = passes * S * n / el / 1e6
-    parity = {"windows_checked": int(S), "symbol_mismatches": int((sym != gsym).sum())}
+    parity = {"windows_checked": int(n_win), "symbol_mismatches": int((sym != gsym).sum())}
     if gmag is not None:
         parity["max_rel_mag_err"] = float((np.abs(gmag - P).max(1) / P.max(1)).max())
+    what = ("double radix-2 FFT, argmax over tone bins" if fft else "double Goertzel")
     base = {"value": round(msps, 3), "unit": "Msamples/s", "cores": int(threads),
             "kind": "port",
-            "sample": f"first {S} windows (x{n} int16) of the timed batch, {passes} passes "
-                      f"in {el:.1f} s, oracle/fsk_oracle.c double Goertzel, OpenMP"}
+            "sample": f"first {S * n} samples ({n_win} windows, hop {hop}) of the timed batch, "
+                      f"{passes} passes in {el:.1f} s, oracle/fsk_oracle.c {what}, OpenMP"}
     return base, parity
 
 
@@ -97,9 +107,12 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", choices=["fsk2", "fsk8", "streams"], default="fsk2",
-                    help="fsk2 = configs[1] (default), fsk8 = configs[2], streams = configs[4]: "
-                         "1024 streams x 2048 windows sharded over ranks (strong scaling)")
+    ap.add_argument("--config", choices=["fsk2", "fsk8", "fft", "streams"], default="fsk2",
+                    help="fsk2 = configs[1] (default), fsk8 = configs[2], fft = configs[3]: "
+                         "sliding 1024-pt full-spectrum FFT (hop --hop) over the same stream, "
+                         "streams = configs[4]: 1024 streams x 2048 windows sharded over ranks "
+                         "(strong scaling)")
+    ap.add_argument("--hop", type=int, default=256, help="window advance for --config fft")
     ap.add_argument("--windows", type=int, default=1 << 20, help="windows per GPU (fsk2/fsk8)")
     ap.add_argument("--no-mags", action="store_true", help="symbols only")
     ap.add_argument("--method", choices=["auto", "goertzel", "folded"], default="auto")
@@ -132,14 +145,19 @@ def main():
     else:
         W = int(args.windows)
         w0, total_windows = rank * W, world * W
+    # windows the detector evaluates over the rank's W x n-sample stream slice
+    n_eval = (W * n - n) // hop + 1
     method = {"auto": A.METHOD_AUTO, "goertzel": A.METHOD_GOERTZEL,
               "folded": A.METHOD_FOLDED}[args.method]
-    cfg = A.make_cfg(freqs=freqs, n=n, device=local, method=method)
+    hop = n
+    if args.config == "fft":
+        method, hop = A.METHOD_FFT, int(args.hop)
+    cfg = A.make_cfg(freqs=freqs, n=n, hop=hop, device=local, method=method)
     dev = torch.device("cuda", local)
     d_pcm = torch.empty((W, n), dtype=torch.int16, device=dev)
     d_true = torch.empty(W, dtype=torch.uint8, device=dev)
-    d_sym = torch.empty(W, dtype=torch.uint8, device=dev)
-    d_mag = None if args.no_mags else torch.empty((W, K), dtype=torch.float32, device=dev)
+    d_sym = torch.empty(n_eval, dtype=torch.uint8, device=dev)
+    d_mag = None if args.no_mags else torch.empty((n_eval, K), dtype=torch.float32, device=dev)
     A.synth_fsk(cfg, A.BENCH_SEED, W, 8000, 400, d_pcm, d_true, w0=w0)
     torch.cuda.synchronize()
     demod = A.Demodulator(cfg)
@@ -149,7 +167,7 @@ def main():
     def step(ev=None):
         if ev is not None:
             ev[0].record(stream)
-        demod.batch_async(d_pcm, W, d_sym, d_mag, stream=stream.cuda_stream)
+        demod.batch_async(d_pcm, n_eval, d_sym, d_mag, stream=stream.cuda_stream)
         if ev is not None:
             ev[1].record(stream)
         if world > 1:
@@ -185,7 +203,12 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
 
     # correctness of the timed output: every symbol vs the transmitted one
-    sym_err = int((d_sym != d_true).sum().item())
+    # (sliding windows straddle two symbols: compare the aligned ones only)
+    if hop == n:
+        sym_err = int((d_sym != d_true).sum().item())
+    else:
+        step_w = n // hop
+        sym_err = int((d_sym[::step_w][:W] != d_true).sum().item())
     framed = None
     if world > 1:
         all_true = D.gather_symbols(d_true, gunits, world, unit=gunit)
@@ -198,9 +221,9 @@ def main():
                       "roundtrip_ok": bool((back == all_sym.cpu().numpy()).all())}
 
     if rank == 0:
-        samples = total_windows * n
+        samples = total_windows * n  # stream samples demodulated (each counted once)
         value = samples / (ms_per_step / 1e3) / 1e6
-        alg_bytes = W * (2 * n + 1 + (0 if args.no_mags else 4 * K))
+        alg_bytes = W * 2 * n + n_eval * (1 + (0 if args.no_mags else 4 * K))
         achieved = alg_bytes / (kernel_ms / 1e3) / 1e9
         out = {
             "metric": METRIC,
@@ -220,16 +243,20 @@ def main():
                 "workload": ("configs[4]: 1024 streams x 2048 windows (2^21 samples each), "
                              f"sharded by stream over {world} GPU(s), 2-FSK"
                              if args.config == "streams" else
+                             f"configs[3]: sliding 1024-pt full-spectrum FFT, hop {hop}, "
+                             f"{n_eval} windows over a {W * n}-sample int16 stream per GPU"
+                             if args.config == "fft" else
                              ("configs[1]: 2-FSK" if K == 2 else "configs[2]: 8-FSK")
                              + f" Goertzel, {W} x {n}-sample int16 windows per GPU, HBM-resident"),
                 "tones_hz": list(freqs),
-                "windows_per_gpu": W,
+                "windows_per_gpu": n_eval,
+                "hop": hop,
                 "n": n,
                 "outputs": "symbols" + ("" if args.no_mags else " + |X_k|^2"),
                 "parallelism": f"dp{world} (independent window shards, RCCL symbol all-gather)",
             },
-            "detector": {A.METHOD_GOERTZEL: "goertzel", A.METHOD_FOLDED: "folded"}.get(
-                demod.method, str(demod.method)),
+            "detector": {A.METHOD_GOERTZEL: "goertzel", A.METHOD_FOLDED: "folded",
+                         A.METHOD_FFT: "fft1024"}.get(demod.method, str(demod.method)),
             "kernel_ms_p10_p50_p90": [round(float(np.percentile(kts, q)), 4) for q in (10, 50, 90)],
             "symbol_errors": sym_err,
             "symbol_error_rate": sym_err / float(total_windows),
@@ -242,15 +269,17 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBPS, 4),
                 "traffic": pmc_traffic(args.config, W),
                 "alg_bytes_per_launch": alg_bytes,
-                "kernel": ("fold_tile_kernel<%d,4>" if demod.method == A.METHOD_FOLDED
-                           else "goertzel_tile_kernel<%d,4>") % K,
+                "kernel": ("fft1024_kernel<4>" if demod.method == A.METHOD_FFT else
+                           ("fold_tile_kernel<%d,4>" if demod.method == A.METHOD_FOLDED
+                            else "goertzel_tile_kernel<%d,4>") % K),
             },
         }
         if framed:
             out["framing"] = framed
         if world == 1 and not args.no_cpu_baseline:
             threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-            base, parity = cpu_baseline(A, d_pcm, d_sym, d_mag, freqs, args.cpu_seconds, threads)
+            base, parity = cpu_baseline(A, d_pcm, d_sym, d_mag, freqs, args.cpu_seconds, threads,
+                                        args.config == "fft", hop)
             out["cpu_baseline"] = base
             out["parity_sample"] = parity
         print(json.dumps(out), flush=True)

@@ -60,7 +60,8 @@ extern "C" {
 /* detector selection */
 #define DEMOD_METHOD_AUTO      0 /* FOLDED when eligible and k >= 3, else GOERTZEL */
 #define DEMOD_METHOD_GOERTZEL  1 /* per-window Goertzel tone bank over all n samples */
-#define DEMOD_METHOD_FFT       2 /* full-spectrum n-point real FFT, argmax over tone bins */
+#define DEMOD_METHOD_FFT       2 /* full-spectrum n-point real FFT (n = 1024), argmax
+                                    over the tone bins round(f*n/fs) */
 #define DEMOD_METHOD_FOLDED    3 /* Goertzel over the window folded to n/8 samples:
                                     exact when every tone is on a multiple of 8
                                     bins (f*n/fs integer, divisible by 8) */
@@ -135,6 +136,15 @@ int demod_batch(demod_t *st, const int16_t *pcm, size_t n_windows,
  */
 int demod_batch_async(demod_t *st, const int16_t *d_pcm, size_t n_windows,
                       uint8_t *d_symbols, float *d_mags, void *stream);
+
+/*
+ * Full-spectrum variant of demod_batch_async for DEMOD_METHOD_FFT handles:
+ * additionally writes |X[b]|^2, b = 0..n/2, to d_spectrum[W][n/2 + 1]
+ * (nullable). Other handles return DEMOD_UNIMPLEMENTED.
+ */
+int demod_batch_spectrum_async(demod_t *st, const int16_t *d_pcm, size_t n_windows,
+                               uint8_t *d_symbols, float *d_mags, float *d_spectrum,
+                               void *stream);
 
 /* ---- ip.proto framing (ToReceiver{AudioData{bytes}}, delimited) ------- */
 

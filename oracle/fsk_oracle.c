@@ -228,6 +228,22 @@ int oracle_fft_demod(const int16_t *x, size_t n_windows, size_t hop,
     return 0;
 }
 
+int oracle_fft_demod_omp(const int16_t *x, size_t n_windows, size_t hop,
+                         uint32_t n, uint32_t k, const double *freqs, double fs,
+                         uint8_t *sym, double *P, int threads)
+{
+    int rc = 0;
+#ifdef _OPENMP
+    if (threads > 0) omp_set_num_threads(threads);
+#pragma omp parallel for schedule(static) reduction(| : rc)
+#endif
+    for (long w = 0; w < (long)n_windows; ++w)
+        rc |= oracle_fft_demod(x + (size_t)w * hop, 1, hop, n, k, freqs, fs,
+                               sym ? sym + w : NULL, P ? P + (size_t)w * k : NULL);
+    (void)threads;
+    return rc;
+}
+
 /* ------------------------------------------------------------------------ */
 /* Streaming demodulate(pcm, n): carry buffer of mono samples, one symbol per */
 /* complete window, advance by hop (the carry mirrors the   */

@@ -56,6 +56,10 @@ int oracle_fft_demod(const int16_t *x, size_t n_windows, size_t hop,
                      uint32_t n, uint32_t k, const double *freqs, double fs,
                      uint8_t *sym, double *P);
 
+int oracle_fft_demod_omp(const int16_t *x, size_t n_windows, size_t hop,
+                         uint32_t n, uint32_t k, const double *freqs, double fs,
+                         uint8_t *sym, double *P, int threads);
+
 /* Streaming restatement of demodulate(pcm, n). */
 typedef struct oracle_stream oracle_stream_t;
 oracle_stream_t *oracle_stream_create(uint32_t n, uint32_t hop,

@@ -52,6 +52,9 @@ def lib() -> ctypes.CDLL:
         L.oracle_fft_demod.argtypes = [_P, _SZ, _SZ, ctypes.c_uint32, ctypes.c_uint32, D,
                                        ctypes.c_double, _P, _P]
         L.oracle_fft_demod.restype = ctypes.c_int
+        L.oracle_fft_demod_omp.argtypes = [_P, _SZ, _SZ, ctypes.c_uint32, ctypes.c_uint32, D,
+                                           ctypes.c_double, _P, _P, ctypes.c_int]
+        L.oracle_fft_demod_omp.restype = ctypes.c_int
         L.oracle_stream_create.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                            ctypes.c_int, ctypes.c_uint32, D, ctypes.c_double]
         L.oracle_stream_create.restype = _P
@@ -131,14 +134,18 @@ def fft_power(x: np.ndarray) -> np.ndarray:
 
 
 def fft_demod(x: np.ndarray, freqs: Sequence[float], n: int, hop: Optional[int] = None,
-              fs: float = 48000.0):
+              fs: float = 48000.0, threads: int = 0):
     x = np.ascontiguousarray(x, np.int16).reshape(-1)
     hop = n if hop is None else hop
     W = 0 if x.size < n else (x.size - n) // hop + 1
     sym = np.empty(W, np.uint8)
     P = np.empty((W, len(freqs)), np.float64)
-    rc = lib().oracle_fft_demod(x.ctypes.data, W, hop, n, len(freqs), _freqs(freqs), fs,
-                                sym.ctypes.data, P.ctypes.data)
+    if threads:
+        rc = lib().oracle_fft_demod_omp(x.ctypes.data, W, hop, n, len(freqs), _freqs(freqs), fs,
+                                        sym.ctypes.data, P.ctypes.data, threads)
+    else:
+        rc = lib().oracle_fft_demod(x.ctypes.data, W, hop, n, len(freqs), _freqs(freqs), fs,
+                                    sym.ctypes.data, P.ctypes.data)
     if rc:
         raise ValueError(f"oracle_fft_demod: {rc}")
     return sym, P

@@ -11,6 +11,7 @@
 #include "../audio-network_amd/csrc/goertzel.hip"
 #include "../audio-network_amd/csrc/synth.hip"
 #include "../audio-network_amd/csrc/fold.hip"
+#include "../audio-network_amd/csrc/fft.hip"
 
 #include <algorithm>
 #include <cmath>
@@ -216,6 +217,46 @@ int main(int argc, char **argv)
     add_variant(vs, FDS(8, 4), 4, "fold NTS", f8, 8, cus, 1);
     add_variant(vs, FDS(8, 4), 4, "fold NTS XSWZ", f8s, 8, cus, 1);
     add_variant(vs, FD(8, 4), 4, "fold nomag", f8n, 8, cus, 1);
+    {
+        // FFT detector tables (2-FSK bins 32, 64)
+        std::vector<float> t1(1024), t2(1024);
+        for (int m = 0; m < 512; ++m) {
+            t1[2 * m] = (float)std::cos(-2 * M_PI * m / 512.0);
+            t1[2 * m + 1] = (float)std::sin(-2 * M_PI * m / 512.0);
+            t2[2 * m] = (float)std::cos(-2 * M_PI * m / 1024.0);
+            t2[2 * m + 1] = (float)std::sin(-2 * M_PI * m / 1024.0);
+        }
+        float *d1, *d2;
+        int *db;
+        int hb[2] = {32, 64};
+        CK(hipMalloc(&d1, 4096));
+        CK(hipMalloc(&d2, 4096));
+        CK(hipMalloc(&db, 8));
+        CK(hipMemcpy(d1, t1.data(), 4096, hipMemcpyHostToDevice));
+        CK(hipMemcpy(d2, t2.data(), 4096, hipMemcpyHostToDevice));
+        CK(hipMemcpy(db, hb, 8, hipMemcpyHostToDevice));
+        for (int hop : {1024, 256}) {
+            for (int swz : {0, 1}) {
+                FftParams fp{};
+                fp.pcm = pcm;
+                fp.hop = hop;
+                fp.n_windows = (W * 1024 - 1024) / hop + 1;
+                fp.k = 2;
+                fp.xcd_swizzle = swz;
+                fp.tw512 = d1;
+                fp.tw1024 = d2;
+                fp.bins = db;
+                CK(hipMalloc(&fp.sym, fp.n_windows));
+                CK(hipMalloc(&fp.mag, fp.n_windows * 8));
+                Variant v;
+                v.name = "fft1024 K=2 hop=" + std::to_string(hop) + " swz=" + std::to_string(swz) +
+                         " windows=" + std::to_string(fp.n_windows);
+                v.bytes = (double)W * 2048 + fp.n_windows * 9.0;  // stream bytes read once
+                v.run = [fp](hipStream_t s) { CK(launch_fft(fp, s)); };
+                vs.push_back(v);
+            }
+        }
+    }
     {
         Variant v;
         v.name = "read-only one-shot tile (8 KiB/wave, nt)";

@@ -51,6 +51,12 @@ def test_create_rejects_bad_config(A, bad):
     assert e.value.code == A.DEMOD_BAD_ARG
 
 
+def test_fft_detector_needs_n1024(A):
+    with pytest.raises(A.DemodError) as e:
+        A.Demodulator(n=512, method=A.METHOD_FFT)
+    assert e.value.code == A.DEMOD_UNIMPLEMENTED
+
+
 def test_create_without_gpu_fails_loudly(A):
     torch = pytest.importorskip("torch")
     if torch.cuda.is_available():

@@ -279,3 +279,80 @@ def test_golden_stereo_stream_on_gpu(A, torch):
         mag = np.concatenate([o[1] for o in out])
         assert (sym == g[f"sym_mode{mode}"]).all()
         assert rel_err(mag, g[f"P_mode{mode}"]) <= MAG_TOL
+
+
+# ---- full-spectrum FFT detector (config 4) ---------------------------------
+FFT = 2
+
+
+def _spec_err(spec, ref):
+    return float((np.abs(spec.astype(np.float64) - ref).max(axis=1) / ref.max(axis=1)).max())
+
+
+@pytest.mark.parametrize("freqs,hop,W", [("FSK2_FREQS", 1024, 1000), ("FSK8_FREQS", 1024, 777),
+                                         ("FSK2_FREQS", 256, 200), ("FSK8_FREQS", 256, 130),
+                                         ("FSK2_FREQS", 8, 3), ("FSK8_FREQS", 1000, 64)])
+def test_fft_detector_matches_oracle(A, O, torch, freqs, hop, W):
+    f = getattr(A, freqs)
+    pcm, truth = O.synth_fsk(f, 1024, W, 31 + hop, 8000, 400)
+    flat = pcm.reshape(-1)
+    Wh = (flat.size - 1024) // hop + 1
+    with A.Demodulator(freqs=f, hop=hop, method=FFT) as d:
+        assert d.method == FFT
+        sym, mag = d.batch(flat, n_windows=Wh, mags=True)
+        # full spectrum on device
+        d_pcm = torch.from_numpy(flat.copy()).cuda()
+        d_sym = torch.empty(Wh, dtype=torch.uint8, device="cuda")
+        d_spec = torch.empty((Wh, 513), dtype=torch.float32, device="cuda")
+        d.batch_spectrum_async(d_pcm, Wh, d_sym, None, d_spec)
+        torch.cuda.synchronize()
+    ref_sym, ref_P = O.fft_demod(flat, f, 1024, hop)
+    assert (sym == ref_sym).all()
+    assert (d_sym.cpu().numpy() == ref_sym).all()
+    assert rel_err(mag, ref_P) <= MAG_TOL
+    # integer bins: the FFT detector computes the same |X_k|^2 as the Goertzel bank
+    gs, gP = O.goertzel(flat, f, 1024, hop, Wh)
+    assert (sym == gs).all()
+    idx = np.arange(0, Wh, max(1, Wh // 64))
+    full = np.stack([O.fft_power(flat[i * hop:i * hop + 1024]) for i in idx])
+    assert _spec_err(d_spec.cpu().numpy()[idx], full) <= MAG_TOL
+    if hop == 1024:
+        assert (sym == truth).mean() > 0.999
+
+
+def test_fft_detector_noninteger_tones_pick_nearest_bin(A, O, torch):
+    f = (612.3, 2471.9, 5003.3, 9100.0, 15777.7)
+    pcm, _ = O.synth_fsk(f, 1024, 300, 5, 8000, 400)
+    with A.Demodulator(freqs=f, method=FFT) as d:
+        sym, mag = d.batch(pcm, mags=True)
+    ref_sym, ref_P = O.fft_demod(pcm, f, 1024)
+    assert (sym == ref_sym).all()
+    assert rel_err(mag, ref_P) <= MAG_TOL
+
+
+def test_fft_detector_extremes_and_streaming(A, O, torch):
+    n = 1024
+    x = np.zeros((5, n), np.int16)
+    x[1] = 32767
+    x[2, ::2] = 32767
+    x[2, 1::2] = -32768
+    x[3] = np.random.default_rng(9).integers(-32768, 32768, n)
+    x[4] = np.round(32767 * np.cos(2 * np.pi * 64 * np.arange(n) / n))
+    with A.Demodulator(freqs=A.FSK2_FREQS, method=FFT) as d:
+        d_pcm = torch.from_numpy(x.reshape(-1).copy()).cuda()
+        d_sym = torch.empty(5, dtype=torch.uint8, device="cuda")
+        d_spec = torch.empty((5, 513), dtype=torch.float32, device="cuda")
+        d.batch_spectrum_async(d_pcm, 5, d_sym, None, d_spec)
+        torch.cuda.synchronize()
+        spec = d_spec.cpu().numpy()
+        assert (spec[0] == 0).all() and d_sym[0].item() == 0
+        full = np.stack([O.fft_power(x[i]) for i in range(1, 5)])
+        # DC and Nyquist carry all the energy in rows 1, 2: error relative to the peak bin
+        assert _spec_err(spec[1:], full) <= MAG_TOL
+        # streaming entry point through the FFT detector
+        L, _ = O.synth_fsk(A.FSK8_FREQS, n, 12, 3)
+    with A.Demodulator(freqs=A.FSK8_FREQS, method=FFT) as d:
+        got = np.concatenate([d.demodulate(L.reshape(-1)[i:i + 2880])
+                              for i in range(0, L.size, 2880)])
+    ref, _ = O.fft_demod(L.reshape(-1), A.FSK8_FREQS, n)
+    assert (got == ref).all()

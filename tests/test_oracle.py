@@ -153,3 +153,10 @@ def test_stream_oracle_sliding(O):
     got = np.concatenate([st.push(flat[i:i + 700])[0] for i in range(0, flat.size, 700)])
     want, _ = O.goertzel(flat, (1500.0, 3000.0), 1024, 256)
     assert (got == want).all()
+
+
+def test_fft_demod_omp_equals_serial(O):
+    pcm, _ = O.synth_fsk((1500.0, 3000.0), 1024, 20, 12)
+    a = O.fft_demod(pcm, (1500.0, 3000.0), 1024, 256)
+    b = O.fft_demod(pcm, (1500.0, 3000.0), 1024, 256, threads=4)
+    assert (a[0] == b[0]).all() and np.array_equal(a[1], b[1])
