@@ -136,6 +136,11 @@ def main():
     freqs = A.FSK8_FREQS if args.config == "fsk8" else A.FSK2_FREQS
     K = len(freqs)
     n = 1024
+    method = {"auto": A.METHOD_AUTO, "goertzel": A.METHOD_GOERTZEL,
+              "folded": A.METHOD_FOLDED}[args.method]
+    hop = n
+    if args.config == "fft":
+        method, hop = A.METHOD_FFT, int(args.hop)
     if args.config == "streams":
         # config 5: 1024 independent streams x 2^21 samples (2048 windows each);
         # rank r demodulates the contiguous stream shard D.shard_range(1024, r, N)
@@ -147,11 +152,6 @@ def main():
         w0, total_windows = rank * W, world * W
     # windows the detector evaluates over the rank's W x n-sample stream slice
     n_eval = (W * n - n) // hop + 1
-    method = {"auto": A.METHOD_AUTO, "goertzel": A.METHOD_GOERTZEL,
-              "folded": A.METHOD_FOLDED}[args.method]
-    hop = n
-    if args.config == "fft":
-        method, hop = A.METHOD_FFT, int(args.hop)
     cfg = A.make_cfg(freqs=freqs, n=n, hop=hop, device=local, method=method)
     dev = torch.device("cuda", local)
     d_pcm = torch.empty((W, n), dtype=torch.int16, device=dev)

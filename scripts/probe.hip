@@ -113,6 +113,7 @@ static void add_variant(std::vector<Variant> &vs, const void *f, int wpb, const 
 #define FDL(K, WPB) reinterpret_cast<const void *>(&fold_tile_kernel<K, 4, true, WPB, true>)
 #define FDS(K, WPB) reinterpret_cast<const void *>(&fold_tile_kernel<K, 4, true, WPB, false, true>)
 #define GZS(K) reinterpret_cast<const void *>(&goertzel_tile_kernel<K, 4, 1, true, 4, false, true>)
+#define GZP(K) reinterpret_cast<const void *>(&goertzel_tile_kernel<K, 4, 1, true, 4, false, false, true>)
 
 int main(int argc, char **argv)
 {
@@ -208,14 +209,13 @@ int main(int argc, char **argv)
     p2s.xcd_swizzle = f2s.xcd_swizzle = f8s.xcd_swizzle = 1;
     p2n.mag = f8n.mag = nullptr;
     add_variant(vs, GZ(2, 1, true, 4, false), 4, "goertzel [default]", p2, 2, cus, 1);
-    add_variant(vs, GZS(2), 4, "goertzel NTS", p2, 2, cus, 1);
-    add_variant(vs, GZ(2, 1, true, 4, false), 4, "goertzel XSWZ", p2s, 2, cus, 1);
-    add_variant(vs, GZ(2, 1, true, 4, false), 4, "goertzel nomag", p2n, 2, cus, 1);
+    add_variant(vs, GZP(2), 4, "goertzel PK", p2, 2, cus, 1);
     add_variant(vs, FD(2, 4), 4, "fold", f2, 2, cus, 1);
-    add_variant(vs, FDS(2, 4), 4, "fold NTS", f2, 2, cus, 1);
-    add_variant(vs, FD(8, 4), 4, "fold [default]", f8, 8, cus, 1);
-    add_variant(vs, FDS(8, 4), 4, "fold NTS", f8, 8, cus, 1);
-    add_variant(vs, FDS(8, 4), 4, "fold NTS XSWZ", f8s, 8, cus, 1);
+    add_variant(vs, GZ(4, 1, true, 4, false), 4, "goertzel [default]", p8, 4, cus, 1);
+    add_variant(vs, GZP(4), 4, "goertzel PK", p8, 4, cus, 1);
+    add_variant(vs, GZ(8, 1, true, 4, false), 4, "goertzel [default]", p8, 8, cus, 1);
+    add_variant(vs, GZP(8), 4, "goertzel PK", p8, 8, cus, 1);
+    add_variant(vs, FD(8, 4), 4, "fold", f8, 8, cus, 1);
     add_variant(vs, FD(8, 4), 4, "fold nomag", f8n, 8, cus, 1);
     {
         // FFT detector tables (2-FSK bins 32, 64)
