@@ -289,6 +289,7 @@ static int enqueue_batch(demod_t *st, const int16_t *d_pcm, size_t n_windows, ui
                          float *d_mag, hipStream_t s)
 {
     if (n_windows == 0) return 0;
+    HIP_TRY(hipSetDevice(st->device));
     if (st->detector == kDetFft) return enqueue_fft(st, d_pcm, n_windows, d_sym, d_mag, nullptr, s);
     GoertzelParams p;
     std::memset(&p, 0, sizeof(p));
@@ -423,6 +424,7 @@ int demod_batch_spectrum_async(demod_t *st, const int16_t *d_pcm, size_t n_windo
     if (n_windows > 0x7FFFFFFF) return DEMOD_BAD_ARG;
     if (((uintptr_t)d_pcm & 15) != 0) return DEMOD_BAD_ARG;
     if (n_windows == 0) return 0;
+    HIP_TRY(hipSetDevice(st->device));
     return enqueue_fft(st, d_pcm, n_windows, d_symbols, d_mags, d_spectrum, (hipStream_t)stream);
 }
 

@@ -119,6 +119,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
+                    help="nccl (= RCCL over xGMI) on the real node; gloo only to rehearse the "
+                         "multi-rank path with several ranks sharing one GPU")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -126,11 +129,16 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
 
+    if args.dist_backend == "gloo":
+        local = local % torch.cuda.device_count()  # rehearsal: ranks may share a GPU
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
 
     A, D = load_pkg()
     freqs = A.FSK8_FREQS if args.config == "fsk8" else A.FSK2_FREQS
@@ -161,18 +169,48 @@ def main():
     A.synth_fsk(cfg, A.BENCH_SEED, W, 8000, 400, d_pcm, d_true, w0=w0)
     torch.cuda.synchronize()
     demod = A.Demodulator(cfg)
-    stream = torch.cuda.current_stream()
+    main = torch.cuda.current_stream()
     gunits, gunit = (n_streams, wps) if args.config == "streams" else (world, W)
+    # N > 1: kernels run on a compute stream into double-buffered symbol slots;
+    # the RCCL gather of step t-1's symbols is issued on the default stream
+    # (waiting only for step t-1's kernel) and so overlaps step t's kernel.
+    comp = torch.cuda.Stream(device=dev) if world > 1 else main
+    slots = [d_sym, torch.empty_like(d_sym)] if world > 1 else [d_sym]
+    kdone = [torch.cuda.Event() for _ in slots]   # kernel wrote the slot
+    gdone = [torch.cuda.Event() for _ in slots]   # gather finished reading the slot
+    st = {"i": 0, "prev": None, "used": [False] * len(slots)}
+
+    def gather(slot):
+        main.wait_event(kdone[slot])
+        out = D.gather_symbols(slots[slot], gunits, world, unit=gunit)
+        gdone[slot].record(main)
+        return out
 
     def step(ev=None):
+        slot = st["i"] % len(slots)
+        st["i"] += 1
+        if st["used"][slot]:
+            comp.wait_event(gdone[slot])
         if ev is not None:
-            ev[0].record(stream)
-        demod.batch_async(d_pcm, n_eval, d_sym, d_mag, stream=stream.cuda_stream)
+            ev[0].record(comp)
+        demod.batch_async(d_pcm, n_eval, slots[slot], d_mag, stream=comp.cuda_stream)
         if ev is not None:
-            ev[1].record(stream)
+            ev[1].record(comp)
+        out = None
         if world > 1:
-            return D.gather_symbols(d_sym, gunits, world, unit=gunit)
-        return None
+            kdone[slot].record(comp)
+            if st["prev"] is not None:
+                out = gather(st["prev"])
+            st["prev"] = slot
+            st["used"][slot] = True
+        return out
+
+    def flush():
+        out = None
+        if world > 1 and st["prev"] is not None:
+            out = gather(st["prev"])
+            st["prev"] = None
+        return out
 
     # Sustained HBM streaming shows a power-management transient: launch
     # times rise ~25 % after ~10 launches and settle back by ~60 (dispatch
@@ -181,15 +219,16 @@ def main():
     warmup = max(args.warmup, MIN_WARMUP)
     for _ in range(warmup):
         step()
+    flush()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
            for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    all_sym = None
     for i in range(args.steps):
-        all_sym = step(evs[i])
+        step(evs[i])
+    all_sym = flush()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -204,6 +243,7 @@ def main():
 
     # correctness of the timed output: every symbol vs the transmitted one
     # (sliding windows straddle two symbols: compare the aligned ones only)
+    d_sym = slots[(st["i"] - 1) % len(slots)]
     if hop == n:
         sym_err = int((d_sym != d_true).sum().item())
     else:
