@@ -13,7 +13,8 @@
 //     operations complete in order);
 //   * real-FFT post-pass: X[k] = Xe + W_1024^k Xo, X[k+512] = Xe - W_1024^k Xo
 //     with Xe/Xo from Z[k] and conj(Z[512-k]) (mirror read from LDS);
-//   * |X|^2 to LDS, tone-bin gather, argmax; optional full-spectrum store.
+//   * |X|^2 stays in registers: tone bins are read lane-to-scalar (readlane),
+//     argmax in scalars; optional full-spectrum store straight from registers.
 // Cost ~350 VALU + ~60 LDS ops per lane per window: compute-bound.
 #include <algorithm>
 
@@ -66,11 +67,9 @@ template <int WPB = 4>
 __global__ __launch_bounds__(64 * WPB) void fft1024_kernel(FftParams p)
 {
     __shared__ __attribute__((aligned(16))) cf zbuf[WPB][512];   // per-wave exchange slice
-    __shared__ float pbuf[WPB][516];                             // per-wave |X|^2
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     cf *z = zbuf[wave];
-    float *pw = pbuf[wave];
     const cf *t512 = reinterpret_cast<const cf *>(p.tw512);
     const cf *t1024 = reinterpret_cast<const cf *>(p.tw1024);
     cf ta[8], tb[8], tc[8];
@@ -138,6 +137,8 @@ __global__ __launch_bounds__(64 * WPB) void fft1024_kernel(FftParams p)
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         // real post-pass: k = j + 64 r; Zm = conj(Z[(512 - k) mod 512])
+        float pr[8];
+        float p512 = 0.f;
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
             const int k = lane + 64 * r;
@@ -146,31 +147,33 @@ __global__ __launch_bounds__(64 * WPB) void fft1024_kernel(FftParams p)
             const cf d = {0.5f * (v[r].x - zm.x), 0.5f * (v[r].y + zm.y)};
             const cf t = cmul(mul_mj(d), tc[r]);  // W_1024^k (Z - conj Zm) / (2i)
             const cf X = cadd(xe, t);
-            pw[k] = fmaf(X.x, X.x, X.y * X.y);
-            if (r == 0 && lane == 0) {
-                const cf X512 = csub(xe, t);
-                pw[512] = fmaf(X512.x, X512.x, X512.y * X512.y);
+            pr[r] = fmaf(X.x, X.x, X.y * X.y);
+            if (r == 0) {
+                const cf X512 = csub(xe, t);  // meaningful in lane 0 (k = 0)
+                p512 = fmaf(X512.x, X512.x, X512.y * X512.y);
             }
         }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         if (p.spec) {
             float *so = p.spec + w * 513;
 #pragma unroll
-            for (int r = 0; r < 8; ++r) so[lane + 64 * r] = pw[lane + 64 * r];
-            if (lane == 0) so[512] = pw[512];
+            for (int r = 0; r < 8; ++r) so[lane + 64 * r] = pr[r];
+            if (lane == 0) so[512] = p512;
         }
-        float mine = lane < p.k ? pw[p.bins[lane]] : -1.f;
-        if (p.mag && lane < p.k) p.mag[w * p.k + lane] = mine;
-        // argmax over lanes 0..k-1, ties -> lowest index (k <= 16: one DPP row)
-        int arg = lane;
-        float best = mine;
+        // Tone-bin powers: bin b lives in lane b & 63, register b >> 6 (bin
+        // 512 in lane 0's p512); read them into scalars, argmax (ties -> lowest).
+        float best = -1.f;
+        int arg = 0;
+        for (int i = 0; i < p.k; ++i) {
+            const int b = __builtin_amdgcn_readfirstlane(p.bins[i]);
+            float sel = p512;
+            const int rr = b >> 6;
 #pragma unroll
-        for (int off = 1; off < 16; off <<= 1) {
-            const float ob = __shfl_xor(best, off, 16);
-            const int oa = __shfl_xor(arg, off, 16);
-            if (ob > best || (ob == best && oa < arg)) { best = ob; arg = oa; }
+            for (int r = 0; r < 8; ++r)
+                if (rr == r) sel = pr[r];
+            const float pk = __int_as_float(
+                __builtin_amdgcn_readlane(__float_as_int(sel), b == 512 ? 0 : (b & 63)));
+            if (p.mag && lane == i) p.mag[w * p.k + i] = pk;
+            if (pk > best) { best = pk; arg = i; }
         }
         if (lane == 0) p.sym[w] = (uint8_t)arg;
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");

@@ -1,0 +1,28 @@
+"""configs[0]: the native host C test (tests/native/config1.c) — one 1024-sample
+2-FSK buffer through the oracle, the C ABI and the frame codec."""
+import os
+import subprocess
+
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+NATIVE = os.path.join(HERE, "native")
+
+
+def _build_and_run():
+    subprocess.run(["make", "-C", NATIVE, "-s"], check=True, capture_output=True)
+    return subprocess.run([os.path.join(NATIVE, "config1")], capture_output=True, text=True,
+                          timeout=120)
+
+
+def test_config1_native_host_build():
+    r = _build_and_run()
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "config1 OK" in r.stdout
+
+
+@pytest.mark.gpu
+def test_config1_native_gpu_branch():
+    r = _build_and_run()
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "gpu demodulate: symbol" in r.stdout
