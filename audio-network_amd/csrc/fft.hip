@@ -58,26 +58,49 @@ __device__ __forceinline__ void dft8(cf v[8])
     v[7] = csub(E3, T3);
 }
 
+// Physical LDS slot of logical element e of the 512-point exchange buffer:
+// XOR-swizzle the pair index inside each 8-element block with bits 4-5 of e
+// (stage-0 ds_write_b128: lanes 64 B apart -> 8 distinct 16-byte bank slots)
+// and pad each 64-element row by 8 elements (stage-1 ds_write_b64: lanes 512 B
+// apart land on the other half of the banks). Measured before: 537M bank
+// conflict cycles per 4M-window dispatch (SQ_LDS_BANK_CONFLICT), more than the
+// 399M active LDS cycles.
+__device__ __forceinline__ int zi(int e)
+{
+    return 8 * (e >> 6) + ((e & ~7) | ((((e >> 1) & 3) ^ ((e >> 4) & 3)) << 1) | (e & 1));
+}
+
 // Persistent waves: the twiddles a lane needs depend only on its lane index
 // (stage 1: W_512^{8 (j%8) r}, stage 2: W_512^{j r}, post-pass: W_1024^{j+64r}),
 // so they are loaded once into registers and the LDS carries only the data
 // exchange; the next window's 8 input dwords are prefetched during the current
 // window's FFT.
-template <int WPB = 4>
+// TWLDS: stage-1 and post-pass twiddles from block LDS tables instead of
+// registers (-30 VGPRs: more waves per SIMD to hide the LDS round trips).
+template <int WPB = 4, bool TWLDS = false>
 __global__ __launch_bounds__(64 * WPB) void fft1024_kernel(FftParams p)
 {
-    __shared__ __attribute__((aligned(16))) cf zbuf[WPB][512];   // per-wave exchange slice
+    __shared__ __attribute__((aligned(16))) cf zbuf[WPB][576];   // per-wave exchange slice (padded)
+    __shared__ cf tws1[TWLDS ? 64 : 1];                            // W_512^{8 a b}, a,b < 8
+    __shared__ cf tws3[TWLDS ? 512 : 1];                           // W_1024^k
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     cf *z = zbuf[wave];
     const cf *t512 = reinterpret_cast<const cf *>(p.tw512);
     const cf *t1024 = reinterpret_cast<const cf *>(p.tw1024);
-    cf ta[8], tb[8], tc[8];
+    cf ta[TWLDS ? 1 : 8], tb[8], tc[TWLDS ? 1 : 8];
+    if (TWLDS) {
+        for (int i = threadIdx.x; i < 512; i += 64 * WPB) {
+            tws3[i] = t1024[i];
+            if (i < 64) tws1[i] = t512[(8 * (i >> 3) * (i & 7)) & 511];
+        }
+        __syncthreads();
+    }
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
-        ta[r] = t512[(8 * (lane & 7) * r) & 511];
+        if (!TWLDS) ta[TWLDS ? 0 : r] = t512[(8 * (lane & 7) * r) & 511];
         tb[r] = t512[(lane * r) & 511];
-        tc[r] = t1024[lane + 64 * r];
+        if (!TWLDS) tc[TWLDS ? 0 : r] = t1024[lane + 64 * r];
     }
 
     const long long stride = (long long)gridDim.x * WPB;
@@ -89,6 +112,17 @@ __global__ __launch_bounds__(64 * WPB) void fft1024_kernel(FftParams p)
         for (int r = 0; r < 8; ++r) nx[r] = __builtin_nontemporal_load(xw + lane + 64 * r);
     };
     if (w < p.n_windows) load_win(w);
+    // zi() of every access, as a few per-lane bases plus immediates (the
+    // swizzle only touches bits 1-2 within a 72-element padded row):
+    //   zi(j + 64 r)         = zl + 72 r
+    //   zi(8 j + 2 r)        = 72 (j/8) + 8 (j%8) + 2 (r ^ s)       s = (j/2)%4
+    //   zi(64(j/8)+j%8+8r)   = 72 (j/8) + j%2 + 8 r + 2 (s ^ r/2)
+    //   zi((512-j-64r)%512)  = zm0 + 72 (7 - r)   (j = 0, r = 0: slot 0)
+    const int sw = (lane >> 1) & 3;
+    const int zl = zi(lane);
+    const int row0 = 72 * (lane >> 3) + 8 * (lane & 7);
+    const int row1 = 72 * (lane >> 3) + (lane & 1);
+    const int zm0 = zi(64 - lane);
     for (; w < p.n_windows; w += stride) {
         // stage-0 operands: z[j + 64 r] = (x[2(j+64r)], x[2(j+64r)+1])
         cf v[8];
@@ -98,41 +132,37 @@ __global__ __launch_bounds__(64 * WPB) void fft1024_kernel(FftParams p)
         if (w + stride < p.n_windows) load_win(w + stride);
         // stage 0 (Ns = 1): no twiddles; out[8 j + r] (64 contiguous bytes per lane)
         dft8(v);
-        {
-            float4 *z4 = reinterpret_cast<float4 *>(z + 8 * lane);
 #pragma unroll
-            for (int r = 0; r < 4; ++r)
-                z4[r] = make_float4(v[2 * r].x, v[2 * r].y, v[2 * r + 1].x, v[2 * r + 1].y);
-        }
+        for (int r = 0; r < 4; ++r)
+            *reinterpret_cast<float4 *>(z + row0 + 2 * (r ^ sw)) =
+                make_float4(v[2 * r].x, v[2 * r].y, v[2 * r + 1].x, v[2 * r + 1].y);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         // stage 1 (Ns = 8): in[j + 64 r] * W_512^{8 (j%8) r}; out[(j/8) 64 + j%8 + 8 r]
 #pragma unroll
-        for (int r = 0; r < 8; ++r) v[r] = z[lane + 64 * r];
+        for (int r = 0; r < 8; ++r) v[r] = z[zl + 72 * r];
 #pragma unroll
-        for (int r = 1; r < 8; ++r) v[r] = cmul(v[r], ta[r]);
+        for (int r = 1; r < 8; ++r)
+            v[r] = cmul(v[r], TWLDS ? tws1[8 * (lane & 7) + r] : ta[TWLDS ? 0 : r]);
         dft8(v);
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         __builtin_amdgcn_wave_barrier();
-        {
-            const int base = (lane >> 3) * 64 + (lane & 7);
 #pragma unroll
-            for (int r = 0; r < 8; ++r) z[base + 8 * r] = v[r];
-        }
+        for (int r = 0; r < 8; ++r) z[row1 + 8 * r + 2 * (sw ^ (r >> 1))] = v[r];
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         // stage 2 (Ns = 64): in[j + 64 r] * W_512^{j r}; result Z[j + 64 r] stays in v
 #pragma unroll
-        for (int r = 0; r < 8; ++r) v[r] = z[lane + 64 * r];
+        for (int r = 0; r < 8; ++r) v[r] = z[zl + 72 * r];
 #pragma unroll
         for (int r = 1; r < 8; ++r) v[r] = cmul(v[r], tb[r]);
         dft8(v);
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
-        for (int r = 0; r < 8; ++r) z[lane + 64 * r] = v[r];
+        for (int r = 0; r < 8; ++r) z[zl + 72 * r] = v[r];
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -142,10 +172,10 @@ __global__ __launch_bounds__(64 * WPB) void fft1024_kernel(FftParams p)
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
             const int k = lane + 64 * r;
-            const cf zm = z[(512 - k) & 511];
+            const cf zm = z[r == 0 ? (lane == 0 ? 0 : zm0 + 504) : zm0 + 72 * (7 - r)];
             const cf xe = {0.5f * (v[r].x + zm.x), 0.5f * (v[r].y - zm.y)};
             const cf d = {0.5f * (v[r].x - zm.x), 0.5f * (v[r].y + zm.y)};
-            const cf t = cmul(mul_mj(d), tc[r]);  // W_1024^k (Z - conj Zm) / (2i)
+            const cf t = cmul(mul_mj(d), TWLDS ? tws3[k] : tc[TWLDS ? 0 : r]);  // W_1024^k (Z - conj Zm) / (2i)
             const cf X = cadd(xe, t);
             pr[r] = fmaf(X.x, X.x, X.y * X.y);
             if (r == 0) {
@@ -181,19 +211,27 @@ __global__ __launch_bounds__(64 * WPB) void fft1024_kernel(FftParams p)
     }
 }
 
+template <int WPB, bool TWLDS>
+hipError_t launch_fft_variant(const FftParams &p, hipStream_t s);
+
 hipError_t launch_fft(const FftParams &p, hipStream_t s)
 {
-    constexpr int WPB = 4;
+    return launch_fft_variant<4, false>(p, s);
+}
+
+template <int WPB, bool TWLDS>
+hipError_t launch_fft_variant(const FftParams &p, hipStream_t s)
+{
     int dev = 0, cus = 256, per_cu = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fft1024_kernel<WPB>, 64 * WPB, 0) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fft1024_kernel<WPB, TWLDS>, 64 * WPB, 0) !=
             hipSuccess || per_cu < 1)
         per_cu = 1;
     long long blocks = (p.n_windows + WPB - 1) / WPB;
     blocks = std::min<long long>(blocks, (long long)cus * per_cu);
     if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL(fft1024_kernel<WPB>, dim3((unsigned)blocks), dim3(64 * WPB), 0, s, p);
+    hipLaunchKernelGGL((fft1024_kernel<WPB, TWLDS>), dim3((unsigned)blocks), dim3(64 * WPB), 0, s, p);
     return hipGetLastError();
 }
 

@@ -57,9 +57,12 @@ __device__ __forceinline__ float group_sum(float v, int log2g)
 //   DIRECT  no LDS: each lane loads its own 128-byte segment (8 x 16 B;
 //           per instruction 64 lines, each fully consumed over the 8).
 //   NTS     non-temporal output stores.
-//   PK      pair tones into packed fp32 (v_pk_fma_f32 / v_pk_add_f32), K even.
+//   PK      pair tones into packed fp32 (v_pk_fma_f32 / v_pk_add_f32).
+//   SB      sched_barrier after every sample's K-tone step, so the K independent
+//           recurrences stay interleaved (hipcc otherwise serialises one tone's
+//           whole chain after another: issue-stall bound at large K).
 template <int K, int LOG2G, int PF = 1, bool NT = true, int WPB = kWavesPerBlock,
-          bool DIRECT = false, bool NTS = false, bool PK = false>
+          bool DIRECT = false, bool NTS = false, bool PK = false, bool SB = false>
 __global__ __launch_bounds__(64 * WPB) void goertzel_tile_kernel(GoertzelParams p)
 {
     static_assert(PF == 1 || PF == 2, "prefetch depth");
@@ -166,6 +169,7 @@ __global__ __launch_bounds__(64 * WPB) void goertzel_tile_kernel(GoertzelParams 
                         b2 = b1;
                         b1 = a;
                     }
+                    if (SB) __builtin_amdgcn_sched_barrier(0);
                 }
             }
 #pragma unroll
@@ -201,6 +205,7 @@ __global__ __launch_bounds__(64 * WPB) void goertzel_tile_kernel(GoertzelParams 
                     s2[k] = s1[k];
                     s1[k] = a;
                 }
+                if (SB) __builtin_amdgcn_sched_barrier(0);
             }
         }
         }

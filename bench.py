@@ -32,6 +32,7 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+VALU_PEAK_TFLOPS = 157.3  # MI355X fp32 vector peak (MI355X_MICROARCH.md)
 METRIC = "PCM Msamples/s demodulated + symbol-error-rate vs reference, 1/2/4/8 MI355X"
 MIN_WARMUP = 64
 
@@ -63,6 +64,16 @@ def pmc_traffic(config: str, windows: int):
         return None
 
 
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(A, d_pcm, d_sym, d_mag, freqs, seconds: float, threads: int, fft: bool,
                  hop: int):
     """Oracle (C, OpenMP) on a bounded sample of the timed windows: the first
@@ -82,21 +93,32 @@ def cpu_baseline(A, d_pcm, d_sym, d_mag, freqs, seconds: float, threads: int, ff
             return O.fft_demod(flat, freqs, n, hop, threads=threads)
         return O.goertzel(flat, freqs, n, hop, threads=threads)
 
+    def timed(fn, budget):
+        passes, t0 = 0, time.perf_counter()
+        while True:
+            fn()
+            passes += 1
+            el = time.perf_counter() - t0
+            if el >= budget:
+                return passes, el
+
     sym, P = run()  # warm + parity reference
-    passes, t0 = 0, time.perf_counter()
-    while True:
-        run()
-        passes += 1
-        el = time.perf_counter() - t0
-        if el >= seconds:
-            break
+    passes, el = timed(run, seconds)
     msps = passes * S * n / el / 1e6
+    # single-thread rate on a slice of the same sample (SURVEY §8d asks for both)
+    S1 = max(1, S // 16)
+    flat1 = flat[:S1 * n]
+    fn1 = ((lambda: O.fft_demod(flat1, freqs, n, hop, threads=1)) if fft else
+           (lambda: O.goertzel(flat1, freqs, n, hop, threads=1)))
+    p1, el1 = timed(fn1, max(1.0, seconds / 5))
+    msps1 = p1 * S1 * n / el1 / 1e6
     parity = {"windows_checked": int(n_win), "symbol_mismatches": int((sym != gsym).sum())}
     if gmag is not None:
         parity["max_rel_mag_err"] = float((np.abs(gmag - P).max(1) / P.max(1)).max())
     what = ("double radix-2 FFT, argmax over tone bins" if fft else "double Goertzel")
     base = {"value": round(msps, 3), "unit": "Msamples/s", "cores": int(threads),
-            "kind": "port",
+            "kind": "port", "single_thread_value": round(msps1, 3),
+            "host_cpu": cpu_model(), "host_cpus_visible": os.cpu_count(),
             "sample": f"first {S * n} samples ({n_win} windows, hop {hop}) of the timed batch, "
                       f"{passes} passes in {el:.1f} s, oracle/fsk_oracle.c {what}, OpenMP"}
     return base, parity
@@ -314,6 +336,16 @@ def main():
                             else "goertzel_tile_kernel<%d,4>") % K),
             },
         }
+        if args.config == "fft":
+            # the FFT is reported against the VALU roof too.
+            # Algorithmic flops per window: 2.5 N log2 N for the real N-point
+            # FFT + 3 per |X[b]|^2 over the N/2+1 bins.
+            fpw = 2.5 * n * 10 + 3 * (n // 2 + 1)
+            tf = fpw * n_eval / (kernel_ms / 1e3) / 1e12
+            out["roofline_valu"] = {"bound": "valu", "achieved": round(tf, 2),
+                                    "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
+                                    "frac": round(tf / VALU_PEAK_TFLOPS, 4),
+                                    "flop_per_window": fpw}
         if framed:
             out["framing"] = framed
         if world == 1 and not args.no_cpu_baseline:

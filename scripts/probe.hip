@@ -114,6 +114,8 @@ static void add_variant(std::vector<Variant> &vs, const void *f, int wpb, const 
 #define FDS(K, WPB) reinterpret_cast<const void *>(&fold_tile_kernel<K, 4, true, WPB, false, true>)
 #define GZS(K) reinterpret_cast<const void *>(&goertzel_tile_kernel<K, 4, 1, true, 4, false, true>)
 #define GZP(K) reinterpret_cast<const void *>(&goertzel_tile_kernel<K, 4, 1, true, 4, false, false, true>)
+#define GZPB(K) reinterpret_cast<const void *>(&goertzel_tile_kernel<K, 4, 1, true, 4, false, false, true, true>)
+#define GZB(K) reinterpret_cast<const void *>(&goertzel_tile_kernel<K, 4, 1, true, 4, false, false, false, true>)
 
 int main(int argc, char **argv)
 {
@@ -209,14 +211,14 @@ int main(int argc, char **argv)
     p2s.xcd_swizzle = f2s.xcd_swizzle = f8s.xcd_swizzle = 1;
     p2n.mag = f8n.mag = nullptr;
     add_variant(vs, GZ(2, 1, true, 4, false), 4, "goertzel [default]", p2, 2, cus, 1);
-    add_variant(vs, GZP(2), 4, "goertzel PK", p2, 2, cus, 1);
-    add_variant(vs, FD(2, 4), 4, "fold", f2, 2, cus, 1);
-    add_variant(vs, GZ(4, 1, true, 4, false), 4, "goertzel [default]", p8, 4, cus, 1);
-    add_variant(vs, GZP(4), 4, "goertzel PK", p8, 4, cus, 1);
-    add_variant(vs, GZ(8, 1, true, 4, false), 4, "goertzel [default]", p8, 8, cus, 1);
-    add_variant(vs, GZP(8), 4, "goertzel PK", p8, 8, cus, 1);
+    add_variant(vs, GZB(2), 4, "goertzel SB", p2, 2, cus, 1);
+    add_variant(vs, GZP(4), 4, "goertzel PK [default]", p8, 4, cus, 1);
+    add_variant(vs, GZPB(4), 4, "goertzel PK SB", p8, 4, cus, 1);
+    add_variant(vs, GZB(4), 4, "goertzel SB", p8, 4, cus, 1);
+    add_variant(vs, GZP(8), 4, "goertzel PK [default]", p8, 8, cus, 1);
+    add_variant(vs, GZPB(8), 4, "goertzel PK SB", p8, 8, cus, 1);
+    add_variant(vs, GZB(8), 4, "goertzel SB", p8, 8, cus, 1);
     add_variant(vs, FD(8, 4), 4, "fold", f8, 8, cus, 1);
-    add_variant(vs, FD(8, 4), 4, "fold nomag", f8n, 8, cus, 1);
     {
         // FFT detector tables (2-FSK bins 32, 64)
         std::vector<float> t1(1024), t2(1024);
@@ -236,23 +238,27 @@ int main(int argc, char **argv)
         CK(hipMemcpy(d2, t2.data(), 4096, hipMemcpyHostToDevice));
         CK(hipMemcpy(db, hb, 8, hipMemcpyHostToDevice));
         for (int hop : {1024, 256}) {
-            for (int swz : {0, 1}) {
+            for (int swz : {0, 1, 2, 3}) {
                 FftParams fp{};
                 fp.pcm = pcm;
                 fp.hop = hop;
                 fp.n_windows = (W * 1024 - 1024) / hop + 1;
                 fp.k = 2;
-                fp.xcd_swizzle = swz;
+                fp.xcd_swizzle = swz & 1;
                 fp.tw512 = d1;
                 fp.tw1024 = d2;
                 fp.bins = db;
                 CK(hipMalloc(&fp.sym, fp.n_windows));
                 CK(hipMalloc(&fp.mag, fp.n_windows * 8));
                 Variant v;
-                v.name = "fft1024 K=2 hop=" + std::to_string(hop) + " swz=" + std::to_string(swz) +
+                v.name = "fft1024 K=2 hop=" + std::to_string(hop) + " swz=" + std::to_string(swz & 1) +
+                         (swz & 2 ? " TWLDS" : "") +
                          " windows=" + std::to_string(fp.n_windows);
                 v.bytes = (double)W * 2048 + fp.n_windows * 9.0;  // stream bytes read once
-                v.run = [fp](hipStream_t s) { CK(launch_fft(fp, s)); };
+                if (swz & 2)
+                    v.run = [fp](hipStream_t s) { CK((launch_fft_variant<4, true>(fp, s))); };
+                else
+                    v.run = [fp](hipStream_t s) { CK(launch_fft(fp, s)); };
                 vs.push_back(v);
             }
         }
@@ -290,6 +296,14 @@ int main(int argc, char **argv)
         vs.push_back(v);
     }
 
+    // PROBE_FILTER=substr keeps only matching variants (e.g. for rocprofv3 --pmc)
+    if (const char *flt = std::getenv("PROBE_FILTER")) {
+        std::vector<Variant> keep;
+        for (auto &v : vs)
+            if (v.name.find(flt) != std::string::npos) keep.push_back(v);
+        vs.swap(keep);
+        if (vs.empty()) return 0;
+    }
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
