@@ -280,7 +280,7 @@ static int enqueue_fft(demod_t *st, const int16_t *d_pcm, size_t n_windows, uint
     p.sym = d_sym;
     p.mag = d_mag;
     p.spec = d_spec;
-    HIP_TRY(launch_fft(p, s));
+    HIP_TRY(launch_fft_quad(p, s));
     return (int)n_windows;
 }
 

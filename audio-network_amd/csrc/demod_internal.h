@@ -87,6 +87,7 @@ constexpr int kDetFolded = 3;    // fold.hip: Goertzel on the N/8-folded window
 hipError_t launch_detector(int detector, const GoertzelParams &p, hipStream_t s);
 int tile_grid(long long n_windows, int log2g);
 hipError_t launch_synth(const SynthParams &p, hipStream_t s);
-hipError_t launch_fft(const FftParams &p, hipStream_t s);
+hipError_t launch_fft(const FftParams &p, hipStream_t s);       // 64 lanes / window (fft.hip)
+hipError_t launch_fft_quad(const FftParams &p, hipStream_t s);  // 16 lanes / window (fft_quad.hip)
 
 }  // namespace fskd

@@ -12,6 +12,7 @@
 #include "../audio-network_amd/csrc/synth.hip"
 #include "../audio-network_amd/csrc/fold.hip"
 #include "../audio-network_amd/csrc/fft.hip"
+#include "../audio-network_amd/csrc/fft_quad.hip"
 
 #include <algorithm>
 #include <cmath>
@@ -252,11 +253,12 @@ int main(int argc, char **argv)
                 CK(hipMalloc(&fp.mag, fp.n_windows * 8));
                 Variant v;
                 v.name = "fft1024 K=2 hop=" + std::to_string(hop) + " swz=" + std::to_string(swz & 1) +
-                         (swz & 2 ? " TWLDS" : "") +
+                         (swz & 2 ? " QUAD" : "") +
                          " windows=" + std::to_string(fp.n_windows);
                 v.bytes = (double)W * 2048 + fp.n_windows * 9.0;  // stream bytes read once
+                if (hop == 1024) v.sym = fp.sym;  // same windows as the Goertzel K=2 variants
                 if (swz & 2)
-                    v.run = [fp](hipStream_t s) { CK((launch_fft_variant<4, true>(fp, s))); };
+                    v.run = [fp](hipStream_t s) { CK(launch_fft_quad(fp, s)); };
                 else
                     v.run = [fp](hipStream_t s) { CK(launch_fft(fp, s)); };
                 vs.push_back(v);

@@ -330,6 +330,26 @@ def test_fft_detector_noninteger_tones_pick_nearest_bin(A, O, torch):
     assert rel_err(mag, ref_P) <= MAG_TOL
 
 
+@pytest.mark.parametrize("W", [1, 2, 3, 5, 66])
+def test_fft_detector_sixteen_tones_small_batches(A, O, torch, W):
+    """K = 16 (a whole 16-lane row in the quad layout's tone pick) and batches
+    smaller than one 4-window group, with the full spectrum."""
+    f = tuple(1000.0 + 1234.5 * i for i in range(16))
+    pcm, _ = O.synth_fsk(f, 1024, W, 77 + W, 8000, 400)
+    with A.Demodulator(freqs=f, method=FFT) as d:
+        sym, mag = d.batch(pcm, mags=True)
+        d_pcm = torch.from_numpy(pcm.reshape(-1).copy()).cuda()
+        d_sym = torch.empty(W, dtype=torch.uint8, device="cuda")
+        d_spec = torch.empty((W, 513), dtype=torch.float32, device="cuda")
+        d.batch_spectrum_async(d_pcm, W, d_sym, None, d_spec)
+        torch.cuda.synchronize()
+    ref_sym, ref_P = O.fft_demod(pcm, f, 1024)
+    assert (sym == ref_sym).all() and (d_sym.cpu().numpy() == ref_sym).all()
+    assert rel_err(mag, ref_P) <= MAG_TOL
+    full = np.stack([O.fft_power(pcm[i]) for i in range(W)])
+    assert _spec_err(d_spec.cpu().numpy(), full) <= MAG_TOL
+
+
 def test_fft_detector_extremes_and_streaming(A, O, torch):
     n = 1024
     x = np.zeros((5, n), np.int16)
