@@ -221,6 +221,7 @@ __global__ __launch_bounds__(64 * WPB) void fft1024_quad_kernel(FftParams p)
     using namespace quad;
     __shared__ __attribute__((aligned(16))) f2 slab[WPB][kQSlab];
     __shared__ f2 tw1[31 * 16];  // W512^{t k1} / 2 at [k1 - 1][t]
+    __shared__ f2 tw3[16 * 16];  // post-pass W1024^{kP(t, j)} at [j][t]
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int q = lane >> 4;   // window of the wave
@@ -231,10 +232,12 @@ __global__ __launch_bounds__(64 * WPB) void fft1024_quad_kernel(FftParams p)
     // twiddles (and column 0), exact in binary floating point.
     for (int i = threadIdx.x; i < 31 * 16; i += 64 * WPB)
         tw1[i] = 0.5f * t512[((i & 15) * ((i >> 4) + 1)) & 511];
-    // post-pass twiddle bases: W1024^{kP} = base * W32^j (file header)
-    f2 cA = t1024[t];
-    const f2 w16 = t1024[16];
-    f2 cB = t == 0 ? (f2){-w16.y, w16.x} : cA;  // lane 0, j >= 8: i W1024^16
+    // post-pass twiddles W1024^kP for bin kP(t, j) (step 3): t + 32 j, and
+    // for t = 0, j >= 8: 16 + 32 (j - 8)
+    for (int i = threadIdx.x; i < 16 * 16; i += 64 * WPB) {
+        const int tt = i & 15, j = i >> 4;
+        tw3[i] = t1024[(tt == 0 && j >= 8) ? 16 + 32 * (j - 8) : tt + 32 * j];
+    }
     const int k1b = t == 0 ? 16 : 32 - t;
     const int mybin = t < p.k ? p.bins[t] : 0;
     float *pw = reinterpret_cast<float *>(slab[wave]);
@@ -256,8 +259,13 @@ __global__ __launch_bounds__(64 * WPB) void fft1024_quad_kernel(FftParams p)
         const long long w = 4 * g + q;
         f2 a[32];
 #pragma unroll
-        for (int n1 = 0; n1 < 32; ++n1)
+        for (int n1 = 0; n1 < 32; ++n1) {
             a[n1] = (f2){(float)(int)(short)(nx[n1] & 0xFFFFu), (float)((int)nx[n1] >> 16)};
+            // opaque: otherwise the compiler rewrites (float)a + (float)b as
+            // (float)(a + b) and the first butterflies become 2 integer ops +
+            // 2 converts each instead of one packed add
+            asm("" : "+v"(a[n1]));
+        }
 
         // 1. DFT-32 over n1, twiddle W512^{t k1} (and the 1/2 of the real split)
         dft<32>(a);
@@ -300,9 +308,6 @@ __global__ __launch_bounds__(64 * WPB) void fft1024_quad_kernel(FftParams p)
         //    so S + W D is X itself).
         const bool l0 = (t == 0);
         float *pq = pw + q * 513;
-        // the twiddles W32^j cA / cB are loop-invariant: keep them from being
-        // hoisted (16 complex registers) — recomputing costs 2 packed ops per pair
-        asm volatile("" : "+v"(cA), "+v"(cB));
         // bin kP = t + 32 j (lane 0, j >= 8: t + 32 j - 240); mirror 512 - kP
         float *const pA = pq + t, *const pB = pA - (l0 ? 240 : 0);
         float *const mA = pq + 32 - t, *const mB = mA + (l0 ? 240 : 0);
@@ -316,7 +321,7 @@ __global__ __launch_bounds__(64 * WPB) void fft1024_quad_kernel(FftParams p)
             Q = sel_l0((j < 8) ? b[(16 - j) & 15] : b[16 + 23 - j], Q);
             const f2 S = pp_s(P, Q);
             const f2 D = pp_d(P, Q);
-            const f2 T = cmul(D, w32<j>((j < 8) ? cA : cB));
+            const f2 T = cmul(D, tw3[16 * j + t]);
             const f2 re = pp_re(S, T), im = pp_im(S, T);
             const f2 pwr = __builtin_elementwise_fma(re, re, im * im);  // (|X[kP]|^2, |X[512-kP]|^2)
             ((j < 8) ? pA : pB)[32 * j] = pwr.x;

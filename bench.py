@@ -331,7 +331,7 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBPS, 4),
                 "traffic": pmc_traffic(args.config, W),
                 "alg_bytes_per_launch": alg_bytes,
-                "kernel": ("fft1024_kernel<4>" if demod.method == A.METHOD_FFT else
+                "kernel": ("fft1024_quad_kernel<4>" if demod.method == A.METHOD_FFT else
                            ("fold_tile_kernel<%d,4>" if demod.method == A.METHOD_FOLDED
                             else "goertzel_tile_kernel<%d,4>") % K),
             },
