@@ -84,7 +84,7 @@ __global__ __launch_bounds__(64 * WPB) void fft1024_kernel(FftParams p)
     __shared__ cf tws1[TWLDS ? 64 : 1];                            // W_512^{8 a b}, a,b < 8
     __shared__ cf tws3[TWLDS ? 512 : 1];                           // W_1024^k
     const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: tile bases stay in SGPRs (no waterfall loop per buffer load)
     cf *z = zbuf[wave];
     const cf *t512 = reinterpret_cast<const cf *>(p.tw512);
     const cf *t1024 = reinterpret_cast<const cf *>(p.tw1024);

@@ -47,7 +47,7 @@ template <int K, int LOG2G, bool NT = true, int WPB = 4, bool ROTLDS = false, bo
 __global__ __launch_bounds__(64 * WPB) void fold_tile_kernel(GoertzelParams p)
 {
     const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: tile bases stay in SGPRs (no waterfall loop per buffer load)
     const int log2g = LOG2G >= 0 ? LOG2G : p.log2g;
     const int g = 1 << log2g;
     const int n = 64 << log2g;

@@ -68,7 +68,7 @@ __global__ __launch_bounds__(64 * WPB) void goertzel_tile_kernel(GoertzelParams 
     static_assert(PF == 1 || PF == 2, "prefetch depth");
     __shared__ __attribute__((aligned(16))) unsigned char lds[DIRECT ? 16 : WPB * kLdsWaveBytes];
     const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: tile bases stay in SGPRs (no waterfall loop per buffer load)
     unsigned char *wl = lds + wave * kLdsWaveBytes;
     const int log2g = LOG2G >= 0 ? LOG2G : p.log2g;
     const int g = 1 << log2g;

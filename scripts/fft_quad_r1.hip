@@ -23,9 +23,9 @@
 #include <algorithm>
 #include <type_traits>
 
-#include "demod_internal.h"
+#include "../audio-network_amd/csrc/demod_internal.h"
 
-namespace fskd {
+namespace fskd { namespace r1 {
 namespace quad {
 
 // A complex number as a packed fp32 pair: complex add/sub is one v_pk_add_f32,
@@ -49,43 +49,6 @@ __device__ __forceinline__ f2 cmulk(f2 a, f2 w)
     asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,1] op_sel_hi:[1,0]" : "=v"(t) : "v"(a), "s"(w));
     asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1] neg_lo:[0,0,1]" : "=v"(r) : "v"(a), "s"(w), "v"(t));
     return r;
-}
-// Two independent complex products in one block, ordered mul0 mul1 fma0 fma1.
-// gfx950 needs a wait state between a packed-fp32 VGPR write and an
-// immediately dependent packed read: the compiler pads every single cmul
-// (mul -> dependent fma) with an s_nop, which this ordering avoids.
-__device__ __forceinline__ void cmul2(f2 &r0, f2 a0, f2 w0, f2 &r1, f2 a1, f2 w1)
-{
-    f2 t0, t1;
-    asm("v_pk_mul_f32 %2, %4, %5 op_sel:[1,1] op_sel_hi:[1,0]\n\t"
-        "v_pk_mul_f32 %3, %6, %7 op_sel:[1,1] op_sel_hi:[1,0]\n\t"
-        "v_pk_fma_f32 %0, %4, %5, %2 op_sel_hi:[0,1,1] neg_lo:[0,0,1]\n\t"
-        "v_pk_fma_f32 %1, %6, %7, %3 op_sel_hi:[0,1,1] neg_lo:[0,0,1]"
-        : "=&v"(r0), "=&v"(r1), "=&v"(t0), "=&v"(t1)
-        : "v"(a0), "v"(w0), "v"(a1), "v"(w1));
-}
-// the same with both twiddles compile-time constants (SGPR pairs)
-__device__ __forceinline__ void cmulk2(f2 &r0, f2 a0, f2 w0, f2 &r1, f2 a1, f2 w1)
-{
-    f2 t0, t1;
-    asm("v_pk_mul_f32 %2, %4, %5 op_sel:[1,1] op_sel_hi:[1,0]\n\t"
-        "v_pk_mul_f32 %3, %6, %7 op_sel:[1,1] op_sel_hi:[1,0]\n\t"
-        "v_pk_fma_f32 %0, %4, %5, %2 op_sel_hi:[0,1,1] neg_lo:[0,0,1]\n\t"
-        "v_pk_fma_f32 %1, %6, %7, %3 op_sel_hi:[0,1,1] neg_lo:[0,0,1]"
-        : "=&v"(r0), "=&v"(r1), "=&v"(t0), "=&v"(t1)
-        : "v"(a0), "s"(w0), "v"(a1), "s"(w1));
-}
-// (|u|^2 of two pairs): p = (re.x^2 + im.x^2, re.y^2 + im.y^2) for two
-// independent (re, im), interleaved like cmul2
-__device__ __forceinline__ void pwr2(f2 &p0, f2 re0, f2 im0, f2 &p1, f2 re1, f2 im1)
-{
-    f2 t0, t1;
-    asm("v_pk_mul_f32 %2, %5, %5\n\t"
-        "v_pk_mul_f32 %3, %7, %7\n\t"
-        "v_pk_fma_f32 %0, %4, %4, %2\n\t"
-        "v_pk_fma_f32 %1, %6, %6, %3"
-        : "=&v"(p0), "=&v"(p1), "=&v"(t0), "=&v"(t1)
-        : "v"(re0), "v"(im0), "v"(re1), "v"(im1));
 }
 // x + (-i) y = (x.x + y.y, x.y - y.x)
 __device__ __forceinline__ f2 add_mj(f2 x, f2 y)
@@ -191,28 +154,6 @@ __device__ __forceinline__ void static_for(F &&f)
     }
 }
 
-// The non-trivial twiddles W_N^{i2 k1} (not a multiple of a quarter turn) of
-// one dft<N> level: slot i2 + N2 k1 and the W32 exponent.
-template <int N>
-struct TwList {
-    static constexpr int N1 = (N == 32) ? 8 : 4, N2 = N / N1;
-    int slot[N];
-    int j[N];
-    int n;
-    constexpr TwList() : slot(), j(), n(0)
-    {
-        for (int i2 = 0; i2 < N2; ++i2)
-            for (int k1 = 1; k1 < N1; ++k1) {
-                const int jj = ((i2 * k1) * (32 / N)) % 32;
-                if (jj % 8) {
-                    slot[n] = i2 + N2 * k1;
-                    j[n] = jj;
-                    ++n;
-                }
-            }
-    }
-};
-
 // In-register DFT of x[0], x[S], ..., x[(N-1) S] (N = 2, 4, 8, 16, 32), result
 // in natural order in the same slots. Mixed radix N = N1 x N2 (N1 = 4 or 8):
 //   X[k1 + N1 k2] = sum_i2 W_N^{i2 k1} W_N2^{i2 k2} sum_i1 x[N2 i1 + i2] W_N1^{i1 k1}
@@ -233,28 +174,14 @@ __device__ __forceinline__ void dft(f2 *x)
     } else {
         constexpr int N1 = (N == 32) ? 8 : 4;
         constexpr int N2 = N / N1;
-        // DFT-N1 over i1 for every i2 (stride N2 S), then twiddle W_N^{i2 k1}:
-        // the quarter turns in place, the rest two at a time (cmulk2)
+        // DFT-N1 over i1 for every i2 (stride N2 S), then twiddle W_N^{i2 k1}
         static_for<0, N2>([&](auto c) {
             constexpr int i2 = decltype(c)::value;
             dft<N1, N2 * S>(x + i2 * S);
             static_for<1, N1>([&](auto d) {
                 constexpr int k1 = decltype(d)::value;
-                if constexpr (((i2 * k1) * (32 / N)) % 8 == 0)
-                    x[(i2 + N2 * k1) * S] = w32<(i2 * k1) * (32 / N)>(x[(i2 + N2 * k1) * S]);
+                x[(i2 + N2 * k1) * S] = w32<(i2 * k1) * (32 / N)>(x[(i2 + N2 * k1) * S]);
             });
-        });
-        constexpr TwList<N> L{};
-        static_for<0, (L.n + 1) / 2>([&](auto pc) {
-            constexpr int i0 = 2 * decltype(pc)::value, i1 = i0 + 1;
-            constexpr int s0 = L.slot[i0] * S, j0 = L.j[i0];
-            if constexpr (i1 < L.n) {
-                constexpr int s1 = L.slot[i1] * S, j1 = L.j[i1];
-                cmulk2(x[s0], x[s0], (f2){kW32r[j0], kW32i[j0]},
-                       x[s1], x[s1], (f2){kW32r[j1], kW32i[j1]});
-            } else {
-                x[s0] = cmulk(x[s0], (f2){kW32r[j0], kW32i[j0]});
-            }
         });
         // DFT-N2 over i2 for every k1 (contiguous run of N2 at N2 k1)
         static_for<0, N1>([&](auto d) {
@@ -288,17 +215,15 @@ constexpr int kQWin = 16 * kQRow;    // complex per window
 constexpr int kQSlab = 4 * kQWin;    // complex per wave
 static_assert(4 * 513 <= 2 * kQSlab, "bin powers of 4 windows must fit the slab");
 
-// MINW > 0 asks the compiler for MINW waves per SIMD (VGPR budget 512 / MINW).
-template <int WPB = 4, int MINW = 0>
-__global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MINW > 0 ? MINW : 1)))
-void fft1024_quad_kernel(FftParams p)
+template <int WPB = 4>
+__global__ __launch_bounds__(64 * WPB) void fft1024_quad_kernel(FftParams p)
 {
     using namespace quad;
     __shared__ __attribute__((aligned(16))) f2 slab[WPB][kQSlab];
     __shared__ f2 tw1[31 * 16];  // W512^{t k1} / 2 at [k1 - 1][t]
     __shared__ f2 tw3[16 * 16];  // post-pass W1024^{kP(t, j)} at [j][t]
     const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: tile bases stay in SGPRs (no waterfall loop per buffer load)
+    const int wave = threadIdx.x >> 6;
     const int q = lane >> 4;   // window of the wave
     const int t = lane & 15;   // row / column-pair index
     const f2 *t512 = reinterpret_cast<const f2 *>(p.tw512);
@@ -322,22 +247,12 @@ void fft1024_quad_kernel(FftParams p)
     const long long stride = (long long)gridDim.x * WPB;
     long long g = tile_block(p.xcd_swizzle) * WPB + wave;
     uint32_t nx[32];
-    // One buffer descriptor per group (wave-uniform base = its first window);
-    // the lane offset is the window's start + 4 t bytes, and z[t + 16 n1] is
-    // the immediate offset 64 n1 (< 4 KiB), so the 32 loads need no address
-    // arithmetic. Windows past the end are clamped to the last (never stored).
     auto load_group = [&](long long gg) {
-        const long long w0 = 4 * gg;
-        const long long left = p.n_windows - w0;  // >= 1
-        const int wq = q < left ? q : (int)left - 1;
-        long long bytes = ((left - 1) * p.hop + 1024) * 2;
-        if (bytes > 0x7FFFFFF0LL) bytes = 0x7FFFFFF0LL;
-        __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            (void *)(p.pcm + w0 * p.hop), (short)0, (int)bytes, 0x00020000);
-        const int voff = (int)(wq * p.hop * 2) + 4 * t;
+        long long w = 4 * gg + q;
+        if (w >= p.n_windows) w = p.n_windows - 1;  // clamped, never stored
+        const uint32_t *xw = reinterpret_cast<const uint32_t *>(p.pcm + w * p.hop) + t;
 #pragma unroll
-        for (int n1 = 0; n1 < 32; ++n1)
-            nx[n1] = __builtin_amdgcn_raw_buffer_load_b32(rs, voff + 64 * n1, 0, 2);
+        for (int n1 = 0; n1 < 32; ++n1) nx[n1] = __builtin_nontemporal_load(xw + 16 * n1);
     };
     if (g < n_groups) load_group(g);
     for (; g < n_groups; g += stride) {
@@ -356,9 +271,7 @@ void fft1024_quad_kernel(FftParams p)
         dft<32>(a);
         a[0] *= 0.5f;
 #pragma unroll
-        for (int k1 = 1; k1 < 31; k1 += 2)
-            cmul2(a[k1], a[k1], tw1[16 * (k1 - 1) + t], a[k1 + 1], a[k1 + 1], tw1[16 * k1 + t]);
-        a[31] = cmul(a[31], tw1[16 * 30 + t]);
+        for (int k1 = 1; k1 < 32; ++k1) a[k1] = cmul(a[k1], tw1[16 * (k1 - 1) + t]);
 
         // 2. transpose in two column rounds; lane (q, t') gets columns
         //    k1 = t' (round 0) and k1b (round 1) of its window
@@ -398,33 +311,21 @@ void fft1024_quad_kernel(FftParams p)
         // bin kP = t + 32 j (lane 0, j >= 8: t + 32 j - 240); mirror 512 - kP
         float *const pA = pq + t, *const pB = pA - (l0 ? 240 : 0);
         float *const mA = pq + 32 - t, *const mB = mA + (l0 ? 240 : 0);
-        // two pairs at a time (j, j + 1), so no packed result feeds the very
-        // next instruction (cmul2 / pwr2)
-        static_for<0, 8>([&](auto jc) {
-            constexpr int j0 = 2 * decltype(jc)::value, j1 = j0 + 1;
+        static_for<0, 16>([&](auto jc) {
+            constexpr int j = decltype(jc)::value;
             // lane 0's pairing, selected per lane with v_cndmask on a constant
             // lane mask (a C++ select of two b[] elements becomes a runtime
             // index into b, which sends b to scratch)
-            f2 P0 = b[j0], Q0 = b[16 + 15 - j0];
-            f2 P1 = b[j1], Q1 = b[16 + 15 - j1];
-            if constexpr (j0 >= 8) {
-                P0 = sel_l0(b[16 + j0 - 8], P0);
-                P1 = sel_l0(b[16 + j1 - 8], P1);
-            }
-            Q0 = sel_l0((j0 < 8) ? b[(16 - j0) & 15] : b[16 + 23 - j0], Q0);
-            Q1 = sel_l0((j1 < 8) ? b[(16 - j1) & 15] : b[16 + 23 - j1], Q1);
-            const f2 S0 = pp_s(P0, Q0), S1 = pp_s(P1, Q1);
-            const f2 D0 = pp_d(P0, Q0), D1 = pp_d(P1, Q1);
-            f2 T0, T1;
-            cmul2(T0, D0, tw3[16 * j0 + t], T1, D1, tw3[16 * j1 + t]);
-            const f2 re0 = pp_re(S0, T0), re1 = pp_re(S1, T1);
-            const f2 im0 = pp_im(S0, T0), im1 = pp_im(S1, T1);
-            f2 pw0, pw1;  // (|X[kP]|^2, |X[512-kP]|^2)
-            pwr2(pw0, re0, im0, pw1, re1, im1);
-            ((j0 < 8) ? pA : pB)[32 * j0] = pw0.x;
-            ((j0 < 8) ? mA : mB)[32 * (15 - j0)] = pw0.y;
-            ((j1 < 8) ? pA : pB)[32 * j1] = pw1.x;
-            ((j1 < 8) ? mA : mB)[32 * (15 - j1)] = pw1.y;
+            f2 P = b[j], Q = b[16 + 15 - j];
+            if constexpr (j >= 8) P = sel_l0(b[16 + j - 8], P);
+            Q = sel_l0((j < 8) ? b[(16 - j) & 15] : b[16 + 23 - j], Q);
+            const f2 S = pp_s(P, Q);
+            const f2 D = pp_d(P, Q);
+            const f2 T = cmul(D, tw3[16 * j + t]);
+            const f2 re = pp_re(S, T), im = pp_im(S, T);
+            const f2 pwr = __builtin_elementwise_fma(re, re, im * im);  // (|X[kP]|^2, |X[512-kP]|^2)
+            ((j < 8) ? pA : pB)[32 * j] = pwr.x;
+            ((j < 8) ? mA : mB)[32 * (15 - j)] = pwr.y;
         });
         // Z[256] is its own mirror: |X[256]|^2 = |Z[256]|^2 = 4 |b[8]|^2
         if (l0) pq[256] = 4.f * fmaf(b[8].x, b[8].x, b[8].y * b[8].y);
@@ -457,30 +358,21 @@ void fft1024_quad_kernel(FftParams p)
     }
 }
 
-// Persistent grid: as many blocks as fit the chip, each wave strides over
-// groups of 4 windows (the LDS twiddle tables are built once per block).
-template <int WPB, int MINW>
-hipError_t launch_fft_quad_t(const FftParams &p, hipStream_t s)
+hipError_t launch_fft_quad(const FftParams &p, hipStream_t s)
 {
+    constexpr int WPB = 4;
     int dev = 0, cus = 256, per_cu = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fft1024_quad_kernel<WPB, MINW>,
-                                                     64 * WPB, 0) != hipSuccess ||
-        per_cu < 1)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fft1024_quad_kernel<WPB>, 64 * WPB, 0) !=
+            hipSuccess || per_cu < 1)
         per_cu = 1;
     const long long groups = (p.n_windows + 3) / 4;
     long long blocks = (groups + WPB - 1) / WPB;
     blocks = std::min<long long>(blocks, (long long)cus * per_cu);
     if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL((fft1024_quad_kernel<WPB, MINW>), dim3((unsigned)blocks), dim3(64 * WPB), 0,
-                       s, p);
+    hipLaunchKernelGGL((fft1024_quad_kernel<WPB>), dim3((unsigned)blocks), dim3(64 * WPB), 0, s, p);
     return hipGetLastError();
 }
 
-hipError_t launch_fft_quad(const FftParams &p, hipStream_t s)
-{
-    return launch_fft_quad_t<4, 0>(p, s);
-}
-
-}  // namespace fskd
+}  } // namespace fskd::r1

@@ -13,6 +13,7 @@
 #include "../audio-network_amd/csrc/fold.hip"
 #include "../audio-network_amd/csrc/fft.hip"
 #include "../audio-network_amd/csrc/fft_quad.hip"
+#include "fft_quad_r1.hip"
 
 #include <algorithm>
 #include <cmath>
@@ -56,19 +57,21 @@ __global__ __launch_bounds__(256) void read_kernel(const u32x4 *__restrict__ p, 
 
 // The same one-shot access pattern as the tile kernels (each wave reads one
 // contiguous 8 KiB tile with 8 coalesced 16 B/lane nt buffer loads) and no
-// compute: the practical HBM read ceiling for this shape.
-__global__ __launch_bounds__(256) void read_tile_kernel(const int16_t *p, long long n_tiles,
-                                                        unsigned *out)
+// compute: the practical HBM read ceiling for this shape. L = loads per wave
+// (8 KiB at L = 8), WPB = waves per block, AUX = buffer cache-policy bits.
+template <int L, int WPB, int AUX>
+__global__ __launch_bounds__(64 * WPB) void read_tile_kernel(const int16_t *p, long long n_tiles,
+                                                             unsigned *out)
 {
     const int lane = threadIdx.x & 63;
-    const long long t = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const long long t = (long long)blockIdx.x * WPB + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (t >= n_tiles) return;
     __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        (void *)(p + t * 4096), (short)0, 8192, 0x00020000);
+        (void *)(p + t * 512 * L), (short)0, 1024 * L, 0x00020000);
     unsigned acc = 0;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (64 * i + lane) * 16, 0, 2);
+    for (int i = 0; i < L; ++i) {
+        u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (64 * i + lane) * 16, 0, AUX);
         acc ^= v.x ^ v.y ^ v.z ^ v.w;
     }
     if (acc == 0x9E3779B9u) out[0] = acc;
@@ -116,6 +119,7 @@ static void add_variant(std::vector<Variant> &vs, const void *f, int wpb, const 
 #define GZS(K) reinterpret_cast<const void *>(&goertzel_tile_kernel<K, 4, 1, true, 4, false, true>)
 #define GZP(K) reinterpret_cast<const void *>(&goertzel_tile_kernel<K, 4, 1, true, 4, false, false, true>)
 #define GZPB(K) reinterpret_cast<const void *>(&goertzel_tile_kernel<K, 4, 1, true, 4, false, false, true, true>)
+#define GZP2(K) reinterpret_cast<const void *>(&goertzel_tile_kernel<K, 4, 2, true, 4, false, false, true>)
 #define GZB(K) reinterpret_cast<const void *>(&goertzel_tile_kernel<K, 4, 1, true, 4, false, false, false, true>)
 
 int main(int argc, char **argv)
@@ -212,13 +216,14 @@ int main(int argc, char **argv)
     p2s.xcd_swizzle = f2s.xcd_swizzle = f8s.xcd_swizzle = 1;
     p2n.mag = f8n.mag = nullptr;
     add_variant(vs, GZ(2, 1, true, 4, false), 4, "goertzel [default]", p2, 2, cus, 1);
-    add_variant(vs, GZB(2), 4, "goertzel SB", p2, 2, cus, 1);
     add_variant(vs, GZP(4), 4, "goertzel PK [default]", p8, 4, cus, 1);
-    add_variant(vs, GZPB(4), 4, "goertzel PK SB", p8, 4, cus, 1);
-    add_variant(vs, GZB(4), 4, "goertzel SB", p8, 4, cus, 1);
     add_variant(vs, GZP(8), 4, "goertzel PK [default]", p8, 8, cus, 1);
-    add_variant(vs, GZPB(8), 4, "goertzel PK SB", p8, 8, cus, 1);
-    add_variant(vs, GZB(8), 4, "goertzel SB", p8, 8, cus, 1);
+    add_variant(vs, GZP(8), 4, "goertzel PK", p8, 8, cus, 2);
+    add_variant(vs, GZP(8), 4, "goertzel PK", p8, 8, cus, 4);
+    add_variant(vs, GZP(8), 4, "goertzel PK", p8, 8, cus, 0);
+    add_variant(vs, GZP2(8), 4, "goertzel PK PF2", p8, 8, cus, 0);
+    add_variant(vs, GZP2(8), 4, "goertzel PK PF2", p8, 8, cus, 4);
+    add_variant(vs, FD(2, 4), 4, "fold", f2, 2, cus, 1);
     add_variant(vs, FD(8, 4), 4, "fold", f8, 8, cus, 1);
     {
         // FFT detector tables (2-FSK bins 32, 64)
@@ -239,7 +244,7 @@ int main(int argc, char **argv)
         CK(hipMemcpy(d2, t2.data(), 4096, hipMemcpyHostToDevice));
         CK(hipMemcpy(db, hb, 8, hipMemcpyHostToDevice));
         for (int hop : {1024, 256}) {
-            for (int swz : {0, 1, 2, 3}) {
+            for (int swz : {2, 4, 5}) {
                 FftParams fp{};
                 fp.pcm = pcm;
                 fp.hop = hop;
@@ -253,29 +258,47 @@ int main(int argc, char **argv)
                 CK(hipMalloc(&fp.mag, fp.n_windows * 8));
                 Variant v;
                 v.name = "fft1024 K=2 hop=" + std::to_string(hop) + " swz=" + std::to_string(swz & 1) +
-                         (swz & 2 ? " QUAD" : "") +
+                         (swz == 2 || swz == 3 ? " QUAD-r1" : swz == 6 ? " QUAD-new-4w" : " QUAD-new") +
                          " windows=" + std::to_string(fp.n_windows);
                 v.bytes = (double)W * 2048 + fp.n_windows * 9.0;  // stream bytes read once
                 if (hop == 1024) v.sym = fp.sym;  // same windows as the Goertzel K=2 variants
-                if (swz & 2)
-                    v.run = [fp](hipStream_t s) { CK(launch_fft_quad(fp, s)); };
+                if (swz == 2 || swz == 3)
+                    v.run = [fp](hipStream_t s) { CK(r1::launch_fft_quad(fp, s)); };
+                else if (swz == 6)
+                    v.run = [fp](hipStream_t s) { CK((launch_fft_quad_t<4, 4>(fp, s))); };
                 else
-                    v.run = [fp](hipStream_t s) { CK(launch_fft(fp, s)); };
+                    v.run = [fp](hipStream_t s) { CK(launch_fft_quad(fp, s)); };
                 vs.push_back(v);
             }
         }
     }
-    {
+    auto add_read = [&](const char *label, const void *f, int L, int wpb) {
         Variant v;
-        v.name = "read-only one-shot tile (8 KiB/wave, nt)";
+        v.name = label;
         v.bytes = (double)W * 2048;
-        const long long nt = W / 4;
+        const long long nt = W * 2048 / (1024LL * L);
+        const unsigned blocks = (unsigned)((nt + wpb - 1) / wpb);
         v.run = [=](hipStream_t s) {
-            hipLaunchKernelGGL(read_tile_kernel, dim3((unsigned)((nt + 3) / 4)), dim3(256), 0, s,
-                               (const int16_t *)pcm, nt, sink);
+            const int16_t *pp = pcm;
+            long long ntt = nt;
+            unsigned *sk = sink;
+            void *args[] = {&pp, &ntt, &sk};
+            CK(hipLaunchKernel(f, dim3(blocks), dim3(64 * wpb), args, 0, s));
         };
         vs.push_back(v);
-    }
+    };
+#define RT(L, WPB, AUX) reinterpret_cast<const void *>(&read_tile_kernel<L, WPB, AUX>), L, WPB
+    add_read("read-only one-shot tile (8 KiB/wave, nt, 4 waves/WG)", RT(8, 4, 2));
+    add_read("read-only one-shot tile (8 KiB/wave, plain, 4 waves/WG)", RT(8, 4, 0));
+    add_read("read-only one-shot tile (8 KiB/wave, nt, 8 waves/WG)", RT(8, 8, 2));
+    add_read("read-only one-shot tile (8 KiB/wave, nt, 16 waves/WG)", RT(8, 16, 2));
+    add_read("read-only one-shot tile (4 KiB/wave, nt, 4 waves/WG)", RT(4, 4, 2));
+    add_read("read-only one-shot tile (16 KiB/wave, nt, 4 waves/WG)", RT(16, 4, 2));
+    add_read("read-only one-shot tile (16 KiB/wave, nt, 8 waves/WG)", RT(16, 8, 2));
+    add_read("read-only one-shot tile (32 KiB/wave, nt, 4 waves/WG)", RT(32, 4, 2));
+    add_read("read-only one-shot tile (8 KiB/wave, sc0|nt, 4 waves/WG)", RT(8, 4, 3));
+    add_read("read-only one-shot tile (8 KiB/wave, sc1|nt, 4 waves/WG)", RT(8, 4, 18));
+#undef RT
     {
         const long long n16 = W * 2048 / 16;
         for (int g : {2048, 4096, 8192}) {
