@@ -376,3 +376,40 @@ def test_fft_detector_extremes_and_streaming(A, O, torch):
                               for i in range(0, L.size, 2880)])
     ref, _ = O.fft_demod(L.reshape(-1), A.FSK8_FREQS, n)
     assert (got == ref).all()
+
+
+@pytest.mark.parametrize("method,hop", [(GOERTZEL, 1024), (GOERTZEL, 256), (FOLDED, 512),
+                                        (2, 256)])
+def test_host_batch_multi_chunk(A, O, torch, method, hop):
+    """Host-pointer demod_batch streams its input in 65536-window chunks over
+    two device slots (demod_api.cpp run_host). Across chunk boundaries (and
+    the n - hop overlap of sliding windows) its output must equal the
+    device-pointer path on the same samples bit-for-bit, and a sample of
+    windows must match the oracle."""
+    n = 1024
+    f = A.FSK8_FREQS if method == FOLDED else A.FSK2_FREQS
+    Wsrc = 3 * 65536 // (n // hop) + 37           # source windows of n samples
+    cfg = A.make_cfg(n=n, freqs=f)
+    d_src = torch.empty((Wsrc, n), dtype=torch.int16, device="cuda")
+    d_true = torch.empty(Wsrc, dtype=torch.uint8, device="cuda")
+    A.synth_fsk(cfg, A.BENCH_SEED + hop, Wsrc, 8000, 400, d_src, d_true)
+    torch.cuda.synchronize()
+    W = (Wsrc * n - n) // hop + 1
+    assert W > 3 * 65536
+    d_sym = torch.empty(W, dtype=torch.uint8, device="cuda")
+    d_mag = torch.empty((W, len(f)), dtype=torch.float32, device="cuda")
+    flat = d_src.cpu().numpy().reshape(-1)
+    with A.Demodulator(n=n, hop=hop, freqs=f, method=method) as d:
+        assert d.method == method
+        d.batch_device(d_src, W, d_sym, d_mag)
+        sym, mag = d.batch(flat, n_windows=W, mags=True)
+        sym2 = d.batch(flat, n_windows=W)   # second call reuses the slots
+    assert np.array_equal(sym, d_sym.cpu().numpy())
+    assert np.array_equal(sym2, sym)
+    assert np.array_equal(mag, d_mag.cpu().numpy())
+    idx = np.array([0, 1, 65535, 65536, 65537, 131071, 131072, W - 2, W - 1])
+    win = np.stack([flat[i * hop:i * hop + n] for i in idx])
+    oracle = O.fft_demod if method == 2 else O.goertzel
+    ref_sym, ref_P = oracle(win.reshape(-1), f, n, n)
+    assert (sym[idx] == ref_sym).all()
+    assert rel_err(mag[idx], ref_P) <= MAG_TOL
