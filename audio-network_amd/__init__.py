@@ -116,6 +116,9 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "demod_pack_symbols": (ctypes.c_int, [_P, _SZ, ctypes.c_int, _P, _SZ]),
         "demod_unpack_symbols": (ctypes.c_int, [_P, _SZ, ctypes.c_int, _P, _SZ]),
         "demod_frame_symbols": (ctypes.c_longlong, [_P, _SZ, ctypes.c_int, _SZ, _P, _SZ]),
+        "demod_frame_symbols_size": (ctypes.c_longlong, [_SZ, ctypes.c_int, _SZ]),
+        "demod_frame_streams_async": (ctypes.c_longlong, [_P, _SZ, _SZ, ctypes.c_int, _SZ, _P,
+                                                          _P]),
         "demod_synth_fsk": (ctypes.c_int, [ctypes.POINTER(DemodCfg), ctypes.c_uint64,
                                            ctypes.c_uint64, _SZ, ctypes.c_int, ctypes.c_int,
                                            _P, _P, _P]),
@@ -384,6 +387,25 @@ def frame_symbols(symbols: np.ndarray, bits: int,
     if rc < 0:
         raise DemodError(int(rc), "demod_frame_symbols")
     return out[:rc].tobytes()
+
+
+def frame_symbols_size(n: int, bits: int, max_payload: int = DEMOD_MAX_FRAME_PAYLOAD) -> int:
+    """Bytes frame_symbols produces for n symbols."""
+    rc = int(load_library().demod_frame_symbols_size(n, bits, max_payload))
+    if rc < 0:
+        raise DemodError(rc, "demod_frame_symbols_size")
+    return rc
+
+
+def frame_streams_async(d_symbols, n_streams: int, n: int, bits: int, d_out,
+                        max_payload: int = DEMOD_MAX_FRAME_PAYLOAD, stream: int = 0) -> int:
+    """Device framing of [n_streams][n] symbols: stream s's frames (as
+    frame_symbols would make them) at d_out[s * stride]; returns stride."""
+    rc = int(load_library().demod_frame_streams_async(_ptr(d_symbols), n_streams, n, bits,
+                                                      max_payload, _ptr(d_out), stream or None))
+    if rc < 0:
+        raise DemodError(rc, "demod_frame_streams_async")
+    return rc
 
 
 def iter_frames(stream: bytes):

@@ -568,6 +568,27 @@ int demod_synth_fsk(const demod_cfg_t *cfg, uint64_t seed, uint64_t w0, size_t n
     return DEMOD_OK;
 }
 
+long long demod_frame_symbols_size(size_t n, int bits, size_t max_payload)
+{
+    if (bits < 1 || bits > 8) return DEMOD_BAD_ARG;
+    if (max_payload < 1 || max_payload > DEMOD_MAX_FRAME_PAYLOAD) return DEMOD_BAD_ARG;
+    if (n > (size_t)1 << 40) return DEMOD_BAD_ARG;
+    return frame_streams_size((long long)n, bits, (long long)max_payload, nullptr, nullptr, nullptr);
+}
+
+long long demod_frame_streams_async(const uint8_t *d_symbols, size_t n_streams, size_t n,
+                                    int bits, size_t max_payload, uint8_t *d_out, void *stream)
+{
+    const long long stride = demod_frame_symbols_size(n, bits, max_payload);
+    if (stride < 0) return stride;
+    if (n_streams && n && (!d_symbols || !d_out)) return DEMOD_BAD_ARG;
+    if (n_streams > (size_t)1 << 31) return DEMOD_BAD_ARG;
+    if (n_streams == 0 || n == 0) return stride;
+    HIP_TRY(launch_frame_streams(d_symbols, (long long)n_streams, (long long)n, bits,
+                                 (long long)max_payload, d_out, (hipStream_t)stream));
+    return stride;
+}
+
 const char *demod_strerror(int error)
 {
     switch (error) {

@@ -89,5 +89,10 @@ int tile_grid(long long n_windows, int log2g);
 hipError_t launch_synth(const SynthParams &p, hipStream_t s);
 hipError_t launch_fft(const FftParams &p, hipStream_t s);       // 64 lanes / window (fft.hip)
 hipError_t launch_fft_quad(const FftParams &p, hipStream_t s);  // 16 lanes / window (fft_quad.hip)
+// ip.proto framing of [n_streams][n] symbols, one frame run per stream (frame_gpu.hip)
+long long frame_streams_size(long long n, int bits, long long max_payload, unsigned *per,
+                             unsigned *full, int *frames);
+hipError_t launch_frame_streams(const uint8_t *d_sym, long long n_streams, long long n, int bits,
+                                long long max_payload, uint8_t *d_out, hipStream_t s);
 
 }  // namespace fskd

@@ -411,8 +411,13 @@ void fft1024_quad_kernel(FftParams p)
                 P0 = sel_l0(b[16 + j0 - 8], P0);
                 P1 = sel_l0(b[16 + j1 - 8], P1);
             }
-            Q0 = sel_l0((j0 < 8) ? b[(16 - j0) & 15] : b[16 + 23 - j0], Q0);
-            Q1 = sel_l0((j1 < 8) ? b[(16 - j1) & 15] : b[16 + 23 - j1], Q1);
+            if constexpr (j0 < 8) {
+                Q0 = sel_l0(b[(16 - j0) & 15], Q0);
+                Q1 = sel_l0(b[(16 - j1) & 15], Q1);
+            } else {
+                Q0 = sel_l0(b[16 + 23 - j0], Q0);
+                Q1 = sel_l0(b[16 + 23 - j1], Q1);
+            }
             const f2 S0 = pp_s(P0, Q0), S1 = pp_s(P1, Q1);
             const f2 D0 = pp_d(P0, Q0), D1 = pp_d(P1, Q1);
             f2 T0, T1;

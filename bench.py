@@ -198,13 +198,25 @@ def main():
     # (waiting only for step t-1's kernel) and so overlaps step t's kernel.
     comp = torch.cuda.Stream(device=dev) if world > 1 else main
     slots = [d_sym, torch.empty_like(d_sym)] if world > 1 else [d_sym]
+    # config 5: every rank frames its own streams on the device (one
+    # ToReceiver run per stream, demod_frame_streams_async) and RCCL gathers
+    # the frames; the other configs gather symbols and rank 0 frames them.
+    dev_framing = args.config == "streams"
+    if dev_framing:
+        bits = A.bits_per_symbol(K)
+        fstride = A.frame_symbols_size(wps, bits)
+        fslots = [torch.empty(max(s_count * fstride, 1), dtype=torch.uint8, device=dev)
+                  for _ in slots]
     kdone = [torch.cuda.Event() for _ in slots]   # kernel wrote the slot
     gdone = [torch.cuda.Event() for _ in slots]   # gather finished reading the slot
     st = {"i": 0, "prev": None, "used": [False] * len(slots)}
 
     def gather(slot):
         main.wait_event(kdone[slot])
-        out = D.gather_symbols(slots[slot], gunits, world, unit=gunit)
+        if dev_framing:
+            out = D.gather_symbols(fslots[slot][:s_count * fstride], gunits, world, unit=fstride)
+        else:
+            out = D.gather_symbols(slots[slot], gunits, world, unit=gunit)
         gdone[slot].record(main)
         return out
 
@@ -218,6 +230,9 @@ def main():
         demod.batch_async(d_pcm, n_eval, slots[slot], d_mag, stream=comp.cuda_stream)
         if ev is not None:
             ev[1].record(comp)
+        if dev_framing:
+            A.frame_streams_async(slots[slot], s_count, wps, bits, fslots[slot],
+                                  stream=comp.cuda_stream)
         out = None
         if world > 1:
             kdone[slot].record(comp)
@@ -272,7 +287,20 @@ def main():
         step_w = n // hop
         sym_err = int((d_sym[::step_w][:W] != d_true).sum().item())
     framed = None
-    if world > 1:
+    if dev_framing:
+        # frames of the last step: gathered (N > 1) or this rank's own (N = 1)
+        frames = all_sym if world > 1 else fslots[(st["i"] - 1) % len(slots)][:s_count * fstride]
+        all_true = D.gather_symbols(d_true, gunits, world, unit=gunit) if world > 1 else d_true
+        if rank == 0:
+            fb = frames.cpu().numpy()
+            back = np.concatenate([D.unframe_symbols(A, fb[i * fstride:(i + 1) * fstride].tobytes(),
+                                                     wps, K) for i in range(gunits)])
+            sym_err = int((back != all_true.cpu().numpy()).sum())
+            framed = {"frames_bytes": int(fb.size), "frame_bytes_per_stream": fstride,
+                      "bits_per_symbol": bits, "framing": "device (demod_frame_streams_async)",
+                      "gathered": "frames" if world > 1 else "n/a (1 rank)",
+                      "roundtrip_ok": sym_err == 0}
+    elif world > 1:
         all_true = D.gather_symbols(d_true, gunits, world, unit=gunit)
         sym_err = int((all_sym != all_true).sum().item())
         if rank == 0:
@@ -315,7 +343,9 @@ def main():
                 "hop": hop,
                 "n": n,
                 "outputs": "symbols" + ("" if args.no_mags else " + |X_k|^2"),
-                "parallelism": f"dp{world} (independent window shards, RCCL symbol all-gather)",
+                "parallelism": (f"dp{world} (stream shards; per-rank device framing, RCCL "
+                                "all-gather of ToReceiver frames)" if dev_framing else
+                                f"dp{world} (independent window shards, RCCL symbol all-gather)"),
             },
             "detector": {A.METHOD_GOERTZEL: "goertzel", A.METHOD_FOLDED: "folded",
                          A.METHOD_FFT: "fft1024"}.get(demod.method, str(demod.method)),

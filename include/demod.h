@@ -181,6 +181,22 @@ int demod_unpack_symbols(const uint8_t *in, size_t n, int bits,
 long long demod_frame_symbols(const uint8_t *symbols, size_t n, int bits,
                               size_t max_payload, uint8_t *out, size_t cap);
 
+/* Bytes demod_frame_symbols writes for n symbols (0 for n = 0), or a
+ * negative code for bad arguments. */
+long long demod_frame_symbols_size(size_t n, int bits, size_t max_payload);
+
+/* Device framing for many streams (config 5: each rank frames its own
+ * streams before the RCCL gather). d_symbols holds n_streams x n symbols,
+ * stream-major; stream s is framed exactly as demod_frame_symbols(symbols
+ * of s, n, bits, max_payload, ...) would, into d_out + s * stride with
+ * stride = demod_frame_symbols_size(n, bits, max_payload). Device pointers,
+ * enqueued on `stream` (hipStream_t; NULL = default stream). Returns the
+ * stride or a negative code. Stands in for nanopb pb_encode_delimited of
+ * ToReceiver (network.cpp:389-403), one message per payload. */
+long long demod_frame_streams_async(const uint8_t *d_symbols, size_t n_streams, size_t n,
+                                    int bits, size_t max_payload, uint8_t *d_out,
+                                    void *stream);
+
 /* ---- synthetic PCM (benchmarks / tests) -------------------------------- */
 
 /* Device generator of the seeded FSK test signal (DESIGN.md §Synthetic

@@ -178,3 +178,14 @@ def test_frame_symbols_stream(A):
         got = np.concatenate([A.unpack_symbols(p, min(per, n - i * per), bits)
                               for i, p in enumerate(payloads)]) if payloads else np.zeros(0, np.uint8)
         assert (got == s).all()
+
+
+@pytest.mark.parametrize("n,bits", [(0, 1), (1, 1), (7, 1), (8, 1), (2048, 1), (32768, 1),
+                                    (32769, 1), (100000, 1), (5, 3), (10923, 3), (40000, 3),
+                                    (16384, 2), (8193, 4), (3, 8), (4097, 8)])
+def test_frame_symbols_size_matches_host_framing(A, n, bits):
+    """demod_frame_symbols_size == len(demod_frame_symbols output)."""
+    sym = np.random.default_rng(n + bits).integers(0, 1 << bits, n, dtype=np.uint8)
+    assert A.frame_symbols_size(n, bits) == len(A.frame_symbols(sym, bits))
+    for mp in (1, 17, 256):
+        assert A.frame_symbols_size(n, bits, mp) == len(A.frame_symbols(sym, bits, mp))

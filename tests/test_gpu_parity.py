@@ -413,3 +413,36 @@ def test_host_batch_multi_chunk(A, O, torch, method, hop):
     ref_sym, ref_P = oracle(win.reshape(-1), f, n, n)
     assert (sym[idx] == ref_sym).all()
     assert rel_err(mag[idx], ref_P) <= MAG_TOL
+
+
+@pytest.mark.parametrize("n_streams,n,bits,max_payload", [
+    (1, 1, 1, 4096), (3, 2048, 1, 4096), (128, 2048, 3, 4096), (5, 40000, 1, 4096),
+    (4, 32769, 1, 4096), (7, 10923, 3, 4096), (2, 9000, 4, 4096), (3, 4097, 8, 4096),
+    (6, 1000, 2, 17), (2, 300, 3, 1), (1, 0, 1, 4096), (0, 100, 1, 4096)])
+def test_device_framing_matches_host_codec(A, torch, n_streams, n, bits, max_payload):
+    """demod_frame_streams_async frames every stream byte-for-byte as the host
+    codec demod_frame_symbols (itself pinned to the reference's nanopb in
+    test_frame.py), and the frames decode back to the symbols."""
+    rng = np.random.default_rng(n_streams * 7919 + n + bits)
+    # values above the symbol width are masked, as demod_pack_symbols does
+    sym = rng.integers(0, 256, (n_streams, n), dtype=np.uint8)
+    stride = A.frame_symbols_size(n, bits, max_payload)
+    d_sym = torch.from_numpy(sym.copy()).cuda() if sym.size else torch.zeros(1, dtype=torch.uint8,
+                                                                              device="cuda")
+    d_out = torch.full((max(n_streams * stride, 1),), 0xEE, dtype=torch.uint8, device="cuda")
+    got = A.frame_streams_async(d_sym, n_streams, n, bits, d_out, max_payload)
+    torch.cuda.synchronize()
+    assert got == stride
+    out = d_out.cpu().numpy()
+    mask = (1 << bits) - 1
+    for s in range(n_streams):
+        ref = A.frame_symbols(sym[s], bits, max_payload)
+        assert out[s * stride:(s + 1) * stride].tobytes() == ref
+        if n:
+            per = max_payload * 8 // bits
+            back, got_n = [], 0
+            for payload in A.iter_frames(ref):
+                cnt = min(per, n - got_n)
+                back.append(A.unpack_symbols(payload, cnt, bits))
+                got_n += cnt
+            assert np.array_equal(np.concatenate(back), sym[s] & mask)
