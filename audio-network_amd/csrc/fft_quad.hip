@@ -283,13 +283,31 @@ __device__ __forceinline__ void dft(f2 *x)
 // window stride 544 words = 32 mod 64 puts odd windows on the other 32, so a
 // 32-lane pass of writes or column reads is conflict-free. Reused for the bin
 // powers (4 x 513 floats).
+// Bin powers after step 3, per window (stride kQPow floats): pair j of lane t
+// stores (|X[kP]|^2, |X[512 - kP]|^2) as one f2 at slot 16 j + t; |X[256]|^2
+// sits at float 512. quad_slot(b) is the float index of bin b.
+constexpr int kQPow = 544;  // floats per window: 8-byte aligned, odd windows on the other 32 banks
+__host__ __device__ constexpr int quad_slot(int b)
+{
+    if (b == 256) return 512;
+    const int u = b & 31, v = b >> 5;
+    if (u == 0) return v < 8 ? 2 * (16 * v) : 2 * (16 * (16 - v)) + 1;  // lane 0: kP = 32 j
+    if (u == 16) return v < 8 ? 2 * (16 * (v + 8)) : 2 * (16 * (23 - v)) + 1;  // lane 0, j >= 8
+    if (u < 16) return 2 * (16 * v + u);                 // kP = t + 32 j
+    return 2 * (16 * (15 - v) + (32 - u)) + 1;           // mirror 512 - kP
+}
+
 constexpr int kQRow = 17;            // complex per row (16 + 1 pad)
 constexpr int kQWin = 16 * kQRow;    // complex per window
 constexpr int kQSlab = 4 * kQWin;    // complex per wave
-static_assert(4 * 513 <= 2 * kQSlab, "bin powers of 4 windows must fit the slab");
+static_assert(4 * kQPow <= 2 * kQSlab, "bin powers of 4 windows must fit the slab");
 
 // MINW > 0 asks the compiler for MINW waves per SIMD (VGPR budget 512 / MINW).
-template <int WPB = 4, int MINW = 0>
+// SPLIT: the next group's 32 loads go out in two halves — the 16 dwords the
+// first two DFT-8 columns of stage 1 need (n1 % 4 < 2) during the transpose,
+// the rest after the post-pass — so only 16 prefetch VGPRs are live across
+// the DFT-16 and post-pass.
+template <int WPB = 4, int MINW = 0, bool SPLIT = false>
 __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MINW > 0 ? MINW : 1)))
 void fft1024_quad_kernel(FftParams p)
 {
@@ -314,7 +332,7 @@ void fft1024_quad_kernel(FftParams p)
         tw3[i] = t1024[(tt == 0 && j >= 8) ? 16 + 32 * (j - 8) : tt + 32 * j];
     }
     const int k1b = t == 0 ? 16 : 32 - t;
-    const int mybin = t < p.k ? p.bins[t] : 0;
+    const int myslot = quad_slot(t < p.k ? p.bins[t] : 0);
     float *pw = reinterpret_cast<float *>(slab[wave]);
     __syncthreads();
 
@@ -326,7 +344,7 @@ void fft1024_quad_kernel(FftParams p)
     // the lane offset is the window's start + 4 t bytes, and z[t + 16 n1] is
     // the immediate offset 64 n1 (< 4 KiB), so the 32 loads need no address
     // arithmetic. Windows past the end are clamped to the last (never stored).
-    auto load_group = [&](long long gg) {
+    auto load_group = [&](long long gg, int half) {  // half: 0 / 1 of SPLIT, 2 = all
         const long long w0 = 4 * gg;
         const long long left = p.n_windows - w0;  // >= 1
         const int wq = q < left ? q : (int)left - 1;
@@ -337,9 +355,10 @@ void fft1024_quad_kernel(FftParams p)
         const int voff = (int)(wq * p.hop * 2) + 4 * t;
 #pragma unroll
         for (int n1 = 0; n1 < 32; ++n1)
-            nx[n1] = __builtin_amdgcn_raw_buffer_load_b32(rs, voff + 64 * n1, 0, 2);
+            if (half == 2 || ((n1 & 3) < 2) == (half == 0))
+                nx[n1] = __builtin_amdgcn_raw_buffer_load_b32(rs, voff + 64 * n1, 0, 2);
     };
-    if (g < n_groups) load_group(g);
+    if (g < n_groups) load_group(g, 2);
     for (; g < n_groups; g += stride) {
         const long long w = 4 * g + q;
         f2 a[32];
@@ -374,7 +393,7 @@ void fft1024_quad_kernel(FftParams p)
             if (r == 0) {
                 // prefetch the next group here, where half of the DFT-32 output
                 // is already in LDS (unconditional, clamped: one basic block)
-                load_group(g + stride < n_groups ? g + stride : g);
+                load_group(g + stride < n_groups ? g + stride : g, SPLIT ? 0 : 2);
             }
             const int col = r == 0 ? t : k1b - 16;
 #pragma unroll
@@ -394,10 +413,8 @@ void fft1024_quad_kernel(FftParams p)
         //    S = P + conj Q, D = -i (P - conj Q), W = W1024^kP (b holds Z/2,
         //    so S + W D is X itself).
         const bool l0 = (t == 0);
-        float *pq = pw + q * 513;
-        // bin kP = t + 32 j (lane 0, j >= 8: t + 32 j - 240); mirror 512 - kP
-        float *const pA = pq + t, *const pB = pA - (l0 ? 240 : 0);
-        float *const mA = pq + 32 - t, *const mB = mA + (l0 ? 240 : 0);
+        float *pq = pw + q * kQPow;
+        f2 *const ps = reinterpret_cast<f2 *>(pq) + t;  // slot (j, t) at ps[16 j]
         // two pairs at a time (j, j + 1), so no packed result feeds the very
         // next instruction (cmul2 / pwr2)
         static_for<0, 8>([&](auto jc) {
@@ -426,13 +443,12 @@ void fft1024_quad_kernel(FftParams p)
             const f2 im0 = pp_im(S0, T0), im1 = pp_im(S1, T1);
             f2 pw0, pw1;  // (|X[kP]|^2, |X[512-kP]|^2)
             pwr2(pw0, re0, im0, pw1, re1, im1);
-            ((j0 < 8) ? pA : pB)[32 * j0] = pw0.x;
-            ((j0 < 8) ? mA : mB)[32 * (15 - j0)] = pw0.y;
-            ((j1 < 8) ? pA : pB)[32 * j1] = pw1.x;
-            ((j1 < 8) ? mA : mB)[32 * (15 - j1)] = pw1.y;
+            ps[16 * j0] = pw0;
+            ps[16 * j1] = pw1;
         });
         // Z[256] is its own mirror: |X[256]|^2 = |Z[256]|^2 = 4 |b[8]|^2
-        if (l0) pq[256] = 4.f * fmaf(b[8].x, b[8].x, b[8].y * b[8].y);
+        if (l0) pq[512] = 4.f * fmaf(b[8].x, b[8].x, b[8].y * b[8].y);
+        if (SPLIT) load_group(g + stride < n_groups ? g + stride : g, 1);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -442,7 +458,7 @@ void fft1024_quad_kernel(FftParams p)
         const bool live = w < p.n_windows;
         float pk = -1.f;
         int arg = t;
-        if (t < p.k) pk = pq[mybin];
+        if (t < p.k) pk = pq[myslot];
         if (live && t < p.k && p.mag) p.mag[w * p.k + t] = pk;
         // row_ror:1,2,4,8 within the 16-lane row: every lane sees the whole row
         static_for<0, 4>([&](auto sc) {
@@ -450,12 +466,14 @@ void fft1024_quad_kernel(FftParams p)
             const float po = __int_as_float(
                 __builtin_amdgcn_update_dpp(0, __float_as_int(pk), ctrl, 0xF, 0xF, false));
             const int ao = __builtin_amdgcn_update_dpp(0, arg, ctrl, 0xF, 0xF, false);
-            if (po > pk || (po == pk && ao < arg)) { pk = po; arg = ao; }
+            const bool take = (po > pk) | ((po == pk) & (ao < arg));  // branch-free
+            pk = take ? po : pk;
+            arg = take ? ao : arg;
         });
         if (live && t == 0) p.sym[w] = (uint8_t)arg;
         if (p.spec && live) {
             float *so = p.spec + w * 513;
-            for (int i = t; i < 513; i += 16) so[i] = pq[i];
+            for (int i = t; i < 513; i += 16) so[i] = pq[quad_slot(i)];
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -464,13 +482,13 @@ void fft1024_quad_kernel(FftParams p)
 
 // Persistent grid: as many blocks as fit the chip, each wave strides over
 // groups of 4 windows (the LDS twiddle tables are built once per block).
-template <int WPB, int MINW>
+template <int WPB, int MINW, bool SPLIT = false>
 hipError_t launch_fft_quad_t(const FftParams &p, hipStream_t s)
 {
     int dev = 0, cus = 256, per_cu = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fft1024_quad_kernel<WPB, MINW>,
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fft1024_quad_kernel<WPB, MINW, SPLIT>,
                                                      64 * WPB, 0) != hipSuccess ||
         per_cu < 1)
         per_cu = 1;
@@ -478,7 +496,7 @@ hipError_t launch_fft_quad_t(const FftParams &p, hipStream_t s)
     long long blocks = (groups + WPB - 1) / WPB;
     blocks = std::min<long long>(blocks, (long long)cus * per_cu);
     if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL((fft1024_quad_kernel<WPB, MINW>), dim3((unsigned)blocks), dim3(64 * WPB), 0,
+    hipLaunchKernelGGL((fft1024_quad_kernel<WPB, MINW, SPLIT>), dim3((unsigned)blocks), dim3(64 * WPB), 0,
                        s, p);
     return hipGetLastError();
 }
