@@ -139,6 +139,39 @@ __device__ __forceinline__ f2 pp_im(f2 S, f2 T)
     return r;
 }
 
+// The real post-pass of two mirror pairs in one block (step 3 of the kernel):
+// S = P + conj Q, D = -i (P - conj Q), T = W D, then
+// pw = (|S + T|^2, |S - T|^2 with the imaginary part of S - T conjugated), i.e.
+// (|X[kP]|^2, |X[512 - kP]|^2). Sixteen packed ops, ordered so that no result
+// feeds the next instruction: one asm block, because the compiler pads every
+// asm boundary whose last write is read next with an s_nop (gfx950 packed-fp32
+// write -> dependent read hazard), and a chain of small blocks is all
+// boundaries.
+__device__ __forceinline__ void post_pair2(f2 &pw0, f2 P0, f2 Q0, f2 W0, f2 &pw1, f2 P1, f2 Q1,
+                                           f2 W1)
+{
+    f2 S0, S1, D0, D1, T0, T1, R0, R1, I0, I1;
+    asm("v_pk_add_f32 %2, %12, %13 neg_hi:[0,1]\n\t"                              // S0
+        "v_pk_add_f32 %3, %15, %16 neg_hi:[0,1]\n\t"                              // S1
+        "v_pk_add_f32 %4, %12, %13 op_sel:[1,1] op_sel_hi:[0,0] neg_hi:[1,0]\n\t" // D0
+        "v_pk_add_f32 %5, %15, %16 op_sel:[1,1] op_sel_hi:[0,0] neg_hi:[1,0]\n\t" // D1
+        "v_pk_mul_f32 %6, %4, %14 op_sel:[1,1] op_sel_hi:[1,0]\n\t"               // t0
+        "v_pk_mul_f32 %7, %5, %17 op_sel:[1,1] op_sel_hi:[1,0]\n\t"               // t1
+        "v_pk_fma_f32 %6, %4, %14, %6 op_sel_hi:[0,1,1] neg_lo:[0,0,1]\n\t"       // T0 = W0 D0
+        "v_pk_fma_f32 %7, %5, %17, %7 op_sel_hi:[0,1,1] neg_lo:[0,0,1]\n\t"       // T1
+        "v_pk_add_f32 %8, %2, %6 op_sel_hi:[0,0] neg_hi:[0,1]\n\t"                // re pair 0
+        "v_pk_add_f32 %9, %3, %7 op_sel_hi:[0,0] neg_hi:[0,1]\n\t"                // re pair 1
+        "v_pk_add_f32 %10, %2, %6 op_sel:[1,1] neg_hi:[0,1]\n\t"                  // im pair 0
+        "v_pk_add_f32 %11, %3, %7 op_sel:[1,1] neg_hi:[0,1]\n\t"                  // im pair 1
+        "v_pk_mul_f32 %4, %10, %10\n\t"                                            // im0^2
+        "v_pk_mul_f32 %5, %11, %11\n\t"                                            // im1^2
+        "v_pk_fma_f32 %0, %8, %8, %4\n\t"                                          // pw0
+        "v_pk_fma_f32 %1, %9, %9, %5"                                                // pw1
+        : "=&v"(pw0), "=&v"(pw1), "=&v"(S0), "=&v"(S1), "=&v"(D0), "=&v"(D1), "=&v"(T0),
+          "=&v"(T1), "=&v"(R0), "=&v"(R1), "=&v"(I0), "=&v"(I1)
+        : "v"(P0), "v"(Q0), "v"(W0), "v"(P1), "v"(Q1), "v"(W1));
+}
+
 // lane % 16 == 0 ? a : b (lanes 0, 16, 32, 48 of the wave)
 __device__ __forceinline__ f2 sel_l0(f2 a, f2 b)
 {
@@ -307,7 +340,10 @@ static_assert(4 * kQPow <= 2 * kQSlab, "bin powers of 4 windows must fit the sla
 // first two DFT-8 columns of stage 1 need (n1 % 4 < 2) during the transpose,
 // the rest after the post-pass — so only 16 prefetch VGPRs are live across
 // the DFT-16 and post-pass.
-template <int WPB = 4, int MINW = 0, bool SPLIT = false>
+// FUSE: step 3 as one asm block per two pairs (post_pair2) instead of the
+// cmul2 / pwr2 pieces: 23 -> 8 hazard nops but 142 -> 160 VGPRs, and the same
+// time (interleaved A/B, profiles/round1/probe_fft_fuse.log), so off.
+template <int WPB = 4, int MINW = 0, bool SPLIT = false, bool FUSE = false>
 __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MINW > 0 ? MINW : 1)))
 void fft1024_quad_kernel(FftParams p)
 {
@@ -435,14 +471,18 @@ void fft1024_quad_kernel(FftParams p)
                 Q0 = sel_l0(b[16 + 23 - j0], Q0);
                 Q1 = sel_l0(b[16 + 23 - j1], Q1);
             }
-            const f2 S0 = pp_s(P0, Q0), S1 = pp_s(P1, Q1);
-            const f2 D0 = pp_d(P0, Q0), D1 = pp_d(P1, Q1);
-            f2 T0, T1;
-            cmul2(T0, D0, tw3[16 * j0 + t], T1, D1, tw3[16 * j1 + t]);
-            const f2 re0 = pp_re(S0, T0), re1 = pp_re(S1, T1);
-            const f2 im0 = pp_im(S0, T0), im1 = pp_im(S1, T1);
             f2 pw0, pw1;  // (|X[kP]|^2, |X[512-kP]|^2)
-            pwr2(pw0, re0, im0, pw1, re1, im1);
+            if constexpr (FUSE) {
+                post_pair2(pw0, P0, Q0, tw3[16 * j0 + t], pw1, P1, Q1, tw3[16 * j1 + t]);
+            } else {
+                const f2 S0 = pp_s(P0, Q0), S1 = pp_s(P1, Q1);
+                const f2 D0 = pp_d(P0, Q0), D1 = pp_d(P1, Q1);
+                f2 T0, T1;
+                cmul2(T0, D0, tw3[16 * j0 + t], T1, D1, tw3[16 * j1 + t]);
+                const f2 re0 = pp_re(S0, T0), re1 = pp_re(S1, T1);
+                const f2 im0 = pp_im(S0, T0), im1 = pp_im(S1, T1);
+                pwr2(pw0, re0, im0, pw1, re1, im1);
+            }
             ps[16 * j0] = pw0;
             ps[16 * j1] = pw1;
         });
@@ -482,13 +522,13 @@ void fft1024_quad_kernel(FftParams p)
 
 // Persistent grid: as many blocks as fit the chip, each wave strides over
 // groups of 4 windows (the LDS twiddle tables are built once per block).
-template <int WPB, int MINW, bool SPLIT = false>
+template <int WPB, int MINW, bool SPLIT = false, bool FUSE = false>
 hipError_t launch_fft_quad_t(const FftParams &p, hipStream_t s)
 {
     int dev = 0, cus = 256, per_cu = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fft1024_quad_kernel<WPB, MINW, SPLIT>,
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fft1024_quad_kernel<WPB, MINW, SPLIT, FUSE>,
                                                      64 * WPB, 0) != hipSuccess ||
         per_cu < 1)
         per_cu = 1;
@@ -496,7 +536,7 @@ hipError_t launch_fft_quad_t(const FftParams &p, hipStream_t s)
     long long blocks = (groups + WPB - 1) / WPB;
     blocks = std::min<long long>(blocks, (long long)cus * per_cu);
     if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL((fft1024_quad_kernel<WPB, MINW, SPLIT>), dim3((unsigned)blocks), dim3(64 * WPB), 0,
+    hipLaunchKernelGGL((fft1024_quad_kernel<WPB, MINW, SPLIT, FUSE>), dim3((unsigned)blocks), dim3(64 * WPB), 0,
                        s, p);
     return hipGetLastError();
 }
