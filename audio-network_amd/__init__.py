@@ -43,7 +43,7 @@ DEMOD_MAX_TONES = 16
 DEMOD_MAX_FRAME_PAYLOAD = 4096
 
 CH_LEFT, CH_RIGHT, CH_DOWNMIX = 0, 1, 2
-METHOD_AUTO, METHOD_GOERTZEL, METHOD_FFT, METHOD_FOLDED = 0, 1, 2, 3
+METHOD_AUTO, METHOD_GOERTZEL, METHOD_FFT, METHOD_FOLDED, METHOD_RESIDUE = 0, 1, 2, 3, 4
 
 FSK2_FREQS = (1500.0, 3000.0)                              # SURVEY §8 tone plan
 FSK8_FREQS = tuple(1500.0 + 375.0 * i for i in range(8))
@@ -232,7 +232,7 @@ class Demodulator:
 
     @property
     def method(self) -> int:
-        """Detector in use: METHOD_GOERTZEL, METHOD_FOLDED or METHOD_FFT."""
+        """Detector in use: METHOD_GOERTZEL, METHOD_FOLDED, METHOD_RESIDUE or METHOD_FFT."""
         return int(self._lib.demod_method(self._h))
 
     def pending(self) -> int:

@@ -31,6 +31,7 @@ struct demod {
     float *d_tw1024 = nullptr;
     int *d_bins = nullptr;
     float coef[kMaxTones] = {};
+    int zcls[kMaxTones] = {};   // residue detector: class each tone reads
     // staging for host-pointer calls
     int16_t *d_in = nullptr;
     size_t d_in_cap = 0;        // samples
@@ -80,14 +81,29 @@ void demod_cfg_default(demod_cfg_t *cfg)
     cfg->freqs[1] = 3000.0;
 }
 
+// Tone i's bin f_i n / fs if it is an integer (within rounding), else -1.
+static long long integer_bin(const demod_cfg_t &c, uint32_t i)
+{
+    const double b = c.freqs[i] * c.n / c.fs;
+    const double r = std::nearbyint(b);
+    if (std::fabs(b - r) > 1e-9 * std::max(1.0, b)) return -1;
+    return (long long)r;
+}
+
+// Every tone on an integer bin (residue.hip's identity).
+static bool residue_eligible(const demod_cfg_t &c)
+{
+    for (uint32_t i = 0; i < c.k; ++i)
+        if (integer_bin(c, i) < 0) return false;
+    return true;
+}
+
 // Every tone on an integer bin that is a multiple of 8 (fold.hip's identity).
 static bool fold_eligible(const demod_cfg_t &c)
 {
     for (uint32_t i = 0; i < c.k; ++i) {
-        const double b = c.freqs[i] * c.n / c.fs;
-        const double r = std::nearbyint(b);
-        if (std::fabs(b - r) > 1e-9 * std::max(1.0, b)) return false;
-        if (((long long)r) % 8 != 0) return false;
+        const long long b = integer_bin(c, i);
+        if (b < 0 || b % 8 != 0) return false;
     }
     return true;
 }
@@ -103,11 +119,13 @@ static int validate(const demod_cfg_t *c)
     if (c->channels != 1 && c->channels != 2) return DEMOD_BAD_ARG;
     if (c->channels == 2 && (c->channel_mode < 0 || c->channel_mode > 2)) return DEMOD_BAD_ARG;
     if (c->method != DEMOD_METHOD_AUTO && c->method != DEMOD_METHOD_GOERTZEL &&
-        c->method != DEMOD_METHOD_FOLDED && c->method != DEMOD_METHOD_FFT)
+        c->method != DEMOD_METHOD_FOLDED && c->method != DEMOD_METHOD_FFT &&
+        c->method != DEMOD_METHOD_RESIDUE)
         return DEMOD_UNIMPLEMENTED;
     if (c->method == DEMOD_METHOD_FFT && c->n != 1024) return DEMOD_UNIMPLEMENTED;
     if (c->reserved != 0) return DEMOD_BAD_ARG;
     if (c->method == DEMOD_METHOD_FOLDED && !fold_eligible(*c)) return DEMOD_BAD_ARG;
+    if (c->method == DEMOD_METHOD_RESIDUE && !residue_eligible(*c)) return DEMOD_BAD_ARG;
     for (uint32_t i = 0; i < c->k; ++i)
         if (!std::isfinite(c->freqs[i]) || c->freqs[i] < 0.0 || c->freqs[i] > c->fs / 2)
             return DEMOD_BAD_ARG;
@@ -138,11 +156,17 @@ static int init_device_state(demod_t *st)
     int g = (int)(c.n / 64), lg = 0;
     while ((1 << lg) < g) ++lg;
     st->log2g = lg;
-    const bool eligible = fold_eligible(c);
-    st->detector = (c.method == DEMOD_METHOD_FOLDED || (c.method == DEMOD_METHOD_AUTO && eligible &&
-                                                        c.k >= 3))
-                       ? kDetFolded
-                       : kDetGoertzel;
+    // AUTO: the plain bank is HBM-bound up to K = 2 and within
+    // a few % of it to K = 4; beyond, fold when every tone is a multiple of 8
+    // bins (K >= 3), else fold per residue class when every tone is on an
+    // integer bin (K >= 5: at K = 3, 4 the plain bank measured as fast).
+    st->detector = kDetGoertzel;
+    if (c.method == DEMOD_METHOD_FOLDED) st->detector = kDetFolded;
+    else if (c.method == DEMOD_METHOD_RESIDUE) st->detector = kDetResidue;
+    else if (c.method == DEMOD_METHOD_AUTO) {
+        if (c.k >= 3 && fold_eligible(c)) st->detector = kDetFolded;
+        else if (c.k >= 5 && residue_eligible(c)) st->detector = kDetResidue;
+    }
     if (c.method == DEMOD_METHOD_FFT) {
         st->detector = kDetFft;
         std::vector<float> t1(1024), t2(1024);
@@ -167,15 +191,37 @@ static int init_device_state(demod_t *st)
     // Rotation of each lane's piece into window phase, X += A s1 - B s2:
     //   Goertzel: segment j = samples [64j, 64j+64): A = e^{-jw(64j+63)}, B = e^{-jw(64j+64)}
     //   Folded:   folded samples [8j, 8j+8):         A = e^{-jw(8j+7)},   B = e^{-jw(8j+8)}
-    const double span = st->detector == kDetFolded ? 8.0 : 64.0;
-    std::vector<float4> rot((size_t)c.k * g);
+    //   Residue:  as Folded, with the class input s = (lo, hi) mapped to the
+    //             complex s_c = (alpha lo + beta hi) + i gamma hi, folded into
+    //             X = lo1 C1 + hi1 C2 + lo2 C3 + hi2 C4 (residue.hip):
+    //             C1 = alpha A, C2 = beta A + gamma iA, C3 = -alpha B, C4 = -(beta B + gamma iB)
+    const bool residue = st->detector == kDetResidue;
+    const double span = (st->detector == kDetFolded || residue) ? 8.0 : 64.0;
+    std::vector<float4> rot((size_t)c.k * g * (residue ? 2 : 1));
     for (uint32_t k = 0; k < c.k; ++k) {
         const double w = 2.0 * M_PI * c.freqs[k] / c.fs;
         st->coef[k] = (float)(2.0 * std::cos(w));
+        // residue rho = bin mod 8 -> (class, alpha, beta, gamma); rho and 8 - rho
+        // share a class (conjugates), class 0 carries (Z0, Z4)
+        static const int kCls[8] = {0, 1, 3, 2, 0, 2, 3, 1};
+        static const double kGam[8] = {0, 1, -1, 1, 0, -1, 1, -1};
+        const int rho = residue ? (int)(integer_bin(c, k) % 8) : 0;
+        const double al = rho == 4 ? 0.0 : 1.0, be = rho == 4 ? 1.0 : 0.0, ga = kGam[rho];
+        st->zcls[k] = kCls[rho];
         for (int j = 0; j < g; ++j) {
             const double a = -w * (span * j + span - 1.0), b = -w * (span * j + span);
-            rot[(size_t)k * g + j] = make_float4((float)std::cos(a), (float)std::sin(a),
-                                                 (float)std::cos(b), (float)std::sin(b));
+            const double Ar = std::cos(a), Ai = std::sin(a), Br = std::cos(b), Bi = std::sin(b);
+            if (!residue) {
+                rot[(size_t)k * g + j] = make_float4((float)Ar, (float)Ai, (float)Br, (float)Bi);
+                continue;
+            }
+            // iA = (-Ai, Ar)
+            rot[((size_t)k * g + j) * 2] =
+                make_float4((float)(al * Ar), (float)(al * Ai), (float)(be * Ar - ga * Ai),
+                            (float)(be * Ai + ga * Ar));
+            rot[((size_t)k * g + j) * 2 + 1] =
+                make_float4((float)(-al * Br), (float)(-al * Bi), (float)(-(be * Br - ga * Bi)),
+                            (float)(-(be * Bi + ga * Br)));
         }
     }
     HIP_TRY(hipMalloc(&st->d_rot, rot.size() * sizeof(float4)));
@@ -249,9 +295,10 @@ int demod_reset(demod_t *st)
 int demod_method(const demod_t *st)
 {
     if (!st) return DEMOD_BAD_ARG;
-    return st->detector == kDetFolded ? DEMOD_METHOD_FOLDED
-         : st->detector == kDetFft    ? DEMOD_METHOD_FFT
-                                      : DEMOD_METHOD_GOERTZEL;
+    return st->detector == kDetFolded  ? DEMOD_METHOD_FOLDED
+         : st->detector == kDetFft     ? DEMOD_METHOD_FFT
+         : st->detector == kDetResidue ? DEMOD_METHOD_RESIDUE
+                                       : DEMOD_METHOD_GOERTZEL;
 }
 
 int demod_pending(const demod_t *st)
@@ -310,7 +357,10 @@ static int enqueue_batch(demod_t *st, const int16_t *d_pcm, size_t n_windows, ui
     p.rot = st->d_rot;
     p.sym = d_sym;
     p.mag = d_mag;
-    for (uint32_t k = 0; k < st->cfg.k; ++k) p.coef[k] = st->coef[k];
+    for (uint32_t k = 0; k < st->cfg.k; ++k) {
+        p.coef[k] = st->coef[k];
+        p.zcls[k] = st->zcls[k];
+    }
     HIP_TRY(launch_detector(st->detector, p, s));
     return (int)n_windows;
 }

@@ -24,6 +24,7 @@ struct GoertzelParams {
     uint8_t *sym;            // [n_windows]
     float *mag;              // [n_windows][k] or nullptr
     float coef[kMaxTones];   // 2 cos(w_k)
+    int zcls[kMaxTones];     // residue.hip: residue class (0..3) tone k reads
     int xcd_swizzle;         // 1: blocks b, b+8, b+16.. (one XCD) take adjacent tiles
 };
 
@@ -83,8 +84,12 @@ struct SynthParams {
 constexpr int kDetGoertzel = 1;  // goertzel.hip: 64-sample lane segments
 constexpr int kDetFft = 2;       // fft.hip: 1024-point real FFT, argmax over tone bins
 constexpr int kDetFolded = 3;    // fold.hip: Goertzel on the N/8-folded window
+constexpr int kDetResidue = 4;   // residue.hip: per-residue-class folding (any integer bins)
 
 hipError_t launch_detector(int detector, const GoertzelParams &p, hipStream_t s);
+// residue.hip: rotation table is [k][g][2] float4 {C1, C2}, {C3, C4}
+const void *residue_kernel_ptr(int k, int log2g);
+size_t residue_lds_bytes(int k, int log2g, int qp = 2);
 int tile_grid(long long n_windows, int log2g);
 hipError_t launch_synth(const SynthParams &p, hipStream_t s);
 hipError_t launch_fft(const FftParams &p, hipStream_t s);       // 64 lanes / window (fft.hip)

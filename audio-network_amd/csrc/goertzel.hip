@@ -293,11 +293,14 @@ const void *fold_kernel_ptr(int k, int log2g);
 
 hipError_t launch_detector(int detector, const GoertzelParams &p, hipStream_t s)
 {
-    const void *f = detector == kDetFolded ? fold_kernel_ptr(p.k, p.log2g) : kernel_ptr(p.k, p.log2g);
+    const void *f = detector == kDetFolded    ? fold_kernel_ptr(p.k, p.log2g)
+                  : detector == kDetResidue ? residue_kernel_ptr(p.k, p.log2g)
+                                            : kernel_ptr(p.k, p.log2g);
     if (!f) return hipErrorInvalidValue;
+    const size_t lds = detector == kDetResidue ? residue_lds_bytes(p.k, p.log2g) : 0;
     void *args[] = {const_cast<GoertzelParams *>(&p)};
     return hipLaunchKernel(f, dim3(tile_grid(p.n_windows, p.log2g)), dim3(64 * kWavesPerBlock),
-                           args, 0, s);
+                           args, lds, s);
 }
 
 }  // namespace fskd

@@ -1,0 +1,296 @@
+// residue.hip — Goertzel tone bank on the window folded per residue class
+// mod 8: any tone plan whose tones sit on integer bins (the usual FSK choice:
+// integer bins are what makes the tones orthogonal over a window).
+//
+// Identity (exact): with P = N/8, r < P and m < 8, a tone on integer bin
+// b = 8 beta + rho has
+//     W^{b (r + m P)} = W^{b r} e^{-j 2 pi rho m / 8},
+// so
+//     X_b = sum_{r<P} W^{b r} Z_rho[r],   Z_rho[r] = sum_{m<8} x[r + m P] w8^{rho m},
+// i.e. Z_rho is bin rho of an 8-point DFT over the eight samples spaced P
+// apart. For real x, Z_{8-rho} = conj Z_rho, so four classes cover all eight
+// residues:
+//     class 0: (Z0, Z4)       both real, carried as one pair
+//     class 1: Z1             (rho 7 = conj)
+//     class 2: Z3             (rho 5 = conj)
+//     class 3: (e1, e3) = Z6  (rho 2 = conj)
+// fold.hip is the rho = 0 special case (every tone a multiple of 8 bins). The
+// Goertzel recurrence s = z + c s1 - s2 is linear with a real coefficient, so
+// it runs on the complex z as one packed fp32 pair (re, im) per tone, over 8
+// folded samples per lane instead of 64 raw ones. The class a tone reads is a
+// run-time uniform value: the four class pairs of each folded sample go
+// through a wave-private LDS slice and each tone reads its class at a uniform
+// offset (an SGPR-indexed register file; no per-tone branches, so the K
+// chains stay interleaved). The conjugation, and for class 0 the choice of
+// Z0 or Z4, is folded into the per-lane rotation constants on the host:
+//     X = s1.lo C1 + s1.hi C2 + s2.lo C3 + s2.hi C4   (C* complex, demod_api.cpp).
+//
+// Oracle: the same quantities as oracle/fsk_oracle.c:goertzel_window_d (the
+// plain sequential recurrence over all N samples), to fp32 rounding; the
+// 8-point butterflies are exact integer sums in fp32 except the two products
+// by 1/sqrt 2.
+//
+// Layout: as fold.hip — lane j of a window's G-lane group loads chunks
+// j + G m (m = 0..7), whole 128-byte lines per wave instruction, so folded
+// samples r = 8j .. 8j+7 of all eight spacings m arrive in the lane that
+// folds them. VALU per sample ~ 2.3 for the butterflies + K/4 for the
+// recurrences (vs ~ 1 + K for the plain bank), so K = 8 stays HBM-bound.
+#include "demod_internal.h"
+
+namespace fskd {
+
+typedef unsigned int u32x4r __attribute__((ext_vector_type(4)));
+typedef float f2 __attribute__((ext_vector_type(2)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+template <int CTRL>
+__device__ __forceinline__ float dppr_(float v)
+{
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+
+__device__ __forceinline__ float group_sum_r(float v, int log2g)
+{
+    if (log2g > 0) v += dppr_<0xB1>(v);
+    if (log2g > 1) v += dppr_<0x4E>(v);
+    if (log2g > 2) v += dppr_<0x141>(v);
+    if (log2g > 3) v += dppr_<0x140>(v);
+    if (log2g > 4) v += __shfl_xor(v, 16);
+    if (log2g > 5) v += __shfl_xor(v, 32);
+    return v;
+}
+
+// Class pairs of one folded sample from its eight spaced samples x[m].
+//   a_m = x_m + x_{m+4}, d_m = x_m - x_{m+4}           (m < 4)
+//   e0 = a0 + a2, e1 = a0 - a2, e2 = a1 + a3, e3 = a1 - a3
+//   Z0 = e0 + e2, Z4 = e0 - e2, Z2 = e1 - j e3 (class 3 stores (e1, e3) = Z6)
+//   u = d1 - d3, v = d1 + d3
+//   Z1 = (d0 + u/sqrt2) - j (d2 + v/sqrt2),  Z3 = (d0 - u/sqrt2) + j (d2 - v/sqrt2)
+__device__ __forceinline__ void residue_classes(const float x[8], f2 &z04, f2 &z1, f2 &z3, f2 &z6)
+{
+    const float kr = 0.70710678118654752f;
+    const f2 a02 = f2{x[0], x[2]} + f2{x[4], x[6]};
+    const f2 d02 = f2{x[0], x[2]} - f2{x[4], x[6]};
+    const f2 a13 = f2{x[1], x[3]} + f2{x[5], x[7]};
+    const f2 d13 = f2{x[1], x[3]} - f2{x[5], x[7]};
+    const f2 e01 = f2{a02.x, a02.x} + f2{a02.y, -a02.y};
+    const f2 e23 = f2{a13.x, a13.x} + f2{a13.y, -a13.y};
+    z04 = f2{e01.x, e01.x} + f2{e23.x, -e23.x};
+    z6 = f2{e01.y, e23.y};
+    const f2 uv = f2{d13.x, d13.x} + f2{-d13.y, d13.y};
+    z1 = __builtin_elementwise_fma(uv, f2{kr, -kr}, f2{d02.x, -d02.y});
+    z3 = __builtin_elementwise_fma(uv, f2{-kr, -kr}, d02);
+}
+
+// The same butterflies as one asm block with the op_sel / neg modifiers
+// spelled out: hipcc builds per-half negations and half swaps from v_xor +
+// v_mov. Inputs are the pairs (x0, x2), (x4, x6), (x1, x3), (x5, x7); kk =
+// (1/sqrt2, 1/sqrt2). The sums are formed in place ((a0, a2) -> (e0, e1),
+// (a1, a3) -> (e2, e3), (d1, d3) -> (u, v)) to keep the register footprint at
+// 4 scratch pairs, and every packed result is read no earlier than two
+// instructions after it is written (gfx950 needs one wait state after a
+// packed-fp32 write), so the block needs no s_nop.
+__device__ __forceinline__ void residue_classes_asm(f2 p02, f2 p46, f2 p13, f2 p57, f2 kk,
+                                                   f2 &z04, f2 &z1, f2 &z3, f2 &z6)
+{
+    f2 t02, d02, t13, t_d13;
+    asm("v_pk_add_f32 %[t02], %[p02], %[p46]\n\t"                                    // (a0, a2)
+        "v_pk_add_f32 %[d02], %[p02], %[p46] neg_lo:[0,1] neg_hi:[0,1]\n\t"          // (d0, d2)
+        "v_pk_add_f32 %[t13], %[p13], %[p57]\n\t"                                    // (a1, a3)
+        "v_pk_add_f32 %[d13], %[p13], %[p57] neg_lo:[0,1] neg_hi:[0,1]\n\t"          // (d1, d3)
+        "v_pk_add_f32 %[t02], %[t02], %[t02] op_sel:[0,1] op_sel_hi:[0,1] neg_hi:[0,1]\n\t"  // (e0, e1)
+        "v_pk_add_f32 %[t13], %[t13], %[t13] op_sel:[0,1] op_sel_hi:[0,1] neg_hi:[0,1]\n\t"  // (e2, e3)
+        "v_pk_add_f32 %[d13], %[d13], %[d13] op_sel:[0,1] op_sel_hi:[0,1] neg_lo:[0,1]\n\t"  // (u, v)
+        "v_pk_add_f32 %[z04], %[t02], %[t13] op_sel_hi:[0,0] neg_hi:[0,1]\n\t"       // (Z0, Z4)
+        "v_pk_mov_b32 %[z6], %[t02], %[t13] op_sel:[1,1]\n\t"                         // (e1, e3)
+        "v_pk_fma_f32 %[z1], %[d13], %[kk], %[d02] neg_hi:[0,1,1]\n\t"               // Z1
+        "v_pk_fma_f32 %[z3], %[d13], %[kk], %[d02] neg_lo:[0,1,0] neg_hi:[0,1,0]"       // Z3
+        : [t02] "=&v"(t02), [d02] "=&v"(d02), [t13] "=&v"(t13), [d13] "=&v"(t_d13),
+          [z04] "=v"(z04), [z1] "=v"(z1), [z3] "=v"(z3), [z6] "=v"(z6)
+        : [p02] "v"(p02), [p46] "v"(p46), [p13] "v"(p13), [p57] "v"(p57), [kk] "s"(kk));
+}
+
+// Dynamic LDS: [K][G][2] float4 rotation constants (block), then per wave
+// [4 classes][QP sample pairs][64 lanes] float4 (4 QP KiB).
+constexpr int kResidueQP = 2;  // shipped: two sample pairs per LDS round
+
+// Tunables (defaults = shipped, chosen with scripts/probe.hip):
+//   ASM   butterflies as residue_classes2 (else the plain-C residue_classes),
+//   ROTV  rotation constants in VGPRs (8 per tone) instead of the LDS table,
+//   MINW  > 0: ask for MINW waves per SIMD (VGPR budget 512 / MINW),
+//   QP    sample pairs per LDS round (1, 2 or 4): 4 QP KiB of LDS per wave,
+//   PF    prefetch the wave's next tile before computing the current one
+//         (only matters on grids with more than one tile per wave).
+template <int K, int LOG2G, int WPB = kWavesPerBlock, bool ASM = true, bool ROTV = false,
+          int MINW = (K <= 8 ? 4 : 0), int QP = kResidueQP, bool PF = false>
+__global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MINW > 0 ? MINW : 1)))
+void residue_tile_kernel(GoertzelParams p)
+{
+    extern __shared__ f4 lds_r[];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int log2g = LOG2G >= 0 ? LOG2G : p.log2g;
+    const int g = 1 << log2g;
+    const int n = 64 << log2g;
+    const int j = lane & (g - 1);
+    const int win_in_tile = lane >> log2g;
+    const long long wins_per_tile = 64 >> log2g;
+    const long long n_tiles = (p.n_windows + wins_per_tile - 1) / wins_per_tile;
+
+    f4 *rot = lds_r;
+    f4 *zw = lds_r + K * g * 2 + wave * (4 * QP * 64) + lane;
+    const f4 *grot = reinterpret_cast<const f4 *>(p.rot);
+    int goff[8];
+#pragma unroll
+    for (int m = 0; m < 8; ++m)
+        goff[m] = (int)(((long long)win_in_tile * p.hop + (long long)(j + g * m) * 8) * 2);
+    auto load_tile = [&](long long tt, u32x4r v[8]) {
+        const long long wbase = tt * wins_per_tile;
+        long long bytes = ((p.n_windows - wbase - 1) * p.hop + n) * 2;
+        if (bytes > 0x7FFFFFF0LL) bytes = 0x7FFFFFF0LL;
+        __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)(p.pcm + wbase * p.hop), (short)0, (int)bytes, 0x00020000);
+#pragma unroll
+        for (int m = 0; m < 8; ++m)
+            v[m] = __builtin_amdgcn_raw_buffer_load_b128(rs, goff[m], 0, 2);
+    };
+
+    const long long stride = (long long)gridDim.x * WPB;
+    long long t = tile_block(p.xcd_swizzle) * WPB + wave;
+    // The first tile's loads go out before the rotation table is staged and
+    // the block barrier, so the two latencies overlap: with one tile per wave
+    // (the usual grid) this prologue is on every wave's critical path.
+    u32x4r v[8];
+    if (t < n_tiles) load_tile(t, v);
+    f4 rv[ROTV ? 2 * K : 1];
+    if (ROTV) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            rv[2 * k] = grot[(k * g + j) * 2];
+            rv[2 * k + 1] = grot[(k * g + j) * 2 + 1];
+        }
+    } else {
+        for (int i = threadIdx.x; i < K * g * 2; i += 64 * WPB) rot[i] = grot[i];
+        __syncthreads();
+    }
+    const f2 kk = f2{0.70710678118654752f, 0.70710678118654752f};
+
+    for (bool first = true; t < n_tiles; t += stride, first = false) {
+        const long long wbase = t * wins_per_tile;
+        u32x4r cur[8];
+        if (PF) {
+#pragma unroll
+            for (int m = 0; m < 8; ++m) cur[m] = v[m];
+            if (t + stride < n_tiles) load_tile(t + stride, v);
+        } else {
+            if (!first) load_tile(t, v);
+#pragma unroll
+            for (int m = 0; m < 8; ++m) cur[m] = v[m];
+        }
+
+        f2 s1[K], s2[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) { s1[k] = f2{0.f, 0.f}; s2[k] = f2{0.f, 0.f}; }
+
+        // 4 / QP rounds of 2 QP folded samples: classes -> LDS, then every
+        // tone advances 2 QP steps reading its class
+#pragma unroll
+        for (int h = 0; h < 4 / QP; ++h) {
+#pragma unroll
+            for (int qp = 0; qp < QP; ++qp) {
+                const int d = QP * h + qp;  // dword d of each chunk = samples 2d, 2d+1
+                f2 c[2][4];
+                float x[2][8];
+#pragma unroll
+                for (int e = 0; e < 2; ++e)
+#pragma unroll
+                    for (int m = 0; m < 8; ++m) {
+                        const uint32_t w = cur[m][d];
+                        x[e][m] = e ? (float)((int)w >> 16) : (float)(int)(short)(w & 0xFFFFu);
+                    }
+                if (ASM) {
+#pragma unroll
+                    for (int e = 0; e < 2; ++e)
+                        residue_classes_asm(f2{x[e][0], x[e][2]}, f2{x[e][4], x[e][6]},
+                                            f2{x[e][1], x[e][3]}, f2{x[e][5], x[e][7]}, kk,
+                                            c[e][0], c[e][1], c[e][2], c[e][3]);
+                } else {
+                    residue_classes(x[0], c[0][0], c[0][1], c[0][2], c[0][3]);
+                    residue_classes(x[1], c[1][0], c[1][1], c[1][2], c[1][3]);
+                }
+#pragma unroll
+                for (int cl = 0; cl < 4; ++cl)
+                    zw[(cl * QP + qp) * 64] = f4{c[0][cl].x, c[0][cl].y, c[1][cl].x, c[1][cl].y};
+            }
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const f4 *zk = zw + p.zcls[k] * (QP * 64);
+                const f2 cc = f2{p.coef[k], p.coef[k]};
+#pragma unroll
+                for (int qp = 0; qp < QP; ++qp) {
+                    const f4 z = zk[qp * 64];
+                    f2 a = __builtin_elementwise_fma(cc, s1[k], f2{z.x, z.y} - s2[k]);
+                    s2[k] = s1[k];
+                    s1[k] = a;
+                    a = __builtin_elementwise_fma(cc, s1[k], f2{z.z, z.w} - s2[k]);
+                    s2[k] = s1[k];
+                    s1[k] = a;
+                }
+            }
+        }
+
+        float best = -1.f;
+        int arg = 0;
+        float P[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const f4 c12 = ROTV ? rv[2 * k] : rot[(k * g + j) * 2];
+            const f4 c34 = ROTV ? rv[2 * k + 1] : rot[(k * g + j) * 2 + 1];
+            f2 X = f2{c12.x, c12.y} * s1[k].x;
+            X = __builtin_elementwise_fma(f2{c12.z, c12.w}, f2{s1[k].y, s1[k].y}, X);
+            X = __builtin_elementwise_fma(f2{c34.x, c34.y}, f2{s2[k].x, s2[k].x}, X);
+            X = __builtin_elementwise_fma(f2{c34.z, c34.w}, f2{s2[k].y, s2[k].y}, X);
+            const float re = group_sum_r(X.x, log2g);
+            const float im = group_sum_r(X.y, log2g);
+            P[k] = fmaf(re, re, im * im);
+            if (P[k] > best) { best = P[k]; arg = k; }
+        }
+
+        const long long w = wbase + win_in_tile;
+        if (w < p.n_windows) {
+            if (j == 0) p.sym[w] = (uint8_t)arg;
+            if (p.mag) {
+#pragma unroll
+                for (int k = 0; k < K; ++k)
+                    if ((k & (g - 1)) == j) p.mag[w * K + k] = P[k];
+            }
+        }
+    }
+}
+
+size_t residue_lds_bytes(int k, int log2g, int qp)
+{
+    return ((size_t)k * (1u << log2g) * 2 + (size_t)kWavesPerBlock * 4 * qp * 64) * sizeof(f4);
+}
+
+template <int K>
+static const void *residue_kernel_for(int log2g)
+{
+    if (log2g == 4) return reinterpret_cast<const void *>(&residue_tile_kernel<K, 4>);
+    return reinterpret_cast<const void *>(&residue_tile_kernel<K, -1>);
+}
+
+const void *residue_kernel_ptr(int k, int log2g)
+{
+    switch (k) {
+#define FSKD_CASE(K) case K: return residue_kernel_for<K>(log2g);
+        FSKD_CASE(1) FSKD_CASE(2) FSKD_CASE(3) FSKD_CASE(4)
+        FSKD_CASE(5) FSKD_CASE(6) FSKD_CASE(7) FSKD_CASE(8)
+        FSKD_CASE(9) FSKD_CASE(10) FSKD_CASE(11) FSKD_CASE(12)
+        FSKD_CASE(13) FSKD_CASE(14) FSKD_CASE(15) FSKD_CASE(16)
+#undef FSKD_CASE
+    default: return nullptr;
+    }
+}
+
+}  // namespace fskd

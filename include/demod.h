@@ -58,13 +58,17 @@ extern "C" {
 #define DEMOD_CH_DOWNMIX  2   /* x = (L + R) >> 1 (arithmetic shift) */
 
 /* detector selection */
-#define DEMOD_METHOD_AUTO      0 /* FOLDED when eligible and k >= 3, else GOERTZEL */
+#define DEMOD_METHOD_AUTO      0 /* FOLDED when eligible and k >= 3, else RESIDUE
+                                    when eligible and k >= 5, else GOERTZEL */
 #define DEMOD_METHOD_GOERTZEL  1 /* per-window Goertzel tone bank over all n samples */
 #define DEMOD_METHOD_FFT       2 /* full-spectrum n-point real FFT (n = 1024), argmax
                                     over the tone bins round(f*n/fs) */
 #define DEMOD_METHOD_FOLDED    3 /* Goertzel over the window folded to n/8 samples:
                                     exact when every tone is on a multiple of 8
                                     bins (f*n/fs integer, divisible by 8) */
+#define DEMOD_METHOD_RESIDUE   4 /* Goertzel over the window folded to n/8 samples per
+                                    residue class of the bin mod 8: exact when every
+                                    tone is on an integer bin (f*n/fs integer) */
 
 typedef struct demod_cfg {
     double   fs;                     /* sample rate, Hz (48000) */
@@ -95,7 +99,7 @@ void demod_destroy(demod_t *st);
  * Mirrors playback_start_new_stream (playback.cpp:67-74). */
 int demod_reset(demod_t *st);
 
-/* Detector the handle runs (DEMOD_METHOD_GOERTZEL / _FOLDED / _FFT). */
+/* Detector the handle runs (DEMOD_METHOD_GOERTZEL / _FOLDED / _RESIDUE / _FFT). */
 int demod_method(const demod_t *st);
 
 /* Number of mono samples currently carried between demodulate() calls. */

@@ -11,6 +11,7 @@
 #include "../audio-network_amd/csrc/goertzel.hip"
 #include "../audio-network_amd/csrc/synth.hip"
 #include "../audio-network_amd/csrc/fold.hip"
+#include "../audio-network_amd/csrc/residue.hip"
 #include "../audio-network_amd/csrc/fft.hip"
 #include "../audio-network_amd/csrc/fft_quad.hip"
 #include "fft_quad_r1.hip"
@@ -86,11 +87,12 @@ struct Variant {
 };
 
 static void add_variant(std::vector<Variant> &vs, const void *f, int wpb, const char *label,
-                        GoertzelParams p, int K, int cus, int tpw)
+                        GoertzelParams p, int K, int cus, int tpw, size_t lds = 0,
+                        const char *ksuffix = "")
 {
     // tpw = 0: persistent grid (co-resident blocks); tpw >= 1: tiles per wave
     int per_cu = 0;
-    CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, 64 * wpb, 0));
+    CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, 64 * wpb, lds));
     const long long n_tiles = (p.n_windows + 3) / 4;
     long long blocks = tpw ? (n_tiles + (long long)wpb * tpw - 1) / ((long long)wpb * tpw)
                            : std::min<long long>((n_tiles + wpb - 1) / wpb, (long long)cus * per_cu);
@@ -98,15 +100,15 @@ static void add_variant(std::vector<Variant> &vs, const void *f, int wpb, const 
     CK(hipMalloc(&sym, p.n_windows));
     p.sym = sym;
     char name[200];
-    std::snprintf(name, sizeof name, "%s K=%d WPB=%d %s%d grid=%lld (%d/CU)", label, K, wpb,
-                  tpw ? "tpw=" : "persist", tpw, blocks, per_cu);
+    std::snprintf(name, sizeof name, "%s K=%d%s WPB=%d %s%d grid=%lld (%d/CU)", label, K, ksuffix,
+                  wpb, tpw ? "tpw=" : "persist", tpw, blocks, per_cu);
     Variant v;
     v.name = name;
     v.bytes = (double)p.n_windows * (2048 + 1 + (p.mag ? 4 * K : 0));
     v.sym = sym;
-    v.run = [f, p, blocks, wpb](hipStream_t s) {
+    v.run = [f, p, blocks, wpb, lds](hipStream_t s) {
         void *args[] = {const_cast<GoertzelParams *>(&p)};
-        CK(hipLaunchKernel(f, dim3((unsigned)blocks), dim3(64 * wpb), args, 0, s));
+        CK(hipLaunchKernel(f, dim3((unsigned)blocks), dim3(64 * wpb), args, lds, s));
     };
     vs.push_back(v);
 }
@@ -226,6 +228,94 @@ int main(int argc, char **argv)
     add_variant(vs, FD(2, 4), 4, "fold", f2, 2, cus, 1);
     add_variant(vs, FD(8, 4), 4, "fold", f8, 8, cus, 1);
     {
+        // residue-class folding (residue.hip): rotation table as demod_api.cpp
+        auto make_res = [&](int K, const double *bins, GoertzelParams &p) {
+            static const int kCls[8] = {0, 1, 3, 2, 0, 2, 3, 1};
+            static const double kGam[8] = {0, 1, -1, 1, 0, -1, 1, -1};
+            std::vector<float4> rot(K * 16 * 2);
+            for (int k = 0; k < K; ++k) {
+                const double w = 2 * M_PI * bins[k] / 1024.0;
+                const int rho = (int)bins[k] % 8;
+                const double al = rho == 4 ? 0 : 1, be = rho == 4 ? 1 : 0, ga = kGam[rho];
+                p.coef[k] = (float)(2 * std::cos(w));
+                p.zcls[k] = kCls[rho];
+                for (int j = 0; j < 16; ++j) {
+                    const double a = -w * (8.0 * j + 7), b = -w * (8.0 * j + 8);
+                    const double Ar = std::cos(a), Ai = std::sin(a), Br = std::cos(b), Bi = std::sin(b);
+                    rot[(k * 16 + j) * 2] = make_float4(al * Ar, al * Ai, be * Ar - ga * Ai, be * Ai + ga * Ar);
+                    rot[(k * 16 + j) * 2 + 1] =
+                        make_float4(-al * Br, -al * Bi, -(be * Br - ga * Bi), -(be * Bi + ga * Br));
+                }
+            }
+            float4 *d;
+            CK(hipMalloc(&d, rot.size() * sizeof(float4)));
+            CK(hipMemcpy(d, rot.data(), rot.size() * sizeof(float4), hipMemcpyHostToDevice));
+            p.rot = d;
+            p.k = K;
+        };
+#define RZ(K) reinterpret_cast<const void *>(&residue_tile_kernel<K, 4>)
+#define RZC(K) reinterpret_cast<const void *>(&residue_tile_kernel<K, 4, 4, false, false>)
+#define RZV(K) reinterpret_cast<const void *>(&residue_tile_kernel<K, 4, 4, true, true>)
+#define RZW(K, W) reinterpret_cast<const void *>(&residue_tile_kernel<K, 4, 4, true, false, W>)
+#define RZQ(K, W, Q, PF) reinterpret_cast<const void *>(&residue_tile_kernel<K, 4, 4, true, false, W, Q, PF>)
+        static double bo[16];
+        for (int i = 0; i < 16; ++i) bo[i] = 32 + 9 * i;  // every class mod 8
+        static GoertzelParams r8s = p8, r3 = p8, r4 = p8, r8 = p8, r16 = p8, g3 = p8, g4 = p8, g8 = p8;
+        make_res(8, b8, r8s);
+        make_res(3, bo, r3);
+        make_res(4, bo, r4);
+        make_res(8, bo, r8);
+        make_res(16, bo, r16);
+        make_rot(3, bo, g3);
+        make_rot(4, bo, g4);
+        make_rot(8, bo, g8);
+        g3.k = 3;
+        g4.k = 4;
+        float *mag16;
+        CK(hipMalloc(&mag16, W * 16 * sizeof(float)));
+        r16.mag = mag16;
+        add_variant(vs, RZ(8), 4, "residue (survey plan)", r8s, 8, cus, 1, residue_lds_bytes(8, 4));
+        add_variant(vs, GZP(3), 4, "goertzel PK", g3, 3, cus, 1, 0, "o");
+        add_variant(vs, RZ(3), 4, "residue", r3, 3, cus, 1, residue_lds_bytes(3, 4), "o");
+        add_variant(vs, GZP(4), 4, "goertzel PK", g4, 4, cus, 1, 0, "o");
+        add_variant(vs, RZ(4), 4, "residue", r4, 4, cus, 1, residue_lds_bytes(4, 4), "o");
+        add_variant(vs, GZP(8), 4, "goertzel PK", g8, 8, cus, 1, 0, "o");
+        add_variant(vs, RZ(8), 4, "residue", r8, 8, cus, 1, residue_lds_bytes(8, 4), "o");
+        add_variant(vs, RZC(8), 4, "residue C-butterfly", r8, 8, cus, 1, residue_lds_bytes(8, 4), "o");
+        add_variant(vs, RZV(8), 4, "residue VGPR-rot", r8, 8, cus, 1, residue_lds_bytes(8, 4), "o");
+        add_variant(vs, RZW(8, 4), 4, "residue MINW4", r8, 8, cus, 1, residue_lds_bytes(8, 4), "o");
+        add_variant(vs, RZW(8, 5), 4, "residue MINW5", r8, 8, cus, 1, residue_lds_bytes(8, 4), "o");
+        // measured, not shipped (profiles/round1/probe_residue.log): QP1 (4 KiB LDS
+        // per wave) with MINW5/6 spills; QP4 halves occupancy; PF on 2-4 tiles
+        // per wave and VGPR-resident rotations are slower
+        add_variant(vs, RZQ(8, 4, 1, false), 4, "residue MINW4 QP1", r8, 8, cus, 1, residue_lds_bytes(8, 4, 1), "o");
+        add_variant(vs, RZQ(8, 3, 2, true), 4, "residue MINW3 PF", r8, 8, cus, 4, residue_lds_bytes(8, 4, 2), "o");
+        {
+            static GoertzelParams r5 = p8, r6 = p8, g5 = p8, g6 = p8;
+            make_res(5, bo, r5);
+            make_res(6, bo, r6);
+            make_rot(5, bo, g5);
+            make_rot(6, bo, g6);
+            g5.k = 5;
+            g6.k = 6;
+            add_variant(vs, GZP(5), 4, "goertzel PK", g5, 5, cus, 1, 0, "o");
+            add_variant(vs, RZ(5), 4, "residue", r5, 5, cus, 1, residue_lds_bytes(5, 4), "o");
+            add_variant(vs, GZP(6), 4, "goertzel PK", g6, 6, cus, 1, 0, "o");
+            add_variant(vs, RZ(6), 4, "residue", r6, 6, cus, 1, residue_lds_bytes(6, 4), "o");
+            static GoertzelParams g16 = p8;
+            make_rot(16, bo, g16);
+            g16.k = 16;
+            g16.mag = mag16;
+            add_variant(vs, GZP(16), 4, "goertzel PK", g16, 16, cus, 1, 0, "o");
+        }
+        add_variant(vs, RZ(16), 4, "residue", r16, 16, cus, 1, residue_lds_bytes(16, 4), "o");
+#undef RZ
+#undef RZC
+#undef RZV
+#undef RZW
+#undef RZQ
+    }
+    {
         // FFT detector tables (2-FSK bins 32, 64)
         std::vector<float> t1(1024), t2(1024);
         for (int m = 0; m < 512; ++m) {
@@ -326,11 +416,23 @@ int main(int argc, char **argv)
         vs.push_back(v);
     }
 
-    // PROBE_FILTER=substr keeps only matching variants (e.g. for rocprofv3 --pmc)
+    // PROBE_FILTER=substr[|substr...] keeps only matching variants (e.g. for
+    // rocprofv3 --pmc)
     if (const char *flt = std::getenv("PROBE_FILTER")) {
+        std::vector<std::string> subs;
+        for (std::string f = flt;;) {
+            const size_t bar = f.find('|');
+            subs.push_back(f.substr(0, bar));
+            if (bar == std::string::npos) break;
+            f = f.substr(bar + 1);
+        }
         std::vector<Variant> keep;
         for (auto &v : vs)
-            if (v.name.find(flt) != std::string::npos) keep.push_back(v);
+            for (auto &sub : subs)
+                if (v.name.find(sub) != std::string::npos) {
+                    keep.push_back(v);
+                    break;
+                }
         vs.swap(keep);
         if (vs.empty()) return 0;
     }

@@ -47,18 +47,53 @@ def run_case(A, O, freqs, n=1024, W=257, hop=None, seed=1, amplitude=8000, sigma
     return err
 
 
-GOERTZEL, FOLDED = 1, 3
+GOERTZEL, FOLDED, RESIDUE = 1, 3, 4
+# 8-FSK on integer bins 32 + 9 i (46.875 Hz spacing): bins 32..95 hit every
+# residue class mod 8, so only the residue detector folds this plan
+FSK8_ODD = tuple(46.875 * (32 + 9 * i) for i in range(8))
 
 
-@pytest.mark.parametrize("method", [GOERTZEL, FOLDED])
+@pytest.mark.parametrize("method", [GOERTZEL, FOLDED, RESIDUE])
 @pytest.mark.parametrize("W", [1, 2, 3, 4, 5, 63, 1000, 4097])
 def test_fsk2_window_counts(A, O, torch, W, method):
     run_case(A, O, A.FSK2_FREQS, W=W, seed=W, method=method)
 
 
-@pytest.mark.parametrize("method", [GOERTZEL, FOLDED])
+@pytest.mark.parametrize("method", [GOERTZEL, FOLDED, RESIDUE])
 def test_fsk8(A, O, torch, method):
     run_case(A, O, A.FSK8_FREQS, W=3001, seed=8, method=method)
+
+
+@pytest.mark.parametrize("method", [GOERTZEL, RESIDUE])
+def test_fsk8_every_residue_class(A, O, torch, method):
+    run_case(A, O, FSK8_ODD, W=3001, seed=88, method=method)
+
+
+@pytest.mark.parametrize("k", list(range(1, 17)))
+def test_residue_tone_counts_integer_bins(A, O, torch, k):
+    # random distinct integer bins >= 3 apart, every residue class mod 8 in play
+    rng = np.random.default_rng(500 + k)
+    while True:
+        b = np.sort(rng.choice(np.arange(8, 500), k, replace=False))
+        if k == 1 or np.diff(b).min() >= 3:
+            break
+    freqs = tuple(float(x) * 46.875 for x in rng.permutation(b))
+    run_case(A, O, freqs, W=333, seed=k, method=RESIDUE)
+
+
+@pytest.mark.parametrize("n", [64, 128, 256, 512, 1024, 2048, 4096])
+@pytest.mark.parametrize("hop_div", [1, 4])
+def test_residue_all_lengths(A, O, torch, n, hop_div):
+    # integer bins 3, 4, 5, ... for this n (bin spacing fs/n): every class
+    k_max = min(8, n // 2 - 4)
+    freqs = tuple((3 + 5 * i) * 48000.0 / n for i in range(k_max) if 3 + 5 * i < n // 2)
+    run_case(A, O, freqs, n=n, W=120, hop=n // hop_div, seed=n + hop_div, method=RESIDUE)
+
+
+def test_residue_rejects_noninteger_bins(A, torch):
+    with pytest.raises(A.DemodError) as e:
+        A.Demodulator(freqs=(1500.0, 1510.0, 3000.0), method=RESIDUE)
+    assert e.value.code == A.DEMOD_BAD_ARG
 
 
 def test_auto_method_selection(A, torch):
@@ -67,7 +102,15 @@ def test_auto_method_selection(A, torch):
     with A.Demodulator(freqs=A.FSK2_FREQS) as d:
         assert d.method == GOERTZEL          # plain tone bank already HBM-bound
     with A.Demodulator(freqs=(1500.0, 1546.875, 3000.0)) as d:
-        assert d.method == GOERTZEL          # bin 33: not a multiple of 8
+        assert d.method == GOERTZEL          # bin 33, K = 3: plain bank as fast
+    with A.Demodulator(freqs=FSK8_ODD[:5]) as d:
+        assert d.method == RESIDUE           # integer bins, not multiples of 8, K >= 5
+    with A.Demodulator(freqs=FSK8_ODD) as d:
+        assert d.method == RESIDUE
+    with A.Demodulator(freqs=(1500.0, 1510.0, 3000.0)) as d:
+        assert d.method == GOERTZEL          # 1510 Hz: not an integer bin
+    with A.Demodulator(freqs=(1500.0, 1546.875)) as d:
+        assert d.method == GOERTZEL          # K = 2: plain bank is HBM-bound
 
 
 @pytest.mark.parametrize("n", [64, 128, 256, 512, 1024, 2048, 4096])
@@ -102,14 +145,17 @@ def test_sliding_hop(A, O, torch, hop):
     run_case(A, O, A.FSK2_FREQS, W=40, hop=hop, seed=hop)
 
 
-@pytest.mark.parametrize("method", [GOERTZEL, FOLDED])
+@pytest.mark.parametrize("method", [GOERTZEL, FOLDED, RESIDUE])
 @pytest.mark.parametrize("amplitude,sigma", [(8000, 0), (8000, 2000), (300, 400), (32767, 2000)])
 def test_stress_levels(A, O, torch, amplitude, sigma, method):
     run_case(A, O, A.FSK8_FREQS, W=500, seed=amplitude + sigma, amplitude=amplitude, sigma=sigma,
              method=method)
+    if method != FOLDED:
+        run_case(A, O, FSK8_ODD, W=500, seed=amplitude + sigma + 1, amplitude=amplitude,
+                 sigma=sigma, method=method)
 
 
-@pytest.mark.parametrize("method", [GOERTZEL, FOLDED])
+@pytest.mark.parametrize("method", [GOERTZEL, FOLDED, RESIDUE])
 def test_zero_and_extreme_input(A, O, torch, method):
     n = 1024
     x = np.zeros((8, n), np.int16)
@@ -142,6 +188,37 @@ def test_zero_and_extreme_input(A, O, torch, method):
     margin = (Ps[:, -1] - Ps[:, -2]) / np.maximum(denom, 1e-30)
     posed = margin > 4 * MAG_TOL
     assert set(np.flatnonzero(~posed)) <= {0, 1, 2, 3, 5}  # 5: impulse, P = 1 at every tone
+    assert (sym[posed] == ref_sym[posed]).all()
+
+
+@pytest.mark.parametrize("method", [GOERTZEL, RESIDUE])
+def test_extreme_input_every_residue_class(A, O, torch, method):
+    """Full-scale and degenerate windows through the residue classes (FSK8_ODD
+    touches all four): magnitudes within the bar relative to the window's
+    spectral energy, symbols equal wherever the oracle's decision is not a
+    tie inside fp32 rounding."""
+    n = 1024
+    rng = np.random.default_rng(7)
+    t = np.arange(n)
+    x = np.zeros((12, n), np.int16)
+    x[1] = 32767
+    x[2, ::2] = 32767
+    x[2, 1::2] = -32768
+    x[3] = rng.integers(-32768, 32768, n)
+    x[4] = np.where(np.sin(2 * np.pi * 41 * t / n) >= 0, 32767, -32768)
+    for i, b in enumerate((50, 59, 68, 77, 86, 95)):
+        x[5 + i] = np.clip(np.round(32767 * np.cos(2 * np.pi * b * t / n + i)
+                                    + rng.normal(0, 3000, n)), -32768, 32767)
+    x[11] = rng.integers(-32768, 32768, n) // 256
+    with A.Demodulator(freqs=FSK8_ODD, method=method) as d:
+        sym, mag = d.batch(x, mags=True)
+    ref_sym, ref_P = O.goertzel(x, FSK8_ODD, n)
+    xe = x.astype(np.float64)
+    denom = np.maximum(np.maximum(ref_P.max(axis=1), n * (xe * xe).sum(axis=1) / 2), 1.0)
+    assert (np.abs(mag.astype(np.float64) - ref_P).max(axis=1) / denom).max() <= MAG_TOL
+    Ps = np.sort(ref_P, axis=1)
+    posed = (Ps[:, -1] - Ps[:, -2]) / denom > 4 * MAG_TOL
+    assert posed[[4, 5, 6, 7, 8, 9, 10]].all()
     assert (sym[posed] == ref_sym[posed]).all()
 
 
@@ -224,12 +301,12 @@ def test_streaming_buffer_too_small_consumes_nothing(A, torch):
 
 
 @pytest.mark.parametrize("freqs,method", [("FSK2_FREQS", GOERTZEL), ("FSK8_FREQS", FOLDED),
-                                          ("FSK8_FREQS", GOERTZEL)])
+                                          ("FSK8_FREQS", GOERTZEL), ("FSK8_ODD", RESIDUE)])
 def test_full_size_2e20_windows(A, O, torch, freqs, method):
     """Configs 2/3 at full size (2^20 windows, 2 GiB): every symbol equals the
     transmitted one (size-independent check), and a 4096-window sample equals
     the oracle bit-for-bit with magnitudes inside the tolerance."""
-    f = getattr(A, freqs)
+    f = FSK8_ODD if freqs == "FSK8_ODD" else getattr(A, freqs)
     n, W = 1024, 1 << 20
     cfg = A.make_cfg(n=n, freqs=f)
     d_pcm = torch.empty((W, n), dtype=torch.int16, device="cuda")
@@ -258,8 +335,10 @@ def test_golden_vectors_on_gpu(A, torch, name):
     g = np.load(os.path.join(os.path.dirname(__file__), "golden", name + ".npz"),
                 allow_pickle=False)
     n, hop = int(g["n"]), int(g["hop"])
-    for method in (0, GOERTZEL):
-        with A.Demodulator(n=n, hop=hop, freqs=tuple(g["freqs"]), method=method) as d:
+    freqs = tuple(g["freqs"])
+    integer = all(abs(f * n / 48000.0 - round(f * n / 48000.0)) < 1e-9 for f in freqs)
+    for method in (0, GOERTZEL) + ((RESIDUE,) if integer else ()):
+        with A.Demodulator(n=n, hop=hop, freqs=freqs, method=method) as d:
             sym, mag = d.batch(g["pcm"], n_windows=g["sym"].size, mags=True)
         assert (sym == g["sym"]).all()
         assert rel_err(mag, g["P"]) <= MAG_TOL
@@ -379,7 +458,7 @@ def test_fft_detector_extremes_and_streaming(A, O, torch):
 
 
 @pytest.mark.parametrize("method,hop", [(GOERTZEL, 1024), (GOERTZEL, 256), (FOLDED, 512),
-                                        (2, 256)])
+                                        (RESIDUE, 1024), (2, 256)])
 def test_host_batch_multi_chunk(A, O, torch, method, hop):
     """Host-pointer demod_batch streams its input in 65536-window chunks over
     two device slots (demod_api.cpp run_host). Across chunk boundaries (and
@@ -387,7 +466,7 @@ def test_host_batch_multi_chunk(A, O, torch, method, hop):
     device-pointer path on the same samples bit-for-bit, and a sample of
     windows must match the oracle."""
     n = 1024
-    f = A.FSK8_FREQS if method == FOLDED else A.FSK2_FREQS
+    f = A.FSK8_FREQS if method == FOLDED else FSK8_ODD if method == RESIDUE else A.FSK2_FREQS
     Wsrc = 3 * 65536 // (n // hop) + 37           # source windows of n samples
     cfg = A.make_cfg(n=n, freqs=f)
     d_src = torch.empty((Wsrc, n), dtype=torch.int16, device="cuda")
