@@ -137,7 +137,11 @@ def main():
     ap.add_argument("--hop", type=int, default=256, help="window advance for --config fft")
     ap.add_argument("--windows", type=int, default=1 << 20, help="windows per GPU (fsk2/fsk8)")
     ap.add_argument("--no-mags", action="store_true", help="symbols only")
-    ap.add_argument("--method", choices=["auto", "goertzel", "folded"], default="auto")
+    ap.add_argument("--method", choices=["auto", "goertzel", "folded", "residue"], default="auto")
+    ap.add_argument("--plan", choices=["survey", "odd"], default="survey",
+                    help="fsk8 tone plan: survey = SURVEY §8 (1500 + 375 i Hz, multiples of 8 "
+                         "bins), odd = integer bins 32 + 9 i (every residue class mod 8: the "
+                         "generic integer-bin path, DESIGN.md §4.3)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -164,10 +168,12 @@ def main():
 
     A, D = load_pkg()
     freqs = A.FSK8_FREQS if args.config == "fsk8" else A.FSK2_FREQS
+    if args.config == "fsk8" and args.plan == "odd":
+        freqs = tuple(46.875 * (32 + 9 * i) for i in range(8))
     K = len(freqs)
     n = 1024
     method = {"auto": A.METHOD_AUTO, "goertzel": A.METHOD_GOERTZEL,
-              "folded": A.METHOD_FOLDED}[args.method]
+              "folded": A.METHOD_FOLDED, "residue": A.METHOD_RESIDUE}[args.method]
     hop = n
     if args.config == "fft":
         method, hop = A.METHOD_FFT, int(args.hop)
@@ -336,7 +342,9 @@ def main():
                              f"configs[3]: sliding 1024-pt full-spectrum FFT, hop {hop}, "
                              f"{n_eval} windows over a {W * n}-sample int16 stream per GPU"
                              if args.config == "fft" else
-                             ("configs[1]: 2-FSK" if K == 2 else "configs[2]: 8-FSK")
+                             ("configs[1]: 2-FSK" if K == 2 else
+                              "configs[2]: 8-FSK" + (" (integer bins 32 + 9 i)" if args.plan == "odd"
+                                                     else ""))
                              + f" Goertzel, {W} x {n}-sample int16 windows per GPU, HBM-resident"),
                 "tones_hz": list(freqs),
                 "windows_per_gpu": n_eval,
@@ -348,6 +356,7 @@ def main():
                                 f"dp{world} (independent window shards, RCCL symbol all-gather)"),
             },
             "detector": {A.METHOD_GOERTZEL: "goertzel", A.METHOD_FOLDED: "folded",
+                         A.METHOD_RESIDUE: "residue",
                          A.METHOD_FFT: "fft1024"}.get(demod.method, str(demod.method)),
             "kernel_ms_p10_p50_p90": [round(float(np.percentile(kts, q)), 4) for q in (10, 50, 90)],
             "symbol_errors": sym_err,
@@ -359,10 +368,11 @@ def main():
                 "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                "traffic": pmc_traffic(args.config, W),
+                "traffic": pmc_traffic(args.config if args.plan == "survey" else "fsk8odd", W),
                 "alg_bytes_per_launch": alg_bytes,
                 "kernel": ("fft1024_quad_kernel<4>" if demod.method == A.METHOD_FFT else
                            ("fold_tile_kernel<%d,4>" if demod.method == A.METHOD_FOLDED
+                            else "residue_tile_kernel<%d,4>" if demod.method == A.METHOD_RESIDUE
                             else "goertzel_tile_kernel<%d,4>") % K),
             },
         }
