@@ -112,12 +112,18 @@ def cpu_baseline(A, d_pcm, d_sym, d_mag, freqs, seconds: float, threads: int, ff
            (lambda: O.goertzel(flat1, freqs, n, hop, threads=1)))
     p1, el1 = timed(fn1, max(1.0, seconds / 5))
     msps1 = p1 * S1 * n / el1 / 1e6
+    # ... and the fp32 variant of the scalar recurrence, hop = n only
+    msps1_f32 = None
+    if not fft and hop == n:
+        pf, elf = timed(lambda: O.goertzel_f32(flat1, freqs, n), max(1.0, seconds / 5))
+        msps1_f32 = round(pf * S1 * n / elf / 1e6, 3)
     parity = {"windows_checked": int(n_win), "symbol_mismatches": int((sym != gsym).sum())}
     if gmag is not None:
         parity["max_rel_mag_err"] = float((np.abs(gmag - P).max(1) / P.max(1)).max())
     what = ("double radix-2 FFT, argmax over tone bins" if fft else "double Goertzel")
     base = {"value": round(msps, 3), "unit": "Msamples/s", "cores": int(threads),
             "kind": "port", "single_thread_value": round(msps1, 3),
+            "single_thread_fp32_value": msps1_f32,
             "host_cpu": cpu_model(), "host_cpus_visible": os.cpu_count(),
             "sample": f"first {S * n} samples ({n_win} windows, hop {hop}) of the timed batch, "
                       f"{passes} passes in {el:.1f} s, oracle/fsk_oracle.c {what}, OpenMP"}

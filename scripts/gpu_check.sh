@@ -8,6 +8,8 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider > $
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $R/gpurun_out/smoke.log 2>&1 && \
 timeout -k 10 300 python -u bench.py > $R/gpurun_out/bench.log 2>&1 && \
 timeout -k 10 300 python -u bench.py --config fsk8 > $R/gpurun_out/bench_fsk8.log 2>&1 && \
+timeout -k 10 300 python -u bench.py --config fsk8 --plan odd --cpu-seconds 5 > $R/gpurun_out/bench_fsk8_odd.log 2>&1 && \
+timeout -k 10 300 python -u bench.py --config fsk8 --plan odd --method goertzel --no-cpu-baseline > $R/gpurun_out/bench_fsk8_odd_plain.log 2>&1 && \
 timeout -k 10 300 python -u bench.py --config streams --cpu-seconds 3 > $R/gpurun_out/bench_streams.log 2>&1 && \
 timeout -k 10 300 python -u bench.py --config fft --cpu-seconds 5 > $R/gpurun_out/bench_fft.log 2>&1 && \
 timeout -k 10 300 python -u bench.py --config fft --hop 1024 --cpu-seconds 5 > $R/gpurun_out/bench_fft1024.log 2>&1 && \
