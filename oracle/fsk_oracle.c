@@ -1,7 +1,8 @@
 /*
  * fsk_oracle.c — TEST INFRASTRUCTURE ONLY. See fsk_oracle.h for who may use
- * it and for its parity status ("parity unpinned" vs the reference, which has
- * no demodulator; pinned to independent known answers instead).
+ * it and for its parity status (spectra pinned to the reference's own FFT and
+ * to independent known answers; the decision itself has no reference
+ * counterpart, since the reference has no demodulator).
  *
  * Plain scalar C, double precision, written for clarity, not speed.
  */

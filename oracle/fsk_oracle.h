@@ -6,9 +6,11 @@
  * Scalar CPU restatement of the north-star path.
  *
  * PARITY STATUS: the reference (tmarsteel/audio-network) contains no
- * Goertzel / FSK / FFT demodulator at all, so this
- * restatement is "parity unpinned" with respect to the reference. It is
- * pinned instead against independent known answers (tests/test_oracle.py):
+ * Goertzel / FSK demodulator at all, so the decision has
+ * no reference counterpart. The spectral values are pinned to the
+ * reference's own FFT, opus_fft_c (libopus celt/kiss_fft.c:569-589, built in
+ * place by oracle/ref.mk; golden tests/golden/ref_kissfft.npz), to its Q15
+ * precision, and to independent known answers (tests/test_oracle.py):
  * numpy.fft bins, a direct double DFT at non-integer frequencies, closed-form
  * pure-tone magnitudes, and the committed golden vectors in tests/golden/.
  */

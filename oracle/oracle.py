@@ -4,10 +4,15 @@ Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
 import this module, and only as the checker / CPU baseline; nothing on the
 product path (audio-network_amd/) uses it.
 
-Parity status: the Goertzel / FFT restatement in fsk_oracle.c is "parity
-unpinned" against the reference, which contains no demodulator (SURVEY.md §0,
-§8c); it is pinned to independent known answers in tests/test_oracle.py.
-Frame bytes are pinned to the reference's own nanopb (oracle/_ref).
+Parity status: the reference contains no demodulator, so
+the Goertzel restatement in fsk_oracle.c has no reference counterpart to be
+compared with directly. Its spectral values are pinned to the reference's own
+FFT code instead: opus_fft_c (libopus celt/kiss_fft.c:569-589, fixed point, the
+four static sizes 480/240/120/60) agrees with oracle Goertzel powers at every
+bin to the reference's Q15 precision (tests/test_oracle.py, golden fixture
+tests/golden/ref_kissfft.npz); and to independent known answers (numpy.fft,
+direct DFT, closed forms) at 1e-9. Frame bytes are pinned to the reference's
+own nanopb (oracle/_ref).
 """
 from __future__ import annotations
 
@@ -21,6 +26,8 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "liboracle.so")
 REF_NANOPB = os.path.join(HERE, "_ref", "libnanopb_ref.so")
+REF_KISSFFT = os.path.join(HERE, "_ref", "libkissfft_ref.so")
+KISSFFT_PRESHIFT = 14  # int16 samples << 14: the Q31 range opus_fft_c is built for
 
 _lib = None
 _P = ctypes.c_void_p
@@ -67,7 +74,12 @@ def lib() -> ctypes.CDLL:
     return _lib
 
 
+MAX_TONES = 64  # fixed coefficient arrays in fsk_oracle.c
+
+
 def _freqs(freqs: Sequence[float]):
+    if len(freqs) > MAX_TONES:
+        raise ValueError(f"oracle takes at most {MAX_TONES} tones per call, got {len(freqs)}")
     arr = (ctypes.c_double * len(freqs))(*[float(f) for f in freqs])
     return arr
 
@@ -220,3 +232,36 @@ def ref_decode(buf: bytes):
     used = _SZ()
     rc = R.ref_decode_to_receiver(src, len(buf), out, 8192, ctypes.byref(pl), ctypes.byref(used))
     return rc, bytes(out[:pl.value]), int(used.value)
+
+
+# ---- reference FFT (libopus opus_fft_c, oracle/_ref, built by ref.mk) --------
+_ref_kf = None
+
+
+def ref_kissfft() -> Optional[ctypes.CDLL]:
+    """The reference's own fixed-point opus_fft_c (static states), or None."""
+    global _ref_kf
+    if _ref_kf is None and os.path.exists(REF_KISSFFT):
+        R = ctypes.CDLL(REF_KISSFFT)
+        R.ref_fft_static_size.argtypes = [ctypes.c_int]
+        R.ref_fft_static_size.restype = ctypes.c_int
+        R.ref_fft_static32.argtypes = [ctypes.c_int, _P, ctypes.c_int, _P, _P]
+        R.ref_fft_static32.restype = ctypes.c_int
+        _ref_kf = R
+    return _ref_kf
+
+
+def ref_fft_static(which: int, x: np.ndarray):
+    """opus_fft_c of int16 frame x with static state kfft[which]; returns the
+    reference's raw complex output (X / nfft, scaled by 2^KISSFFT_PRESHIFT)."""
+    R = ref_kissfft()
+    n = R.ref_fft_static_size(which)
+    x32 = (np.ascontiguousarray(x, np.int16).astype(np.int32) << KISSFFT_PRESHIFT)
+    if x32.size != n:
+        raise ValueError(f"kfft[{which}] is {n}-point, got {x32.size} samples")
+    re = np.empty(n)
+    im = np.empty(n)
+    rc = R.ref_fft_static32(which, x32.ctypes.data, n, re.ctypes.data, im.ctypes.data)
+    if rc != n:
+        raise ValueError(f"ref_fft_static32: {rc}")
+    return re + 1j * im

@@ -5,9 +5,10 @@
 
 Demodulation vectors: inputs from the seeded generator, expected symbols and
 P_k from the double-precision oracle (oracle/fsk_oracle.c) — which is itself
-pinned to numpy.fft / direct-DFT known answers (tests/test_oracle.py); the
-reference has no demodulator, so these are NOT reference outputs ("parity
-unpinned" vs the reference).
+pinned to the reference's own FFT (opus_fft_c, tests/golden/ref_kissfft.npz)
+and to numpy.fft / direct-DFT known answers (tests/test_oracle.py); the
+reference has no demodulator, so these are oracle outputs, not reference
+outputs.
 
 Frame vectors: ToReceiver frames encoded and decode verdicts given by the
 reference's OWN nanopb 0.4.5 + generated ip.pb.c, compiled in place from

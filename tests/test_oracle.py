@@ -1,10 +1,14 @@
 """Pinning the oracle before trusting it (CPU only).
 
 The reference has no demodulator, so the Goertzel
-restatement cannot be checked against reference outputs ("parity unpinned").
-It is pinned here against independent known answers instead: numpy.fft at
-integer bins, a direct double DFT at arbitrary frequencies, closed-form pure
-tone magnitudes, and Parseval; plus the committed golden vectors.
+restatement has no reference counterpart to be compared with directly. Its
+spectral values are pinned to the reference's OWN FFT code (opus_fft_c,
+libopus celt/kiss_fft.c:569-589, fixed point, static sizes 480/240/120/60;
+golden fixture tests/golden/ref_kissfft.npz, regenerated and checked live
+when oracle/_ref is built) to the reference's Q15 precision, and to
+independent known answers (numpy.fft at integer bins, a direct double DFT at
+arbitrary frequencies, closed-form pure tone magnitudes, Parseval) at 1e-9;
+plus the committed golden vectors.
 """
 import os
 
@@ -160,3 +164,58 @@ def test_fft_demod_omp_equals_serial(O):
     a = O.fft_demod(pcm, (1500.0, 3000.0), 1024, 256)
     b = O.fft_demod(pcm, (1500.0, 3000.0), 1024, 256, threads=4)
     assert (a[0] == b[0]).all() and np.array_equal(a[1], b[1])
+
+
+# ---- the reference's own FFT (opus_fft_c) ------------------------------------
+# Tolerance: opus_fft_c is fixed point (Q15 twiddles, 1/N scale in Q15,
+# kiss_fft.c:578-584); its |X|^2 errors scale with the frame's energy, so the
+# bar is relative to the Parseval total N * sum(x^2) (measured <= 1.7e-4, at
+# DC; <= 3.5e-5 elsewhere).
+REF_FFT_TOL = 3e-4
+
+
+def _ref_kissfft_golden():
+    return np.load(os.path.join(HERE, "golden", "ref_kissfft.npz"), allow_pickle=False)
+
+
+def _ref_powers(g, n):
+    Y = (g[f"re{n}"] + 1j * g[f"im{n}"]) * n / 2.0 ** int(g["preshift"])
+    return np.abs(Y[:, : n // 2 + 1]) ** 2
+
+
+@pytest.mark.parametrize("n", [480, 240, 120, 60])
+def test_oracle_goertzel_pinned_to_reference_fft(O, n):
+    """Oracle Goertzel powers at every bin of the n-point frame equal the
+    reference opus_fft_c's |X|^2 (golden outputs) to the reference's Q15
+    precision; at n = 480, where the 2-FSK tones are bins 15 and 30, the
+    oracle's symbol is the argmax of the reference spectrum at those bins."""
+    g = _ref_kissfft_golden()
+    x = g[f"x{n}"]
+    Pr = _ref_powers(g, n)
+    freqs = [k * FS / n for k in range(n // 2 + 1)]
+    for i, row in enumerate(x):
+        P = np.concatenate([O.goertzel(row, freqs[c:c + 16], n)[1][0]
+                            for c in range(0, len(freqs), 16)])
+        energy = n * float((row.astype(np.float64) ** 2).sum())
+        assert np.abs(P - Pr[i]).max() <= REF_FFT_TOL * max(energy, 1.0), (n, i)
+    if n == 480:
+        sym, _ = O.goertzel(x[:4], (1500.0, 3000.0), n)
+        assert (sym == np.argmax(Pr[:4][:, [15, 30]], axis=1)).all()
+
+
+def test_reference_fft_golden_is_live_reference_output(O):
+    """The committed golden outputs are what the reference's opus_fft_c
+    (oracle/_ref/libkissfft_ref.so, built from /root/reference) computes."""
+    if O.ref_kissfft() is None:
+        pytest.skip("oracle/_ref/libkissfft_ref.so not built (needs /root/reference)")
+    g = _ref_kissfft_golden()
+    assert int(g["preshift"]) == O.KISSFFT_PRESHIFT
+    for which in range(4):
+        n = O.ref_kissfft().ref_fft_static_size(which)
+        y = np.stack([O.ref_fft_static(which, row) for row in g[f"x{n}"]])
+        assert np.array_equal(y.real, g[f"re{n}"]) and np.array_equal(y.imag, g[f"im{n}"])
+
+
+def test_oracle_rejects_too_many_tones(O):
+    with pytest.raises(ValueError):
+        O.goertzel(np.zeros(64, np.int16), [100.0] * 65, 64)
