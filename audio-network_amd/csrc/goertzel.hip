@@ -23,6 +23,7 @@
 // 64-sample chains keep the fp32 error <= ~3e-6 of max_k P (a single
 // 1024-sample chain reaches ~2e-5, over the 1e-5 bar).
 #include "demod_internal.h"
+#include "window_sum.h"
 
 namespace fskd {
 
@@ -61,8 +62,11 @@ __device__ __forceinline__ float group_sum(float v, int log2g)
 //   SB      sched_barrier after every sample's K-tone step, so the K independent
 //           recurrences stay interleaved (hipcc otherwise serialises one tone's
 //           whole chain after another: issue-stall bound at large K).
+//   WS      window_sum.h epilogue (reduce-scatter, packed-key argmax, one
+//           coalesced magnitude store) at n = 1024.
 template <int K, int LOG2G, int PF = 1, bool NT = true, int WPB = kWavesPerBlock,
-          bool DIRECT = false, bool NTS = false, bool PK = false, bool SB = false>
+          bool DIRECT = false, bool NTS = false, bool PK = false, bool SB = false,
+          bool WS = false>
 __global__ __launch_bounds__(64 * WPB) void goertzel_tile_kernel(GoertzelParams p)
 {
     static_assert(PF == 1 || PF == 2, "prefetch depth");
@@ -210,6 +214,17 @@ __global__ __launch_bounds__(64 * WPB) void goertzel_tile_kernel(GoertzelParams 
         }
         }
 
+        const long long w = tt * wins_per_tile + win_in_tile;
+        if constexpr (WS && LOG2G == 4) {
+            float xr[K], xi[K];
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                xr[k] = r[k].x * s1[k] - r[k].z * s2[k];
+                xi[k] = r[k].y * s1[k] - r[k].w * s2[k];
+            }
+            window_sum_decide<K>(xr, xi, lane, w, w < p.n_windows, p.sym, p.mag);
+            return;
+        }
         float best = -1.f;
         int arg = 0;
         float P[K];
@@ -223,7 +238,6 @@ __global__ __launch_bounds__(64 * WPB) void goertzel_tile_kernel(GoertzelParams 
             if (P[k] > best) { best = P[k]; arg = k; }
         }
 
-        const long long w = tt * wins_per_tile + win_in_tile;
         if (w < p.n_windows) {
             if (seg == 0) out_store<NTS>(p.sym + w, (uint8_t)arg);
             if (p.mag) {
@@ -251,14 +265,16 @@ __global__ __launch_bounds__(64 * WPB) void goertzel_tile_kernel(GoertzelParams 
 }
 
 // Shipped configuration: packed tone pairs for K >= 3 (K = 4: 407 -> 336 us,
-// K = 8: 657 -> 506 us on 2^20 windows; K = 2 is HBM-bound either way).
+// K = 8: 657 -> 506 us on 2^20 windows; K = 2 is HBM-bound either way) and the
+// window_sum.h epilogue for K >= 3 (K = 8: 484 -> 456 us; neutral at K <= 4,
+// profiles/round1/probe_window_sum.log).
 template <int K>
 static const void *kernel_for(int log2g)
 {
     constexpr bool PK = K >= 3;
     if (log2g == 4)
         return reinterpret_cast<const void *>(
-            &goertzel_tile_kernel<K, 4, 1, true, kWavesPerBlock, false, false, PK>);
+            &goertzel_tile_kernel<K, 4, 1, true, kWavesPerBlock, false, false, PK, false, K >= 3>);
     return reinterpret_cast<const void *>(
         &goertzel_tile_kernel<K, -1, 1, true, kWavesPerBlock, false, false, PK>);
 }

@@ -36,6 +36,7 @@
 // folds them. VALU per sample ~ 2.3 for the butterflies + K/4 for the
 // recurrences (vs ~ 1 + K for the plain bank), so K = 8 stays HBM-bound.
 #include "demod_internal.h"
+#include "window_sum.h"
 
 namespace fskd {
 
@@ -120,9 +121,10 @@ constexpr int kResidueQP = 2;  // shipped: two sample pairs per LDS round
 //   MINW  > 0: ask for MINW waves per SIMD (VGPR budget 512 / MINW),
 //   QP    sample pairs per LDS round (1, 2 or 4): 4 QP KiB of LDS per wave,
 //   PF    prefetch the wave's next tile before computing the current one
-//         (only matters on grids with more than one tile per wave).
+//         (only matters on grids with more than one tile per wave),
+//   WS    window_sum.h epilogue (reduce-scatter, packed-key argmax) at n = 1024.
 template <int K, int LOG2G, int WPB = kWavesPerBlock, bool ASM = true, bool ROTV = false,
-          int MINW = (K <= 8 ? 4 : 0), int QP = kResidueQP, bool PF = false>
+          int MINW = (K <= 8 ? 4 : 0), int QP = kResidueQP, bool PF = false, bool WS = true>
 __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MINW > 0 ? MINW : 1)))
 void residue_tile_kernel(GoertzelParams p)
 {
@@ -239,9 +241,7 @@ void residue_tile_kernel(GoertzelParams p)
             }
         }
 
-        float best = -1.f;
-        int arg = 0;
-        float P[K];
+        float xr[K], xi[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const f4 c12 = ROTV ? rv[2 * k] : rot[(k * g + j) * 2];
@@ -250,13 +250,24 @@ void residue_tile_kernel(GoertzelParams p)
             X = __builtin_elementwise_fma(f2{c12.z, c12.w}, f2{s1[k].y, s1[k].y}, X);
             X = __builtin_elementwise_fma(f2{c34.x, c34.y}, f2{s2[k].x, s2[k].x}, X);
             X = __builtin_elementwise_fma(f2{c34.z, c34.w}, f2{s2[k].y, s2[k].y}, X);
-            const float re = group_sum_r(X.x, log2g);
-            const float im = group_sum_r(X.y, log2g);
+            xr[k] = X.x;
+            xi[k] = X.y;
+        }
+        const long long w = wbase + win_in_tile;
+        if constexpr (WS && LOG2G == 4) {
+            window_sum_decide<K>(xr, xi, lane, w, w < p.n_windows, p.sym, p.mag);
+            continue;
+        }
+        float best = -1.f;
+        int arg = 0;
+        float P[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const float re = group_sum_r(xr[k], log2g);
+            const float im = group_sum_r(xi[k], log2g);
             P[k] = fmaf(re, re, im * im);
             if (P[k] > best) { best = P[k]; arg = k; }
         }
-
-        const long long w = wbase + win_in_tile;
         if (w < p.n_windows) {
             if (j == 0) p.sym[w] = (uint8_t)arg;
             if (p.mag) {

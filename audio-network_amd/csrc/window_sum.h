@@ -1,0 +1,138 @@
+// window_sum.h — epilogue shared by the tone-bank kernels for 16-lane
+// windows (n = 1024): sum every lane's partial X_k = (re, im) over the
+// window's 16 lanes, |X_k|^2, the argmax decision and the stores.
+//
+// The all-reduce it replaces adds all 2K partials at each of the 4 DPP
+// stages (8K adds) and leaves every lane with every X_k, then decides
+// tone by tone and stores one magnitude per instruction. Here the 2K values
+// are reduce-SCATTERED instead: at each stage a lane keeps the half of its
+// list selected by its lane bit, adds its partner's copy of that half (the
+// partner sends the other half), and the list halves. For 2K = 16 that is
+// 8 + 4 + 2 + 1 pairs x (2 selects + 1 DPP add) = 45 instructions instead of
+// 64, and lane l ends with the window total of value l (re_k in lane 2k, im_k
+// in lane 2k + 1): |X_k|^2 is one square plus one DPP add for all tones, the
+// magnitudes go out as one coalesced store, and the argmax is 4 DPP max
+// steps on a packed (power, tone) key.
+//
+// Decision key: the power's IEEE bits (non-negative, so unsigned order is
+// numeric order) with the low 4 mantissa bits replaced by 15 - k, so the
+// unsigned max picks the largest power and, among powers equal in their top
+// 28 bits, the lowest tone (the oracle's tie rule). Two powers within 2^-19
+// relative of each other (2e-6, below the fp32 error of the powers
+// themselves) are treated as a tie.
+#pragma once
+#include "demod_internal.h"
+
+namespace fskd {
+
+template <int CTRL>
+__device__ __forceinline__ float ws_dpp(float v)
+{
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+template <int CTRL>
+__device__ __forceinline__ unsigned ws_dpp_u(unsigned v)
+{
+    return (unsigned)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, true);
+}
+
+// DPP partner of lane bit B inside a 16-lane row: bit 3 row_mirror (i <-> 15 - i),
+// bit 2 row_half_mirror (i <-> 7 - i within 8), bit 1 quad_perm [2,3,0,1],
+// bit 0 quad_perm [1,0,3,2]. Each pairs lanes that differ in bit B (and in the
+// lower bits for the mirrors, which the halving never looks at).
+template <int B> struct WsCtrl;
+template <> struct WsCtrl<3> { static constexpr int v = 0x140; };
+template <> struct WsCtrl<2> { static constexpr int v = 0x141; };
+template <> struct WsCtrl<1> { static constexpr int v = 0x4E; };
+template <> struct WsCtrl<0> { static constexpr int v = 0xB1; };
+
+// Per-lane select on lane bit B: (lane bit B set) ? b : a, as one v_cndmask
+// on a constant lane mask. Written as asm: as C selects, hipcc folds
+// `hi ? v[f] : v[e]` into a lane-dependent index into v and lowers that to
+// compare-and-select chains over the whole list (3800 VALU per tile at K = 8).
+template <int B>
+__device__ __forceinline__ float ws_sel(float a, float b)
+{
+    constexpr unsigned long long m = B == 0 ? 0xAAAAAAAAAAAAAAAAull
+                                   : B == 1 ? 0xCCCCCCCCCCCCCCCCull
+                                   : B == 2 ? 0xF0F0F0F0F0F0F0F0ull
+                                            : 0xFF00FF00FF00FF00ull;
+    float r;
+    asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(m));
+    return r;
+}
+
+// One stage on lane bit B over a list of V values (value index bit B is
+// split if B < log2(min(V, 16)), else the stage all-reduces).
+template <int B, int V>
+__device__ __forceinline__ void ws_stage(float (&v)[V], int lane)
+{
+    constexpr int C = WsCtrl<B>::v;
+    constexpr int VS = V > 16 ? 16 : V;  // values a 16-lane group can scatter
+    if constexpr ((1 << B) >= VS) {
+#pragma unroll
+        for (int e = 0; e < V; ++e) v[e] += ws_dpp<C>(v[e]);
+    } else {
+#pragma unroll
+        for (int e = 0; e < V; ++e) {
+            if (e & (1 << B)) continue;
+            const int f = e | (1 << B);
+            const float keep = ws_sel<B>(v[e], v[f]);
+            const float send = ws_sel<B>(v[f], v[e]);
+            v[e] = keep + ws_dpp<C>(send);
+        }
+    }
+}
+
+// X[k] = this lane's partial (re, im) of tone k. Writes the symbol of window
+// w (lane j == 0) and, if mag, its K magnitudes; `live` = w is a real window.
+template <int K>
+__device__ __forceinline__ void window_sum_decide(const float (&re)[K], const float (&im)[K],
+                                                  int lane, long long w, bool live,
+                                                  uint8_t *sym, float *mag)
+{
+    static_assert(K >= 1 && K <= 16, "tones");
+    constexpr int KP = K <= 1 ? 1 : K <= 2 ? 2 : K <= 4 ? 4 : K <= 8 ? 8 : 16;
+    constexpr int V = 2 * KP;
+    float v[V];
+#pragma unroll
+    for (int k = 0; k < KP; ++k) {
+        v[2 * k] = k < K ? re[k] : 0.f;
+        v[2 * k + 1] = k < K ? im[k] : 0.f;
+    }
+    ws_stage<3>(v, lane);
+    ws_stage<2>(v, lane);
+    ws_stage<1>(v, lane);
+    ws_stage<0>(v, lane);
+    // lane j holds value (j mod VS) in v[0] (and value 16 + j in v[16] if V = 32)
+    constexpr int VS = V > 16 ? 16 : V;
+    const int j = lane & 15;
+    const int idx = j & (VS - 1);
+    const bool re_lane = (idx & 1) == 0 && j < VS;
+    const int t0 = idx >> 1;
+    float sq = v[0] * v[0];
+    const float P0 = sq + ws_dpp<0xB1>(sq);  // re^2 + im^2 in the re lane
+    float P1 = 0.f;
+    if constexpr (V > 16) {
+        sq = v[16] * v[16];
+        P1 = sq + ws_dpp<0xB1>(sq);
+    }
+    const bool ok0 = re_lane && t0 < K;
+    const bool ok1 = V > 16 && re_lane && t0 + 8 < K;
+    if (live && mag) {
+        if (ok0) mag[w * K + t0] = P0;
+        if (ok1) mag[w * K + t0 + 8] = P1;
+    }
+    unsigned key = ok0 ? ((__float_as_uint(P0) & ~15u) | (unsigned)(15 - t0)) : 0u;
+    if constexpr (V > 16) {
+        const unsigned k1 = ok1 ? ((__float_as_uint(P1) & ~15u) | (unsigned)(15 - (t0 + 8))) : 0u;
+        key = key > k1 ? key : k1;
+    }
+    key = max(key, ws_dpp_u<0xB1>(key));
+    key = max(key, ws_dpp_u<0x4E>(key));
+    key = max(key, ws_dpp_u<0x141>(key));
+    key = max(key, ws_dpp_u<0x140>(key));
+    if (live && j == 0) sym[w] = (uint8_t)(15 - (key & 15u));
+}
+
+}  // namespace fskd

@@ -123,6 +123,8 @@ static void add_variant(std::vector<Variant> &vs, const void *f, int wpb, const 
 #define GZPB(K) reinterpret_cast<const void *>(&goertzel_tile_kernel<K, 4, 1, true, 4, false, false, true, true>)
 #define GZP2(K) reinterpret_cast<const void *>(&goertzel_tile_kernel<K, 4, 2, true, 4, false, false, true>)
 #define GZB(K) reinterpret_cast<const void *>(&goertzel_tile_kernel<K, 4, 1, true, 4, false, false, false, true>)
+#define GZW(K) reinterpret_cast<const void *>(&goertzel_tile_kernel<K, 4, 1, true, 4, false, false, (K >= 3), false, true>)
+#define FDW(K) reinterpret_cast<const void *>(&fold_tile_kernel<K, 4, true, 4, false, false, true>)
 
 int main(int argc, char **argv)
 {
@@ -227,6 +229,11 @@ int main(int argc, char **argv)
     add_variant(vs, GZP2(8), 4, "goertzel PK PF2", p8, 8, cus, 4);
     add_variant(vs, FD(2, 4), 4, "fold", f2, 2, cus, 1);
     add_variant(vs, FD(8, 4), 4, "fold", f8, 8, cus, 1);
+    add_variant(vs, GZW(2), 4, "goertzel WS", p2, 2, cus, 1);
+    add_variant(vs, GZW(4), 4, "goertzel PK WS", p8, 4, cus, 1);
+    add_variant(vs, GZW(8), 4, "goertzel PK WS", p8, 8, cus, 1);
+    add_variant(vs, FDW(2), 4, "fold WS", f2, 2, cus, 1);
+    add_variant(vs, FDW(8), 4, "fold WS", f8, 8, cus, 1);
     {
         // residue-class folding (residue.hip): rotation table as demod_api.cpp
         auto make_res = [&](int K, const double *bins, GoertzelParams &p) {
@@ -258,6 +265,7 @@ int main(int argc, char **argv)
 #define RZV(K) reinterpret_cast<const void *>(&residue_tile_kernel<K, 4, 4, true, true>)
 #define RZW(K, W) reinterpret_cast<const void *>(&residue_tile_kernel<K, 4, 4, true, false, W>)
 #define RZQ(K, W, Q, PF) reinterpret_cast<const void *>(&residue_tile_kernel<K, 4, 4, true, false, W, Q, PF>)
+#define RZA(K) reinterpret_cast<const void *>(&residue_tile_kernel<K, 4, 4, true, false, (K <= 8 ? 4 : 0), 2, false, false>)
         static double bo[16];
         for (int i = 0; i < 16; ++i) bo[i] = 32 + 9 * i;  // every class mod 8
         static GoertzelParams r8s = p8, r3 = p8, r4 = p8, r8 = p8, r16 = p8, g3 = p8, g4 = p8, g8 = p8;
@@ -281,6 +289,8 @@ int main(int argc, char **argv)
         add_variant(vs, RZ(4), 4, "residue", r4, 4, cus, 1, residue_lds_bytes(4, 4), "o");
         add_variant(vs, GZP(8), 4, "goertzel PK", g8, 8, cus, 1, 0, "o");
         add_variant(vs, RZ(8), 4, "residue", r8, 8, cus, 1, residue_lds_bytes(8, 4), "o");
+        add_variant(vs, RZA(8), 4, "residue allreduce-epilogue", r8, 8, cus, 1, residue_lds_bytes(8, 4), "o");
+        add_variant(vs, RZA(16), 4, "residue allreduce-epilogue", r16, 16, cus, 1, residue_lds_bytes(16, 4), "o");
         add_variant(vs, RZC(8), 4, "residue C-butterfly", r8, 8, cus, 1, residue_lds_bytes(8, 4), "o");
         add_variant(vs, RZV(8), 4, "residue VGPR-rot", r8, 8, cus, 1, residue_lds_bytes(8, 4), "o");
         add_variant(vs, RZW(8, 4), 4, "residue MINW4", r8, 8, cus, 1, residue_lds_bytes(8, 4), "o");
@@ -314,6 +324,7 @@ int main(int argc, char **argv)
 #undef RZV
 #undef RZW
 #undef RZQ
+#undef RZA
     }
     {
         // FFT detector tables (2-FSK bins 32, 64)
