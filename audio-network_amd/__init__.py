@@ -122,6 +122,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "demod_synth_fsk": (ctypes.c_int, [ctypes.POINTER(DemodCfg), ctypes.c_uint64,
                                            ctypes.c_uint64, _SZ, ctypes.c_int, ctypes.c_int,
                                            _P, _P, _P]),
+        "demod_read_ceiling_async": (ctypes.c_int, [_P, _SZ, _P]),
         "demod_strerror": (ctypes.c_char_p, [ctypes.c_int]),
         "demod_version_string": (ctypes.c_char_p, []),
     }
@@ -315,6 +316,13 @@ def synth_fsk(cfg: DemodCfg, seed: int, n_windows: int, amplitude: int, sigma: i
                                          stream or None)
     if rc < 0:
         raise DemodError(rc, "demod_synth_fsk")
+
+
+def read_ceiling_async(d_buf, n_bytes: int, stream: int = 0) -> None:
+    """Read-only reference stream over a device buffer (demod_read_ceiling_async)."""
+    rc = load_library().demod_read_ceiling_async(_ptr(d_buf), n_bytes, stream or None)
+    if rc < 0:
+        raise DemodError(rc, "demod_read_ceiling_async")
 
 
 # ---- ip.proto framing (host) ---------------------------------------------

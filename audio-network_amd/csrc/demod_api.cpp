@@ -657,6 +657,20 @@ const char *demod_strerror(int error)
     }
 }
 
+int demod_read_ceiling_async(const void *d_buf, size_t n_bytes, void *stream)
+{
+    if (!d_buf || ((uintptr_t)d_buf & 15) || (n_bytes % 8192)) return DEMOD_BAD_ARG;
+    if (n_bytes == 0) return DEMOD_OK;
+    static unsigned *d_sink[64] = {nullptr};
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    if (dev < 0 || dev >= 64) return DEMOD_BAD_ARG;
+    if (!d_sink[dev]) HIP_TRY(hipMalloc(&d_sink[dev], 64));
+    HIP_TRY(launch_read_ceiling((const int16_t *)d_buf, (long long)n_bytes, d_sink[dev],
+                                (hipStream_t)stream));
+    return DEMOD_OK;
+}
+
 const char *demod_version_string(void) { return "fskdemod 0.1.0 (gfx950 HIP)"; }
 
 }  // extern "C"

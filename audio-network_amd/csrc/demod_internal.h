@@ -8,7 +8,12 @@ namespace fskd {
 
 constexpr int kSeg = 64;              // samples per lane segment
 constexpr int kTileSamples = 64 * kSeg;  // samples one wave owns per tile (8 KiB)
-constexpr int kWavesPerBlock = 4;
+constexpr int kWavesPerBlock = 4;  // residue kernel: 4-wave blocks share the rotation table
+// Plain and fold kernels: 2-wave blocks. Same 16 waves per CU as 4-wave blocks
+// (LDS-limited for the plain bank), but a block's LDS and slots free up as
+// soon as its 2 waves finish: K = 2 330.7 -> 322.8 us, plain K = 8 461.7 ->
+// 450.0 us, fold K = 8 350.6 -> 346.5 us (profiles/round1/probe_wpb.log).
+constexpr int kPlainWPB = 2;
 constexpr int kLdsSegStride = 144;    // bytes: 128 B segment + 16 B pad (conflict-free b128 reads)
 constexpr int kLdsWaveBytes = 64 * kLdsSegStride;
 constexpr int kMaxTones = 16;
@@ -90,8 +95,9 @@ hipError_t launch_detector(int detector, const GoertzelParams &p, hipStream_t s)
 // residue.hip: rotation table is [k][g][2] float4 {C1, C2}, {C3, C4}
 const void *residue_kernel_ptr(int k, int log2g);
 size_t residue_lds_bytes(int k, int log2g, int qp = 2);
-int tile_grid(long long n_windows, int log2g);
+int tile_grid(long long n_windows, int log2g, int wpb = kWavesPerBlock);
 hipError_t launch_synth(const SynthParams &p, hipStream_t s);
+hipError_t launch_read_ceiling(const int16_t *p, long long n_bytes, unsigned *sink, hipStream_t s);
 hipError_t launch_fft(const FftParams &p, hipStream_t s);       // 64 lanes / window (fft.hip)
 hipError_t launch_fft_quad(const FftParams &p, hipStream_t s);  // 16 lanes / window (fft_quad.hip)
 // ip.proto framing of [n_streams][n] symbols, one frame run per stream (frame_gpu.hip)

@@ -157,8 +157,9 @@ template <int K>
 static const void *fold_kernel_for(int log2g)
 {
     // window_sum.h epilogue at n = 1024 (K = 8: 352 -> 347 us, K = 2: 335 -> 329 us)
-    if (log2g == 4) return reinterpret_cast<const void *>(&fold_tile_kernel<K, 4, true, 4, false, false, true>);
-    return reinterpret_cast<const void *>(&fold_tile_kernel<K, -1>);
+    if (log2g == 4)
+        return reinterpret_cast<const void *>(&fold_tile_kernel<K, 4, true, kPlainWPB, false, false, true>);
+    return reinterpret_cast<const void *>(&fold_tile_kernel<K, -1, true, kPlainWPB>);
 }
 
 const void *fold_kernel_ptr(int k, int log2g)

@@ -274,9 +274,9 @@ static const void *kernel_for(int log2g)
     constexpr bool PK = K >= 3;
     if (log2g == 4)
         return reinterpret_cast<const void *>(
-            &goertzel_tile_kernel<K, 4, 1, true, kWavesPerBlock, false, false, PK, false, K >= 3>);
+            &goertzel_tile_kernel<K, 4, 1, true, kPlainWPB, false, false, PK, false, K >= 3>);
     return reinterpret_cast<const void *>(
-        &goertzel_tile_kernel<K, -1, 1, true, kWavesPerBlock, false, false, PK>);
+        &goertzel_tile_kernel<K, -1, 1, true, kPlainWPB, false, false, PK>);
 }
 
 static const void *kernel_ptr(int k, int log2g)
@@ -295,11 +295,11 @@ static const void *kernel_ptr(int k, int log2g)
 // One tile per wave (grid = tiles / waves-per-block): measured 317 us vs
 // 363 us for a persistent grid-stride grid on 2^20 windows (profiles/,
 // DESIGN.md §Tuning) — the dispatcher keeps every CU fed to the last tile.
-int tile_grid(long long n_windows, int log2g)
+int tile_grid(long long n_windows, int log2g, int wpb)
 {
     const long long wins_per_tile = 64 >> log2g;
     const long long n_tiles = (n_windows + wins_per_tile - 1) / wins_per_tile;
-    long long blocks = (n_tiles + kWavesPerBlock - 1) / kWavesPerBlock;
+    long long blocks = (n_tiles + wpb - 1) / wpb;
     if (blocks > 0x7FFFFFFFLL) blocks = 0x7FFFFFFFLL;  // kernels grid-stride beyond
     if (blocks < 1) blocks = 1;
     return (int)blocks;
@@ -314,9 +314,10 @@ hipError_t launch_detector(int detector, const GoertzelParams &p, hipStream_t s)
                                             : kernel_ptr(p.k, p.log2g);
     if (!f) return hipErrorInvalidValue;
     const size_t lds = detector == kDetResidue ? residue_lds_bytes(p.k, p.log2g) : 0;
+    const int wpb = detector == kDetResidue ? kWavesPerBlock : kPlainWPB;
     void *args[] = {const_cast<GoertzelParams *>(&p)};
-    return hipLaunchKernel(f, dim3(tile_grid(p.n_windows, p.log2g)), dim3(64 * kWavesPerBlock),
-                           args, lds, s);
+    return hipLaunchKernel(f, dim3(tile_grid(p.n_windows, p.log2g, wpb)), dim3(64 * wpb), args,
+                           lds, s);
 }
 
 }  // namespace fskd

@@ -290,6 +290,24 @@ def main():
     kernel_ms = float(kts.mean())
     ms_per_step = elapsed / args.steps * 1e3
 
+    # Practical read ceiling of this box for the same access pattern: the
+    # read-only reference stream (8 KiB per wave, 16 B/lane nt loads, no
+    # compute; demod_read_ceiling_async) over the same input buffer, after the
+    # timed region, median of 20 launches (HIP events on the launch stream).
+    ceil_gbps = None
+    if args.config != "fft":
+        nb = (d_pcm.numel() * 2) // 8192 * 8192
+        cev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(20)]
+        for _ in range(8):
+            A.read_ceiling_async(d_pcm, nb, stream=comp.cuda_stream)
+        for a, b in cev:
+            a.record(comp)
+            A.read_ceiling_async(d_pcm, nb, stream=comp.cuda_stream)
+            b.record(comp)
+        torch.cuda.synchronize()
+        ceil_gbps = nb / (float(np.median([a.elapsed_time(b) for a, b in cev])) / 1e3) / 1e9
+
     # correctness of the timed output: every symbol vs the transmitted one
     # (sliding windows straddle two symbols: compare the aligned ones only)
     d_sym = slots[(st["i"] - 1) % len(slots)]
@@ -376,6 +394,10 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBPS, 4),
                 "traffic": pmc_traffic(args.config if args.plan == "survey" else "fsk8odd", W),
                 "alg_bytes_per_launch": alg_bytes,
+                # this box's read-only ceiling for the same access pattern
+                # (see above) and the kernel's achieved rate as a fraction of it
+                "read_ceiling": round(ceil_gbps, 1) if ceil_gbps else None,
+                "frac_of_read_ceiling": round(achieved / ceil_gbps, 4) if ceil_gbps else None,
                 "kernel": ("fft1024_quad_kernel<4>" if demod.method == A.METHOD_FFT else
                            ("fold_tile_kernel<%d,4>" if demod.method == A.METHOD_FOLDED
                             else "residue_tile_kernel<%d,4>" if demod.method == A.METHOD_RESIDUE

@@ -212,6 +212,13 @@ int demod_synth_fsk(const demod_cfg_t *cfg, uint64_t seed, uint64_t w0,
                     size_t n_windows, int amplitude, int sigma, int16_t *d_pcm,
                     uint8_t *d_symbols, void *stream);
 
+/* Read-only reference stream (benchmarks): reads n_bytes (a multiple of
+ * 8192, 16-byte aligned) of device memory with the detector kernels' access
+ * pattern (8 KiB per wave, coalesced 16 B/lane non-temporal loads) and
+ * discards it, enqueued on `stream`. Its bandwidth is the practical HBM read
+ * ceiling the detectors are reported against. */
+int demod_read_ceiling_async(const void *d_buf, size_t n_bytes, void *stream);
+
 /* ---- misc -------------------------------------------------------------- */
 const char *demod_strerror(int error);   /* mirrors opus_strerror */
 const char *demod_version_string(void);  /* mirrors opus_get_version_string */

@@ -220,6 +220,13 @@ int main(int argc, char **argv)
     p2s.xcd_swizzle = f2s.xcd_swizzle = f8s.xcd_swizzle = 1;
     p2n.mag = f8n.mag = nullptr;
     add_variant(vs, GZ(2, 1, true, 4, false), 4, "goertzel [default]", p2, 2, cus, 1);
+    add_variant(vs, GZ(2, 1, true, 4, false), 4, "goertzel K2", p2, 2, cus, 2);
+    add_variant(vs, GZ(2, 1, true, 4, false), 4, "goertzel K2", p2, 2, cus, 4);
+    add_variant(vs, GZ(2, 1, true, 4, false), 4, "goertzel K2", p2, 2, cus, 8);
+    add_variant(vs, GZ(2, 2, true, 4, false), 4, "goertzel K2 PF2", p2, 2, cus, 4);
+    add_variant(vs, GZ(2, 1, true, 8, false), 8, "goertzel K2", p2, 2, cus, 1);
+    add_variant(vs, GZ(2, 1, true, 2, false), 2, "goertzel K2", p2, 2, cus, 1);
+    add_variant(vs, GZ(2, 1, true, 1, false), 1, "goertzel K2", p2, 2, cus, 1);
     add_variant(vs, GZP(4), 4, "goertzel PK [default]", p8, 4, cus, 1);
     add_variant(vs, GZP(8), 4, "goertzel PK [default]", p8, 8, cus, 1);
     add_variant(vs, GZP(8), 4, "goertzel PK", p8, 8, cus, 2);
@@ -234,6 +241,11 @@ int main(int argc, char **argv)
     add_variant(vs, GZW(8), 4, "goertzel PK WS", p8, 8, cus, 1);
     add_variant(vs, FDW(2), 4, "fold WS", f2, 2, cus, 1);
     add_variant(vs, FDW(8), 4, "fold WS", f8, 8, cus, 1);
+#define FDWB(K, B) reinterpret_cast<const void *>(&fold_tile_kernel<K, 4, true, B, false, false, true>)
+#define GZWB(K, B) reinterpret_cast<const void *>(&goertzel_tile_kernel<K, 4, 1, true, B, false, false, true, false, true>)
+    add_variant(vs, FDWB(8, 2), 2, "fold WS", f8, 8, cus, 1);
+    add_variant(vs, FDWB(8, 1), 1, "fold WS", f8, 8, cus, 1);
+    add_variant(vs, GZWB(8, 2), 2, "goertzel PK WS", p8, 8, cus, 1);
     {
         // residue-class folding (residue.hip): rotation table as demod_api.cpp
         auto make_res = [&](int K, const double *bins, GoertzelParams &p) {
@@ -290,6 +302,10 @@ int main(int argc, char **argv)
         add_variant(vs, GZP(8), 4, "goertzel PK", g8, 8, cus, 1, 0, "o");
         add_variant(vs, RZ(8), 4, "residue", r8, 8, cus, 1, residue_lds_bytes(8, 4), "o");
         add_variant(vs, RZA(8), 4, "residue allreduce-epilogue", r8, 8, cus, 1, residue_lds_bytes(8, 4), "o");
+        add_variant(vs, reinterpret_cast<const void *>(&residue_tile_kernel<8, 4, 2>), 2, "residue", r8, 8, cus, 1,
+                    (8 * 16 * 2 + 2 * 4 * 2 * 64) * 16, "o");
+        add_variant(vs, reinterpret_cast<const void *>(&residue_tile_kernel<8, 4, 1>), 1, "residue", r8, 8, cus, 1,
+                    (8 * 16 * 2 + 1 * 4 * 2 * 64) * 16, "o");
         add_variant(vs, RZA(16), 4, "residue allreduce-epilogue", r16, 16, cus, 1, residue_lds_bytes(16, 4), "o");
         add_variant(vs, RZC(8), 4, "residue C-butterfly", r8, 8, cus, 1, residue_lds_bytes(8, 4), "o");
         add_variant(vs, RZV(8), 4, "residue VGPR-rot", r8, 8, cus, 1, residue_lds_bytes(8, 4), "o");
