@@ -244,6 +244,9 @@ int main(int argc, char **argv)
 #define FDWB(K, B) reinterpret_cast<const void *>(&fold_tile_kernel<K, 4, true, B, false, false, true>)
 #define GZWB(K, B) reinterpret_cast<const void *>(&goertzel_tile_kernel<K, 4, 1, true, B, false, false, true, false, true>)
     add_variant(vs, FDWB(8, 2), 2, "fold WS", f8, 8, cus, 1);
+    add_variant(vs, FDWB(2, 2), 2, "fold WS", f2, 2, cus, 1);
+    add_variant(vs, FDWB(2, 1), 1, "fold WS", f2, 2, cus, 1);
+    add_variant(vs, FDWB(2, 8), 8, "fold WS", f2, 2, cus, 1);
     add_variant(vs, FDWB(8, 1), 1, "fold WS", f8, 8, cus, 1);
     add_variant(vs, GZWB(8, 2), 2, "goertzel PK WS", p8, 8, cus, 1);
     {
