@@ -222,6 +222,30 @@ def test_extreme_input_every_residue_class(A, O, torch, method):
     assert (sym[posed] == ref_sym[posed]).all()
 
 
+@pytest.mark.parametrize("freqs,method", [("FSK8_FREQS", FOLDED), ("FSK8_ODD", RESIDUE),
+                                          ("NONINT8", GOERTZEL)])
+def test_ties_k8(A, O, torch, freqs, method):
+    """window_sum.h decision rule (K = 8 kernels): an exact tie (the all-zero
+    window: every power 0) goes to the lowest tone. A unit impulse puts
+    exactly equal power x^2 on every tone too, but the fp32 powers differ by
+    ~1e-6 relative (rounding of the rotation constants, amplified by the
+    recurrence), more than the 2^-19 tie band: an ill-posed decision, so only
+    its magnitudes are checked (within the 1e-5 bar)."""
+    f = {"FSK8_FREQS": A.FSK8_FREQS, "FSK8_ODD": FSK8_ODD,
+         "NONINT8": tuple(1234.5 + 1111.1 * i for i in range(8))}[freqs]
+    n = 1024
+    x = np.zeros((6, n), np.int16)
+    for r, pos in enumerate((0, 1, 333, 1023)):
+        x[r + 1, pos] = 12345 if r % 2 else -7
+    with A.Demodulator(freqs=f, method=method) as d:
+        assert d.method == method
+        sym, mag = d.batch(x, mags=True)
+    assert sym[0] == 0 and sym[5] == 0 and (mag[0] == 0).all() and (mag[5] == 0).all()
+    _, ref_P = O.goertzel(x, f, n)
+    for r in range(1, 5):
+        assert np.abs(mag[r] / ref_P[r] - 1).max() <= MAG_TOL  # every tone at x^2
+
+
 def test_device_pointers_and_async(A, O, torch):
     n, W = 1024, 2048
     pcm, truth = O.synth_fsk(A.FSK8_FREQS, n, W, 5)
