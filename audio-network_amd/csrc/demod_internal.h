@@ -98,7 +98,6 @@ size_t residue_lds_bytes(int k, int log2g, int qp = 2);
 int tile_grid(long long n_windows, int log2g, int wpb = kWavesPerBlock);
 hipError_t launch_synth(const SynthParams &p, hipStream_t s);
 hipError_t launch_read_ceiling(const int16_t *p, long long n_bytes, unsigned *sink, hipStream_t s);
-hipError_t launch_fft(const FftParams &p, hipStream_t s);       // 64 lanes / window (fft.hip)
 hipError_t launch_fft_quad(const FftParams &p, hipStream_t s);  // 16 lanes / window (fft_quad.hip)
 // ip.proto framing of [n_streams][n] symbols, one frame run per stream (frame_gpu.hip)
 long long frame_streams_size(long long n, int bits, long long max_payload, unsigned *per,

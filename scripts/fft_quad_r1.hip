@@ -1,6 +1,6 @@
 // fft_quad.hip — the full-spectrum detector laid
 // out as 16 lanes per window, 4 windows per wave. Same contract as
-// fft1024_kernel (fft.hip): per window a 1024-point real FFT, |X[b]|^2 for
+// fft1024_kernel (scripts/fft_r0.hip): per window a 1024-point real FFT, |X[b]|^2 for
 // b = 0..512, symbol = argmax over the tone bins (ties -> lowest k). Oracle:
 // oracle/fsk_oracle.c:oracle_fft_demod.
 //
@@ -18,7 +18,7 @@
 //      |X[512 - k]|^2.
 // LDS traffic per window: 4 KiB written + 4 KiB read for the transpose, plus
 // 2 KiB of bin powers for the tone pick — against 12 + 12 KiB for the
-// 64-lane radix-8 Stockham layout (fft.hip), whose LDS writes bound it (guide:
+// 64-lane radix-8 Stockham layout (scripts/fft_r0.hip), whose LDS writes bound it (guide:
 // ds_write aggregates 38-51 TB/s).
 #include <algorithm>
 #include <type_traits>

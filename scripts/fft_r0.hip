@@ -1,4 +1,6 @@
-// fft.hip — full-spectrum detector: per window a
+// fft_r0.hip — FIRST LAYOUT of the full-spectrum detector, kept for the
+// interleaved A/B in scripts/probe.hip only (not built into libfskdemod.so;
+// the shipped detector is audio-network_amd/csrc/fft_quad.hip). Full-spectrum detector: per window a
 // 1024-point real FFT, |X[b]|^2 for b = 0..512, symbol = argmax over the tone
 // bins b_k = round(f_k N / fs) (ties -> lowest k). Oracle:
 // oracle/fsk_oracle.c:oracle_fft_demod (double radix-2 FFT).
@@ -18,7 +20,7 @@
 // Cost ~350 VALU + ~60 LDS ops per lane per window: compute-bound.
 #include <algorithm>
 
-#include "demod_internal.h"
+#include "../audio-network_amd/csrc/demod_internal.h"
 
 namespace fskd {
 
@@ -214,6 +216,7 @@ __global__ __launch_bounds__(64 * WPB) void fft1024_kernel(FftParams p)
 template <int WPB, bool TWLDS>
 hipError_t launch_fft_variant(const FftParams &p, hipStream_t s);
 
+hipError_t launch_fft(const FftParams &p, hipStream_t s);  // 64 lanes / window (first layout)
 hipError_t launch_fft(const FftParams &p, hipStream_t s)
 {
     return launch_fft_variant<4, false>(p, s);

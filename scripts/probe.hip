@@ -12,7 +12,7 @@
 #include "../audio-network_amd/csrc/synth.hip"
 #include "../audio-network_amd/csrc/fold.hip"
 #include "../audio-network_amd/csrc/residue.hip"
-#include "../audio-network_amd/csrc/fft.hip"
+#include "fft_r0.hip"
 #include "../audio-network_amd/csrc/fft_quad.hip"
 #include "fft_quad_r1.hip"
 
