@@ -116,7 +116,7 @@ __device__ __forceinline__ void residue_classes_asm(f2 p02, f2 p46, f2 p13, f2 p
 constexpr int kResidueQP = 2;  // shipped: two sample pairs per LDS round
 
 // Tunables (defaults = shipped, chosen with scripts/probe.hip):
-//   ASM   butterflies as residue_classes2 (else the plain-C residue_classes),
+//   ASM   butterflies as residue_classes_asm (else the plain-C residue_classes),
 //   ROTV  rotation constants in VGPRs (8 per tone) instead of the LDS table,
 //   MINW  > 0: ask for MINW waves per SIMD (VGPR budget 512 / MINW),
 //   QP    sample pairs per LDS round (1, 2 or 4): 4 QP KiB of LDS per wave,
