@@ -29,7 +29,7 @@
 static int usage(void)
 {
     fprintf(stderr, "usage: fskrx [-c 1|2] [-m left|right|downmix] [-f f1,f2,...] [-n N] "
-                    "[-H hop] [-M auto|goertzel|folded|fft] [-p frames] [-b] < pcm > frames\n");
+                    "[-H hop] [-M auto|goertzel|folded|residue|fft] [-p frames] [-b] < pcm > frames\n");
     return 2;
 }
 
@@ -100,6 +100,7 @@ int main(int argc, char **argv)
             if (!strcmp(v, "auto")) cfg.method = DEMOD_METHOD_AUTO;
             else if (!strcmp(v, "goertzel")) cfg.method = DEMOD_METHOD_GOERTZEL;
             else if (!strcmp(v, "folded")) cfg.method = DEMOD_METHOD_FOLDED;
+            else if (!strcmp(v, "residue")) cfg.method = DEMOD_METHOD_RESIDUE;
             else if (!strcmp(v, "fft")) cfg.method = DEMOD_METHOD_FFT;
             else return usage();
         } else if (!strcmp(a, "-f")) {
