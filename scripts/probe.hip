@@ -416,6 +416,8 @@ int main(int argc, char **argv)
     add_read("read-only one-shot tile (8 KiB/wave, nt, 4 waves/WG)", RT(8, 4, 2));
     add_read("read-only one-shot tile (8 KiB/wave, plain, 4 waves/WG)", RT(8, 4, 0));
     add_read("read-only one-shot tile (8 KiB/wave, nt, 8 waves/WG)", RT(8, 8, 2));
+    add_read("read-only one-shot tile (8 KiB/wave, nt, 2 waves/WG)", RT(8, 2, 2));
+    add_read("read-only one-shot tile (8 KiB/wave, nt, 1 waves/WG)", RT(8, 1, 2));
     add_read("read-only one-shot tile (8 KiB/wave, nt, 16 waves/WG)", RT(8, 16, 2));
     add_read("read-only one-shot tile (4 KiB/wave, nt, 4 waves/WG)", RT(4, 4, 2));
     add_read("read-only one-shot tile (16 KiB/wave, nt, 4 waves/WG)", RT(16, 4, 2));
