@@ -23,6 +23,7 @@
 namespace fskd {
 
 typedef unsigned int u32x4f __attribute__((ext_vector_type(4)));
+typedef float f32x2f __attribute__((ext_vector_type(2)));
 
 template <int CTRL>
 __device__ __forceinline__ float dppf_(float v)
@@ -45,8 +46,15 @@ __device__ __forceinline__ float group_sum_f(float v, int log2g)
 //           of 4K VGPRs (raises occupancy for large K).
 //   NTS: non-temporal output stores.
 //   WS: window_sum.h epilogue (reduce-scatter, packed-key argmax) at n = 1024.
+//   PK: (with WS) tone pairs in packed fp32, one v_pk_add_f32 + v_pk_fma_f32
+//       per pair per folded sample instead of 2 scalar instructions per tone.
+//   LDST: (n = 1024) load the tile as the plain bank does, 1 KiB contiguous per
+//       wave instruction, and regroup it through an 8 KiB wave-private LDS
+//       slice (linear: chunk q at 16 q, conflict-free for both the 64-chunk
+//       writes and the j + 16 m reads), instead of the direct per-lane
+//       layout whose instructions each touch four 256-byte pieces.
 template <int K, int LOG2G, bool NT = true, int WPB = 4, bool ROTLDS = false, bool NTS = false,
-          bool WS = false>
+          bool WS = false, bool PK = false, bool LDST = false>
 __global__ __launch_bounds__(64 * WPB) void fold_tile_kernel(GoertzelParams p)
 {
     const int lane = threadIdx.x & 63;
@@ -68,10 +76,19 @@ __global__ __launch_bounds__(64 * WPB) void fold_tile_kernel(GoertzelParams p)
 #pragma unroll
         for (int k = 0; k < K; ++k) r[k] = p.rot[k * g + j];
     }
+    static_assert(!LDST || LOG2G == 4, "LDST regrouping is written for n = 1024");
+    __shared__ __attribute__((aligned(16))) unsigned char lds_t[LDST ? WPB * 8192 : 16];
+    u32x4f *wl = reinterpret_cast<u32x4f *>(lds_t + (LDST ? wave * 8192 : 0));
     int goff[8];
 #pragma unroll
-    for (int m = 0; m < 8; ++m)
-        goff[m] = (int)(((long long)win_in_tile * p.hop + (long long)(j + g * m) * 8) * 2);
+    for (int m = 0; m < 8; ++m) {
+        if (LDST) {
+            const int q = 64 * m + lane;  // chunk q of the tile: window q / 128, chunk q % 128
+            goff[m] = (int)(((long long)(q >> 7) * p.hop + (long long)(q & 127) * 8) * 2);
+        } else {
+            goff[m] = (int)(((long long)win_in_tile * p.hop + (long long)(j + g * m) * 8) * 2);
+        }
+    }
 
     const long long stride = (long long)gridDim.x * WPB;
     for (long long t = tile_block(p.xcd_swizzle) * WPB + wave; t < n_tiles; t += stride) {
@@ -84,6 +101,17 @@ __global__ __launch_bounds__(64 * WPB) void fold_tile_kernel(GoertzelParams p)
 #pragma unroll
         for (int m = 0; m < 8; ++m)
             v[m] = __builtin_amdgcn_raw_buffer_load_b128(rs, goff[m], 0, NT ? 2 : 0);
+        if (LDST) {
+#pragma unroll
+            for (int m = 0; m < 8; ++m) wl[64 * m + lane] = v[m];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+            for (int m = 0; m < 8; ++m) v[m] = wl[128 * win_in_tile + 16 * m + j];
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+        }
 
         int acc[8];
 #pragma unroll
@@ -103,8 +131,25 @@ __global__ __launch_bounds__(64 * WPB) void fold_tile_kernel(GoertzelParams p)
 
         if constexpr (WS && LOG2G == 4) {
             float xr[K], xi[K];
+            float t1[K], t2[K];
+            constexpr int H = PK ? K / 2 : 0;  // packed tone pairs; the rest scalar
 #pragma unroll
-            for (int k = 0; k < K; ++k) {
+            for (int h = 0; h < H; ++h) {
+                const f32x2f c2 = f32x2f{p.coef[2 * h], p.coef[2 * h + 1]};
+                f32x2f a1 = f32x2f{0.f, 0.f}, a2 = f32x2f{0.f, 0.f};
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const f32x2f a = __builtin_elementwise_fma(c2, a1, f32x2f{xf[q], xf[q]} - a2);
+                    a2 = a1;
+                    a1 = a;
+                }
+                t1[2 * h] = a1.x;
+                t1[2 * h + 1] = a1.y;
+                t2[2 * h] = a2.x;
+                t2[2 * h + 1] = a2.y;
+            }
+#pragma unroll
+            for (int k = 2 * H; k < K; ++k) {
                 float s1 = 0.f, s2 = 0.f;
 #pragma unroll
                 for (int q = 0; q < 8; ++q) {
@@ -112,9 +157,14 @@ __global__ __launch_bounds__(64 * WPB) void fold_tile_kernel(GoertzelParams p)
                     s2 = s1;
                     s1 = a;
                 }
+                t1[k] = s1;
+                t2[k] = s2;
+            }
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
                 const float4 rk = ROTLDS ? rot_lds[k * g + j] : r[ROTLDS ? 0 : k];
-                xr[k] = rk.x * s1 - rk.z * s2;
-                xi[k] = rk.y * s1 - rk.w * s2;
+                xr[k] = rk.x * t1[k] - rk.z * t2[k];
+                xi[k] = rk.y * t1[k] - rk.w * t2[k];
             }
             const long long w = wbase + win_in_tile;
             window_sum_decide<K>(xr, xi, lane, w, w < p.n_windows, p.sym, p.mag);
@@ -156,9 +206,12 @@ __global__ __launch_bounds__(64 * WPB) void fold_tile_kernel(GoertzelParams p)
 template <int K>
 static const void *fold_kernel_for(int log2g)
 {
-    // window_sum.h epilogue at n = 1024 (K = 8: 352 -> 347 us, K = 2: 335 -> 329 us)
+    // n = 1024: window_sum.h epilogue (K = 8: 352 -> 347 us, K = 2: 335 -> 329 us)
+    // and LDS regrouping of contiguous loads (K = 8: 345.8 -> 339.9 us, K = 2:
+    // 338.5 -> 319.9 us; profiles/round1/probe_ldst.log)
     if (log2g == 4)
-        return reinterpret_cast<const void *>(&fold_tile_kernel<K, 4, true, kPlainWPB, false, false, true>);
+        return reinterpret_cast<const void *>(
+            &fold_tile_kernel<K, 4, true, kPlainWPB, false, false, true, false, true>);
     return reinterpret_cast<const void *>(&fold_tile_kernel<K, -1, true, kPlainWPB>);
 }
 

@@ -122,9 +122,14 @@ constexpr int kResidueQP = 2;  // shipped: two sample pairs per LDS round
 //   QP    sample pairs per LDS round (1, 2 or 4): 4 QP KiB of LDS per wave,
 //   PF    prefetch the wave's next tile before computing the current one
 //         (only matters on grids with more than one tile per wave),
-//   WS    window_sum.h epilogue (reduce-scatter, packed-key argmax) at n = 1024.
+//   WS    window_sum.h epilogue (reduce-scatter, packed-key argmax) at n = 1024,
+//   LDST  (n = 1024, QP = 2) load the tile 1 KiB contiguous per wave
+//         instruction, as the plain bank does, and regroup it through the
+//         wave's LDS slice (linear chunk q at 16 q; the class pairs reuse the
+//         slice afterwards) instead of the direct per-lane layout.
 template <int K, int LOG2G, int WPB = kWavesPerBlock, bool ASM = true, bool ROTV = false,
-          int MINW = (K <= 8 ? 4 : 0), int QP = kResidueQP, bool PF = false, bool WS = true>
+          int MINW = (K <= 8 ? 4 : 0), int QP = kResidueQP, bool PF = false, bool WS = true,
+          bool LDST = false>
 __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MINW > 0 ? MINW : 1)))
 void residue_tile_kernel(GoertzelParams p)
 {
@@ -142,10 +147,17 @@ void residue_tile_kernel(GoertzelParams p)
     f4 *rot = lds_r;
     f4 *zw = lds_r + K * g * 2 + wave * (4 * QP * 64) + lane;
     const f4 *grot = reinterpret_cast<const f4 *>(p.rot);
+    static_assert(!LDST || (LOG2G == 4 && QP == 2), "LDST regrouping: n = 1024, 8 KiB slice");
     int goff[8];
 #pragma unroll
-    for (int m = 0; m < 8; ++m)
-        goff[m] = (int)(((long long)win_in_tile * p.hop + (long long)(j + g * m) * 8) * 2);
+    for (int m = 0; m < 8; ++m) {
+        if (LDST) {
+            const int q = 64 * m + lane;  // chunk q of the tile: window q / 128, chunk q % 128
+            goff[m] = (int)(((long long)(q >> 7) * p.hop + (long long)(q & 127) * 8) * 2);
+        } else {
+            goff[m] = (int)(((long long)win_in_tile * p.hop + (long long)(j + g * m) * 8) * 2);
+        }
+    }
     auto load_tile = [&](long long tt, u32x4r v[8]) {
         const long long wbase = tt * wins_per_tile;
         long long bytes = ((p.n_windows - wbase - 1) * p.hop + n) * 2;
@@ -188,6 +200,18 @@ void residue_tile_kernel(GoertzelParams p)
             if (!first) load_tile(t, v);
 #pragma unroll
             for (int m = 0; m < 8; ++m) cur[m] = v[m];
+        }
+        if (LDST) {
+            u32x4r *wl = reinterpret_cast<u32x4r *>(zw - lane);  // the wave's 8 KiB slice
+#pragma unroll
+            for (int m = 0; m < 8; ++m) wl[64 * m + lane] = cur[m];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+            for (int m = 0; m < 8; ++m) cur[m] = wl[128 * win_in_tile + 16 * m + j];
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            __builtin_amdgcn_wave_barrier();
         }
 
         f2 s1[K], s2[K];

@@ -242,12 +242,21 @@ int main(int argc, char **argv)
     add_variant(vs, FDW(2), 4, "fold WS", f2, 2, cus, 1);
     add_variant(vs, FDW(8), 4, "fold WS", f8, 8, cus, 1);
 #define FDWB(K, B) reinterpret_cast<const void *>(&fold_tile_kernel<K, 4, true, B, false, false, true>)
+#define FDWP(K, B) reinterpret_cast<const void *>(&fold_tile_kernel<K, 4, true, B, false, false, true, true>)
+#define FDWT(K, B) reinterpret_cast<const void *>(&fold_tile_kernel<K, 4, true, B, false, false, true, false, true>)
 #define GZWB(K, B) reinterpret_cast<const void *>(&goertzel_tile_kernel<K, 4, 1, true, B, false, false, true, false, true>)
     add_variant(vs, FDWB(8, 2), 2, "fold WS", f8, 8, cus, 1);
     add_variant(vs, FDWB(2, 2), 2, "fold WS", f2, 2, cus, 1);
     add_variant(vs, FDWB(2, 1), 1, "fold WS", f2, 2, cus, 1);
     add_variant(vs, FDWB(2, 8), 8, "fold WS", f2, 2, cus, 1);
     add_variant(vs, FDWB(8, 1), 1, "fold WS", f8, 8, cus, 1);
+    add_variant(vs, FDWP(8, 2), 2, "fold WS PK", f8, 8, cus, 1);
+    add_variant(vs, FDWP(8, 4), 4, "fold WS PK", f8, 8, cus, 1);
+    add_variant(vs, FDWT(8, 2), 2, "fold WS LDST", f8, 8, cus, 1);
+    add_variant(vs, FDWT(8, 4), 4, "fold WS LDST", f8, 8, cus, 1);
+    add_variant(vs, FDWT(2, 2), 2, "fold WS LDST", f2, 2, cus, 1);
+    add_variant(vs, reinterpret_cast<const void *>(&fold_tile_kernel<8, 4, true, 2, false, false, true, true, true>),
+                2, "fold WS PK LDST", f8, 8, cus, 1);
     add_variant(vs, GZWB(8, 2), 2, "goertzel PK WS", p8, 8, cus, 1);
     {
         // residue-class folding (residue.hip): rotation table as demod_api.cpp
@@ -305,6 +314,10 @@ int main(int argc, char **argv)
         add_variant(vs, GZP(8), 4, "goertzel PK", g8, 8, cus, 1, 0, "o");
         add_variant(vs, RZ(8), 4, "residue", r8, 8, cus, 1, residue_lds_bytes(8, 4), "o");
         add_variant(vs, RZA(8), 4, "residue allreduce-epilogue", r8, 8, cus, 1, residue_lds_bytes(8, 4), "o");
+        add_variant(vs, reinterpret_cast<const void *>(&residue_tile_kernel<8, 4, 4, true, false, 4, 2, false, true, true>),
+                    4, "residue LDST", r8, 8, cus, 1, residue_lds_bytes(8, 4), "o");
+        add_variant(vs, reinterpret_cast<const void *>(&residue_tile_kernel<16, 4, 4, true, false, 0, 2, false, true, true>),
+                    4, "residue LDST", r16, 16, cus, 1, residue_lds_bytes(16, 4), "o");
         add_variant(vs, reinterpret_cast<const void *>(&residue_tile_kernel<8, 4, 2>), 2, "residue", r8, 8, cus, 1,
                     (8 * 16 * 2 + 2 * 4 * 2 * 64) * 16, "o");
         add_variant(vs, reinterpret_cast<const void *>(&residue_tile_kernel<8, 4, 1>), 1, "residue", r8, 8, cus, 1,
