@@ -70,3 +70,13 @@ def test_strerror_and_version(A):
     assert A.strerror(A.DEMOD_NO_DEVICE).startswith("no gfx950")
     assert A.strerror(12345) == "unknown error"
     assert "gfx950" in A.version_string()
+
+
+def test_integration_doc_maps_every_export(A):
+    """INTEGRATION.md §1 names every entry point include/demod.h declares
+    (mapped to the reference interface it replaces, or marked as having none)."""
+    import os
+    doc = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                            "INTEGRATION.md")).read()
+    missing = [n for n in A.header_exports() if n not in doc]
+    assert not missing, missing
