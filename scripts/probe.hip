@@ -298,6 +298,11 @@ int main(int argc, char **argv)
         make_res(4, bo, r4);
         make_res(8, bo, r8);
         make_res(16, bo, r16);
+        static double be[8];
+        for (int i = 0; i < 8; ++i) be[i] = 34 + 6 * i;  // even bins: classes 0 and 3 only
+        static GoertzelParams r8e = p8, g8e = p8;
+        make_res(8, be, r8e);
+        make_rot(8, be, g8e);
         make_rot(3, bo, g3);
         make_rot(4, bo, g4);
         make_rot(8, bo, g8);
@@ -351,6 +356,8 @@ int main(int argc, char **argv)
             add_variant(vs, GZP(16), 4, "goertzel PK", g16, 16, cus, 1, 0, "o");
         }
         add_variant(vs, RZ(16), 4, "residue", r16, 16, cus, 1, residue_lds_bytes(16, 4), "o");
+        add_variant(vs, RZ(8), 4, "residue", r8e, 8, cus, 1, residue_lds_bytes(8, 4), "e");
+        add_variant(vs, GZW(8), 4, "goertzel PK WS", g8e, 8, cus, 1, 0, "e");
 #undef RZ
 #undef RZC
 #undef RZV
