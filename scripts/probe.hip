@@ -358,6 +358,7 @@ int main(int argc, char **argv)
         add_variant(vs, RZ(16), 4, "residue", r16, 16, cus, 1, residue_lds_bytes(16, 4), "o");
         add_variant(vs, RZ(8), 4, "residue", r8e, 8, cus, 1, residue_lds_bytes(8, 4), "e");
         add_variant(vs, GZW(8), 4, "goertzel PK WS", g8e, 8, cus, 1, 0, "e");
+        add_variant(vs, GZW(8), 4, "goertzel PK WS", g8, 8, cus, 1, 0, "o");
 #undef RZ
 #undef RZC
 #undef RZV
