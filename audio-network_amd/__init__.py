@@ -66,6 +66,43 @@ class DemodCfg(ctypes.Structure):
     ]
 
 
+DEMOD_PORT_AUDIO_RX = 58764
+DEMOD_PORT_DISCOVERY = 58765
+DEMOD_BROADCAST_MAGIC = 0x2C5DA044
+DEMOD_INFO_STRING_CAP = 128
+DEMOD_MAX_DECODED_FRAME = 11520
+DEMOD_MSG_NONE = 0
+DEMOD_MSG_DISCOVERY_REQUEST = 2
+DEMOD_MSG_DISCOVERY_RESPONSE = 3
+DEMOD_MSG_RECEIVER_INFORMATION = 1
+DEMOD_MSG_RECEIVER_ERROR = 2
+
+
+class DemodDiscovery(ctypes.Structure):
+    """demod_discovery_t (include/demod.h) = DiscoveryResponse, ip.pb.h:17-24."""
+    _fields_ = [
+        ("protocol_version", ctypes.c_uint32),
+        ("mac_address", ctypes.c_uint64),
+        ("device_name", ctypes.c_char * DEMOD_INFO_STRING_CAP),
+        ("currently_streaming", ctypes.c_int),
+        ("opus_version", ctypes.c_char * DEMOD_INFO_STRING_CAP),
+    ]
+
+
+class DemodReceiverInfo(ctypes.Structure):
+    """demod_receiver_info_t = ReceiverInformation, ip.pb.h:55-59."""
+    _fields_ = [
+        ("discovery_data", DemodDiscovery),
+        ("max_encoded_frame_size", ctypes.c_uint32),
+        ("max_decoded_frame_size", ctypes.c_uint32),
+    ]
+
+
+class DemodReceiverError(ctypes.Structure):
+    """demod_receiver_error_t = ReceiverError, ip.pb.h:26-31."""
+    _fields_ = [("audio_underflow", ctypes.c_int), ("audio_decode_error", ctypes.c_int)]
+
+
 class DemodError(RuntimeError):
     def __init__(self, code: int, what: str = ""):
         self.code = code
@@ -119,6 +156,17 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "demod_frame_symbols_size": (ctypes.c_longlong, [_SZ, ctypes.c_int, _SZ]),
         "demod_frame_streams_async": (ctypes.c_longlong, [_P, _SZ, _SZ, ctypes.c_int, _SZ, _P,
                                                           _P]),
+        "demod_broadcast_request_encode": (ctypes.c_int, [_P, _SZ]),
+        "demod_broadcast_response_encode": (ctypes.c_int, [ctypes.POINTER(DemodDiscovery), _P,
+                                                           _SZ]),
+        "demod_broadcast_decode": (ctypes.c_int, [_P, _SZ, ctypes.POINTER(ctypes.c_uint32),
+                                                  ctypes.POINTER(DemodDiscovery)]),
+        "demod_hello_encode": (ctypes.c_int, [ctypes.POINTER(DemodReceiverInfo), _P, _SZ]),
+        "demod_receiver_error_encode": (ctypes.c_int, [ctypes.POINTER(DemodReceiverError), _P,
+                                                       _SZ]),
+        "demod_to_transmitter_decode": (ctypes.c_int, [_P, _SZ, ctypes.POINTER(DemodReceiverInfo),
+                                                       ctypes.POINTER(DemodReceiverError),
+                                                       ctypes.POINTER(_SZ)]),
         "demod_synth_fsk": (ctypes.c_int, [ctypes.POINTER(DemodCfg), ctypes.c_uint64,
                                            ctypes.c_uint64, _SZ, ctypes.c_int, ctypes.c_int,
                                            _P, _P, _P]),
@@ -355,6 +403,98 @@ def frame_decode(buf: bytes) -> Tuple[bytes, int]:
         raise DemodError(rc, "demod_frame_decode")
     off = (pl.value or ctypes.addressof(src)) - ctypes.addressof(src)
     return bytes(buf[off:off + pl_len.value]), int(used.value)
+
+
+# ---- ip.proto session messages (host; include/demod.h, demod_session.c) ----
+
+def _discovery_struct(d: dict) -> DemodDiscovery:
+    s = DemodDiscovery()
+    s.protocol_version = int(d.get("protocol_version", 1))
+    s.mac_address = int(d.get("mac_address", 0))
+    s.device_name = bytes(d.get("device_name", b""))
+    s.currently_streaming = int(bool(d.get("currently_streaming", False)))
+    s.opus_version = bytes(d.get("opus_version", b""))
+    return s
+
+
+def _discovery_dict(s: DemodDiscovery) -> dict:
+    return {"protocol_version": int(s.protocol_version), "mac_address": int(s.mac_address),
+            "device_name": bytes(s.device_name), "currently_streaming": bool(s.currently_streaming),
+            "opus_version": bytes(s.opus_version)}
+
+
+def _session_call(fn, name, *args, cap=1024) -> bytes:
+    out = (ctypes.c_uint8 * cap)()
+    rc = fn(*args, out, cap)
+    if rc < 0:
+        raise DemodError(rc, name)
+    return bytes(out[:rc])
+
+
+def broadcast_request_encode() -> bytes:
+    """BroadcastMessage{magic, discovery_request = true} (discovery.kt:44-48)."""
+    return _session_call(load_library().demod_broadcast_request_encode,
+                         "demod_broadcast_request_encode")
+
+
+def broadcast_response_encode(d: dict) -> bytes:
+    """BroadcastMessage{magic, discovery_response = d} (network.cpp:356-378)."""
+    s = _discovery_struct(d)
+    return _session_call(load_library().demod_broadcast_response_encode,
+                         "demod_broadcast_response_encode", ctypes.byref(s))
+
+
+def broadcast_decode(buf: bytes):
+    """-> (which, magic, discovery dict or None); DemodError where nanopb fails."""
+    lib = load_library()
+    src = (ctypes.c_uint8 * max(len(buf), 1)).from_buffer_copy(buf or b"\0")
+    magic = ctypes.c_uint32()
+    d = DemodDiscovery()
+    rc = lib.demod_broadcast_decode(src, len(buf), ctypes.byref(magic), ctypes.byref(d))
+    if rc < 0:
+        raise DemodError(rc, "demod_broadcast_decode")
+    return rc, int(magic.value), (_discovery_dict(d) if rc == DEMOD_MSG_DISCOVERY_RESPONSE
+                                  else None)
+
+
+def hello_encode(info: dict) -> bytes:
+    """Delimited ToTransmitter{receiver_information} (network.cpp:388-403)."""
+    s = DemodReceiverInfo()
+    s.discovery_data = _discovery_struct(info.get("discovery_data", {}))
+    s.max_encoded_frame_size = int(info.get("max_encoded_frame_size", DEMOD_MAX_FRAME_PAYLOAD))
+    s.max_decoded_frame_size = int(info.get("max_decoded_frame_size", DEMOD_MAX_DECODED_FRAME))
+    return _session_call(load_library().demod_hello_encode, "demod_hello_encode",
+                         ctypes.byref(s))
+
+
+def receiver_error_encode(audio_underflow: bool, audio_decode_error: bool) -> bytes:
+    """Delimited ToTransmitter{error}."""
+    s = DemodReceiverError(int(bool(audio_underflow)), int(bool(audio_decode_error)))
+    return _session_call(load_library().demod_receiver_error_encode,
+                         "demod_receiver_error_encode", ctypes.byref(s))
+
+
+def to_transmitter_decode(buf: bytes):
+    """Delimited ToTransmitter -> (which, fields dict or None, bytes consumed)."""
+    lib = load_library()
+    src = (ctypes.c_uint8 * max(len(buf), 1)).from_buffer_copy(buf or b"\0")
+    info = DemodReceiverInfo()
+    err = DemodReceiverError()
+    used = _SZ()
+    rc = lib.demod_to_transmitter_decode(src, len(buf), ctypes.byref(info), ctypes.byref(err),
+                                         ctypes.byref(used))
+    if rc < 0:
+        raise DemodError(rc, "demod_to_transmitter_decode")
+    if rc == DEMOD_MSG_RECEIVER_INFORMATION:
+        fields = {"discovery_data": _discovery_dict(info.discovery_data),
+                  "max_encoded_frame_size": int(info.max_encoded_frame_size),
+                  "max_decoded_frame_size": int(info.max_decoded_frame_size)}
+    elif rc == DEMOD_MSG_RECEIVER_ERROR:
+        fields = {"audio_underflow": bool(err.audio_underflow),
+                  "audio_decode_error": bool(err.audio_decode_error)}
+    else:
+        fields = None
+    return rc, fields, int(used.value)
 
 
 def bits_per_symbol(k: int) -> int:

@@ -8,6 +8,7 @@
  *
  *   fskrx [-c 1|2] [-m left|right|downmix] [-f f1,f2,...] [-n N] [-H hop]
  *         [-M auto|goertzel|folded|fft] [-p frames_per_read] [-b] < pcm > frames
+ *   fskrx [same options] -l tcp_port [-u udp_port] [-a addr] [-N name] [-1] > frames
  *
  * Default: 48 kHz mono, N = hop = 1024, 2-FSK at 1500/3000 Hz, reads of 2880
  * frames (one 60 ms packet) each passed to demodulate(). -b reads all input
@@ -16,20 +17,43 @@
  * the final partial payload is flushed at EOF. Statistics go to stderr.
  * Exit status: 0 ok, 2 usage, 3 demod_create failed (e.g. no gfx950 device:
  * there is no CPU fallback), 4 demodulation / framing error, 5 I/O error.
+ *
+ * Network mode (-l) takes the receiver's place on the
+ * wire instead of stdin: it listens on TCP (58764 in the reference,
+ * network.cpp:496-516; 0 = any free port), writes the ToTransmitter hello to
+ * each transmitter that connects (network.cpp:380-403), resets the stream
+ * (playback_start_new_stream, network.cpp:406-407) and reads delimited
+ * ToReceiver frames until the transmitter closes or sends a frame nanopb
+ * would reject (network.cpp:409-430). One transmitter at a time, like the
+ * firmware. With -u it also answers UDP discovery requests
+ * (network.cpp:449-494). The AudioData bytes are taken as raw int16 LE PCM of
+ * the configured channel layout: Opus decoding is outside this build (the
+ * reference libopus needs an ESP32 header this image lacks),
+ * so a transmitter feeds PCM through the same frame layout. -1 exits after
+ * the first transmitter disconnects. The bound ports are printed on stderr
+ * as "fskrx: listening tcp <port> udp <port>".
  */
-#define _POSIX_C_SOURCE 199309L
+#define _POSIX_C_SOURCE 200112L
+#include <arpa/inet.h>
+#include <errno.h>
+#include <netinet/in.h>
+#include <poll.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/socket.h>
 #include <time.h>
+#include <unistd.h>
 
 #include "../../include/demod.h"
 
 static int usage(void)
 {
     fprintf(stderr, "usage: fskrx [-c 1|2] [-m left|right|downmix] [-f f1,f2,...] [-n N] "
-                    "[-H hop] [-M auto|goertzel|folded|residue|fft] [-p frames] [-b] < pcm > frames\n");
+                    "[-H hop] [-M auto|goertzel|folded|residue|fft] [-p frames] [-b] < pcm > frames\n"
+                    "       fskrx [options] -l tcp_port [-u udp_port] [-a addr] [-N name] [-1] "
+                    "> frames\n");
     return 2;
 }
 
@@ -75,19 +99,224 @@ static int sink_push(struct sink *s, const uint8_t *sym, size_t n)
     return 0;
 }
 
+/* ---- network mode ------------------------------------------------------ */
+
+struct net {
+    const char *addr;
+    int tcp_port, udp_port; /* udp_port < 0: no discovery responder */
+    const char *name;
+    int once;
+};
+
+static int bind_socket(int type, const char *addr, int port, int *bound)
+{
+    int fd = socket(AF_INET, type, 0);
+    if (fd < 0) return -1;
+    int one = 1;
+    setsockopt(fd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
+    struct sockaddr_in sa;
+    memset(&sa, 0, sizeof sa);
+    sa.sin_family = AF_INET;
+    sa.sin_port = htons((uint16_t)port);
+    if (inet_pton(AF_INET, addr, &sa.sin_addr) != 1 ||
+        bind(fd, (struct sockaddr *)&sa, sizeof sa) != 0 ||
+        (type == SOCK_STREAM && listen(fd, 1) != 0)) {
+        close(fd);
+        return -1;
+    }
+    socklen_t len = sizeof sa;
+    getsockname(fd, (struct sockaddr *)&sa, &len);
+    *bound = ntohs(sa.sin_port);
+    return fd;
+}
+
+static int send_all(int fd, const uint8_t *p, size_t n)
+{
+    while (n) {
+        ssize_t w = send(fd, p, n, MSG_NOSIGNAL);
+        if (w < 0 && errno == EINTR) continue;
+        if (w <= 0) return -1;
+        p += w;
+        n -= (size_t)w;
+    }
+    return 0;
+}
+
+/* Demodulate the whole frames of pcm bytes held in buf[0..*len); keeps the
+ * bytes of a frame split across payloads for the next call. */
+static int feed_pcm(demod_t *st, struct sink *s, uint8_t *buf, size_t *len, size_t frame_bytes,
+                    uint8_t **sym, size_t *sym_cap, unsigned long long *frames_in)
+{
+    size_t nf = *len / frame_bytes;
+    if (!nf) return 0;
+    int need = demod_max_symbols(st, nf);
+    if (need < 0) return 4;
+    if ((size_t)need > *sym_cap) {
+        uint8_t *p = realloc(*sym, (size_t)need + 16);
+        if (!p) return 4;
+        *sym = p;
+        *sym_cap = (size_t)need + 16;
+    }
+    int ns = demodulate(st, (const int16_t *)(const void *)buf, nf, *sym, *sym_cap);
+    if (ns < 0) {
+        fprintf(stderr, "fskrx: demodulate: %s\n", demod_strerror(ns));
+        return 4;
+    }
+    *frames_in += nf;
+    memmove(buf, buf + nf * frame_bytes, *len - nf * frame_bytes);
+    *len -= nf * frame_bytes;
+    return sink_push(s, *sym, (size_t)ns);
+}
+
+static int serve(demod_t *st, const demod_cfg_t *cfg, struct sink *s, const struct net *nt,
+                 unsigned long long *frames_in)
+{
+    int tport = 0, uport = -1;
+    int lfd = bind_socket(SOCK_STREAM, nt->addr, nt->tcp_port, &tport);
+    int ufd = nt->udp_port >= 0 ? bind_socket(SOCK_DGRAM, nt->addr, nt->udp_port, &uport) : -1;
+    if (lfd < 0 || (nt->udp_port >= 0 && ufd < 0)) {
+        fprintf(stderr, "fskrx: cannot bind %s: %s\n", nt->addr, strerror(errno));
+        if (lfd >= 0) close(lfd);
+        return 5;
+    }
+    fprintf(stderr, "fskrx: listening tcp %d udp %d\n", tport, uport);
+    fflush(stderr);
+
+    demod_discovery_t disc;
+    memset(&disc, 0, sizeof disc);
+    disc.protocol_version = 1; /* network.cpp:374 */
+    snprintf(disc.device_name, sizeof disc.device_name, "%s", nt->name);
+    snprintf(disc.opus_version, sizeof disc.opus_version, "%s", demod_version_string());
+
+    const size_t frame_bytes = sizeof(int16_t) * cfg->channels;
+    size_t in_cap = 2 * demod_frame_size(DEMOD_MAX_FRAME_PAYLOAD), in_len = 0;
+    size_t pcm_cap = 4 * DEMOD_MAX_FRAME_PAYLOAD, pcm_len = 0;
+    uint8_t *in = malloc(in_cap), *pcm = malloc(pcm_cap), *sym = NULL;
+    size_t sym_cap = 0;
+    int cfd = -1, rc = (in && pcm) ? 0 : 4, done = 0;
+    unsigned long long clients = 0, answered = 0;
+    while (!rc && !done) {
+        struct pollfd pf[2];
+        int np = 0;
+        pf[np].fd = cfd >= 0 ? cfd : lfd; /* one transmitter at a time */
+        pf[np++].events = POLLIN;
+        if (ufd >= 0) {
+            pf[np].fd = ufd;
+            pf[np++].events = POLLIN;
+        }
+        if (poll(pf, (nfds_t)np, -1) < 0) {
+            if (errno == EINTR) continue;
+            rc = 5;
+            break;
+        }
+        if (ufd >= 0 && (pf[1].revents & POLLIN)) {
+            uint8_t dg[768]; /* protobuf_buffer_len, network.cpp:450 */
+            struct sockaddr_storage from;
+            socklen_t flen = sizeof from;
+            ssize_t n = recvfrom(ufd, dg, sizeof dg, 0, (struct sockaddr *)&from, &flen);
+            uint32_t magic = 0;
+            if (n >= 0 &&
+                demod_broadcast_decode(dg, (size_t)n, &magic, NULL) == DEMOD_MSG_DISCOVERY_REQUEST &&
+                magic == DEMOD_BROADCAST_MAGIC) {
+                disc.currently_streaming = cfd >= 0;
+                int w = demod_broadcast_response_encode(&disc, dg, sizeof dg);
+                if (w > 0 && sendto(ufd, dg, (size_t)w, 0, (struct sockaddr *)&from, flen) == w)
+                    ++answered;
+            }
+        }
+        if (!(pf[0].revents & (POLLIN | POLLHUP | POLLERR))) continue;
+        if (cfd < 0) {
+            cfd = accept(lfd, NULL, NULL);
+            if (cfd < 0) continue;
+            ++clients;
+            demod_receiver_info_t info;
+            memset(&info, 0, sizeof info);
+            info.discovery_data = disc;
+            info.discovery_data.currently_streaming = 0;
+            info.max_encoded_frame_size = DEMOD_MAX_FRAME_PAYLOAD;  /* network.cpp:392 */
+            info.max_decoded_frame_size = DEMOD_MAX_DECODED_FRAME;  /* network.cpp:393 */
+            uint8_t hello[512];
+            int w = demod_hello_encode(&info, hello, sizeof hello);
+            if (w < 0 || send_all(cfd, hello, (size_t)w) != 0) {
+                fprintf(stderr, "fskrx: failed to write hello, closing connection\n");
+                close(cfd);
+                cfd = -1;
+                continue;
+            }
+            demod_reset(st);
+            in_len = pcm_len = 0;
+            continue;
+        }
+        ssize_t got = recv(cfd, in + in_len, in_cap - in_len, 0);
+        if (got < 0 && errno == EINTR) continue;
+        int end_stream = got <= 0;
+        if (got > 0) in_len += (size_t)got;
+        size_t off = 0;
+        while (!rc && !end_stream) {
+            const uint8_t *pl;
+            size_t pl_len, used;
+            int d = demod_frame_decode(in + off, in_len - off, &pl, &pl_len, &used);
+            if (d == DEMOD_BUFFER_TOO_SMALL) break;
+            if (d != DEMOD_OK) {
+                fprintf(stderr, "fskrx: bad frame (%s), closing connection\n", demod_strerror(d));
+                end_stream = 1;
+                break;
+            }
+            if (pcm_len + pl_len > pcm_cap) {
+                uint8_t *p = realloc(pcm, pcm_cap * 2 + pl_len);
+                if (!p) { rc = 4; break; }
+                pcm = p;
+                pcm_cap = pcm_cap * 2 + pl_len;
+            }
+            memcpy(pcm + pcm_len, pl, pl_len);
+            pcm_len += pl_len;
+            off += used;
+        }
+        memmove(in, in + off, in_len - off);
+        in_len -= off;
+        if (!end_stream && in_len == in_cap) { /* a frame larger than any valid one */
+            fprintf(stderr, "fskrx: oversized frame, closing connection\n");
+            end_stream = 1;
+        }
+        if (!rc) rc = feed_pcm(st, s, pcm, &pcm_len, frame_bytes, &sym, &sym_cap, frames_in);
+        if (end_stream) {
+            close(cfd);
+            cfd = -1;
+            if (!rc && s->n) rc = sink_emit(s, s->n); /* end of this stream's symbols */
+            if (!rc && fflush(stdout) != 0) rc = 5;
+            done = nt->once;
+        }
+    }
+    fprintf(stderr, "fskrx: %llu transmitter(s) served, %llu discovery request(s) answered\n",
+            clients, answered);
+    if (cfd >= 0) close(cfd);
+    close(lfd);
+    if (ufd >= 0) close(ufd);
+    free(in);
+    free(pcm);
+    free(sym);
+    return rc;
+}
+
 int main(int argc, char **argv)
 {
     demod_cfg_t cfg;
     demod_cfg_default(&cfg);
     size_t per_read = 2880; /* one 60 ms packet at 48 kHz (playback.cpp:10) */
     int batch = 0;
+    struct net nt = {"0.0.0.0", -1, -1, "", 0};
     for (int i = 1; i < argc; ++i) {
         const char *a = argv[i];
         const char *v = i + 1 < argc ? argv[i + 1] : NULL;
         if (!strcmp(a, "-b")) { batch = 1; continue; }
+        if (!strcmp(a, "-1")) { nt.once = 1; continue; }
         if (!v) return usage();
         ++i;
         if (!strcmp(a, "-c")) cfg.channels = (uint32_t)atoi(v);
+        else if (!strcmp(a, "-l")) nt.tcp_port = atoi(v);
+        else if (!strcmp(a, "-u")) nt.udp_port = atoi(v);
+        else if (!strcmp(a, "-a")) nt.addr = v;
+        else if (!strcmp(a, "-N")) nt.name = v;
         else if (!strcmp(a, "-n")) cfg.n = (uint32_t)atoi(v);
         else if (!strcmp(a, "-H")) cfg.hop = (uint32_t)atoi(v);
         else if (!strcmp(a, "-p")) per_read = (size_t)strtoull(v, NULL, 10);
@@ -117,7 +346,9 @@ int main(int argc, char **argv)
             return usage();
         }
     }
-    if (per_read == 0) return usage();
+    if (per_read == 0 || (nt.tcp_port < 0 && (nt.udp_port >= 0 || nt.once)) ||
+        strlen(nt.name) >= DEMOD_INFO_STRING_CAP)
+        return usage();
 
     int err = 0;
     demod_t *st = demod_create(&cfg, &err);
@@ -135,13 +366,14 @@ int main(int argc, char **argv)
 
     const size_t ch = cfg.channels;
     size_t cap = batch ? ((size_t)1 << 20) : per_read;
-    int16_t *pcm = malloc(cap * ch * sizeof(int16_t));
+    int16_t *pcm = nt.tcp_port >= 0 ? NULL : malloc(cap * ch * sizeof(int16_t));
     uint8_t *sym = NULL;
     size_t sym_cap = 0;
     size_t have = 0;
     struct timespec t0, t1;
     clock_gettime(CLOCK_MONOTONIC, &t0);
     unsigned long long frames_in = 0;
+    if (!rc && nt.tcp_port >= 0) rc = serve(st, &cfg, &s, &nt, &frames_in);
     while (!rc && pcm) {
         size_t got = fread(pcm + have * ch, sizeof(int16_t) * ch, cap - have, stdin);
         have += got;

@@ -201,6 +201,82 @@ long long demod_frame_streams_async(const uint8_t *d_symbols, size_t n_streams, 
                                     int bits, size_t max_payload, uint8_t *d_out,
                                     void *stream);
 
+/* ---- ip.proto session messages ------------------ */
+/* What a receiver exchanges around the audio stream: the delimited
+ * ToTransmitter hello it writes when a transmitter connects on TCP 58764
+ * (network.cpp:388-403; read by RemoteAudioReceiver.connect,
+ * RemoteAudioReceiver.kt:60-68), and the BroadcastMessage datagrams of UDP
+ * 58765 discovery (network.cpp:449-494; discovery.kt:23-97). Encoders emit
+ * nanopb's bytes for the same struct; decoders return nanopb's verdict
+ * (demod_session.c). Pure host byte work. */
+#define DEMOD_PORT_AUDIO_RX    58764        /* ip.proto:28-31 (TCP) */
+#define DEMOD_PORT_DISCOVERY   58765        /* ip.proto:5-7 (UDP) */
+#define DEMOD_BROADCAST_MAGIC  0x2C5DA044u  /* ip.proto:10, network.cpp:448 */
+#define DEMOD_INFO_STRING_CAP  128          /* char[128] strings, ip.pb.h:20,23 */
+#define DEMOD_MAX_DECODED_FRAME 11520       /* AUDIO_BUFFER_SIZE, playback.cpp:10,193 */
+
+/* oneof member tags returned by the decoders */
+#define DEMOD_MSG_NONE                 0
+#define DEMOD_MSG_DISCOVERY_REQUEST    2  /* BroadcastMessage.discovery_request */
+#define DEMOD_MSG_DISCOVERY_RESPONSE   3  /* BroadcastMessage.discovery_response */
+#define DEMOD_MSG_RECEIVER_INFORMATION 1  /* ToTransmitter.receiver_information */
+#define DEMOD_MSG_RECEIVER_ERROR       2  /* ToTransmitter.error */
+
+typedef struct {                  /* DiscoveryResponse, ip.pb.h:17-24 */
+    uint32_t protocol_version;    /* 1 in the firmware (network.cpp:374) */
+    uint64_t mac_address;         /* 6 MAC bytes, byte i at bits 8i (network.cpp:360-363) */
+    char device_name[DEMOD_INFO_STRING_CAP];   /* NUL-terminated, <= 127 bytes */
+    int currently_streaming;
+    char opus_version[DEMOD_INFO_STRING_CAP];  /* NUL-terminated, <= 127 bytes */
+} demod_discovery_t;
+
+typedef struct {                  /* ReceiverInformation, ip.pb.h:55-59 */
+    demod_discovery_t discovery_data;
+    uint32_t max_encoded_frame_size;   /* 4096 in the firmware (network.cpp:392) */
+    uint32_t max_decoded_frame_size;   /* 11520 in the firmware (network.cpp:393) */
+} demod_receiver_info_t;
+
+typedef struct {                  /* ReceiverError, ip.pb.h:61-64 */
+    int audio_underflow;
+    int audio_decode_error;
+} demod_receiver_error_t;
+
+/* BroadcastMessage{magic_word = DEMOD_BROADCAST_MAGIC, discovery_request =
+ * true}, the datagram a transmitter broadcasts (discovery.kt:44-48).
+ * Returns bytes written or DEMOD_BUFFER_TOO_SMALL. */
+int demod_broadcast_request_encode(uint8_t *out, size_t cap);
+
+/* BroadcastMessage{magic_word, discovery_response = *d}, the receiver's
+ * unicast answer (network.cpp:356-378,486-492). Returns bytes written,
+ * DEMOD_BUFFER_TOO_SMALL, or DEMOD_BAD_ARG for an unterminated string. */
+int demod_broadcast_response_encode(const demod_discovery_t *d, uint8_t *out, size_t cap);
+
+/* Decode one datagram as BroadcastMessage. Returns the oneof member
+ * (DEMOD_MSG_NONE / _DISCOVERY_REQUEST / _DISCOVERY_RESPONSE) with *magic
+ * set (and *resp filled for a response; resp may be NULL), or
+ * DEMOD_INVALID_PACKET where nanopb's pb_decode fails. A receiver answers
+ * exactly when this returns DEMOD_MSG_DISCOVERY_REQUEST and *magic ==
+ * DEMOD_BROADCAST_MAGIC (network.cpp:473-485). */
+int demod_broadcast_decode(const uint8_t *in, size_t len, uint32_t *magic,
+                           demod_discovery_t *resp);
+
+/* Length-delimited ToTransmitter{receiver_information = *info}: the hello
+ * (network.cpp:388-403). Returns bytes written, DEMOD_BUFFER_TOO_SMALL or
+ * DEMOD_BAD_ARG. */
+int demod_hello_encode(const demod_receiver_info_t *info, uint8_t *out, size_t cap);
+
+/* Length-delimited ToTransmitter{error = *e} (ip.proto:41-44,61-66). */
+int demod_receiver_error_encode(const demod_receiver_error_t *e, uint8_t *out, size_t cap);
+
+/* Decode one length-delimited ToTransmitter from in[0..len) (the
+ * transmitter side, RemoteAudioReceiver.kt:60). Returns the oneof member
+ * (DEMOD_MSG_NONE / _RECEIVER_INFORMATION / _RECEIVER_ERROR), filling *info
+ * or *err (either may be NULL) and *consumed; DEMOD_BUFFER_TOO_SMALL when
+ * only part of the message is in `in`; DEMOD_INVALID_PACKET where nanopb's
+ * pb_decode_delimited fails. */
+int demod_to_transmitter_decode(const uint8_t *in, size_t len, demod_receiver_info_t *info,
+                                demod_receiver_error_t *err, size_t *consumed);
+
 /* ---- synthetic PCM (benchmarks / tests) -------------------------------- */
 
 /* Device generator of the seeded FSK test signal (DESIGN.md §Synthetic

@@ -3,8 +3,9 @@
  *
  * Links the reference's own nanopb 0.4.5 runtime and its generated ip.pb.c
  * (compiled in place from /root/reference by oracle/ref.mk, output only into
- * oracle/_ref/) so tests can mint and check ToReceiver frame bytes with the
- * reference's codec.
+ * oracle/_ref/) so tests can mint and check ToReceiver frame bytes, and the
+ * session messages (BroadcastMessage, ToTransmitter), with the reference's
+ * codec.
  *
  * ip.pb.h:161-162 binds AudioData's field callback to the application symbol
  * network_pb_callback_audio_data, which the firmware defines in
@@ -88,5 +89,104 @@ int ref_decode_to_receiver(const uint8_t *in, size_t len, uint8_t *payload,
     *payload_len = ctx.got;
     if (!ok) return ctx.too_large ? -10 : -1;
     if (msg.which_message != ToReceiver_audio_data_tag) return -1;
+    return 0;
+}
+
+/* ---- session messages (BroadcastMessage, ToTransmitter), reference codec --
+ * Flat view of DiscoveryResponse (ip.pb.h:17-24) for ctypes. */
+typedef struct {
+    uint32_t protocol_version;
+    uint64_t mac_address;
+    char device_name[128];
+    int32_t currently_streaming;
+    char opus_version[128];
+} ref_disc;
+
+static void disc_to_pb(const ref_disc *d, DiscoveryResponse *p)
+{
+    p->protocol_version = d->protocol_version;
+    p->mac_address = d->mac_address;
+    memcpy(p->device_name, d->device_name, sizeof p->device_name);
+    p->currently_streaming = d->currently_streaming != 0;
+    memcpy(p->opus_version, d->opus_version, sizeof p->opus_version);
+}
+
+static void disc_from_pb(const DiscoveryResponse *p, ref_disc *d)
+{
+    d->protocol_version = p->protocol_version;
+    d->mac_address = p->mac_address;
+    memcpy(d->device_name, p->device_name, sizeof d->device_name);
+    d->currently_streaming = p->currently_streaming;
+    memcpy(d->opus_version, p->opus_version, sizeof d->opus_version);
+}
+
+/* which: 0 none, 2 discovery_request (= req), 3 discovery_response (= *d).
+ * pb_encode as network.cpp:486-492. Returns bytes or -1. */
+int ref_encode_broadcast(int which, uint32_t magic, int req, const ref_disc *d, uint8_t *out,
+                         size_t cap)
+{
+    BroadcastMessage m = BroadcastMessage_init_zero;
+    m.magic_word = magic;
+    m.which_message = (pb_size_t)which;
+    if (which == BroadcastMessage_discovery_request_tag) m.message.discovery_request = req != 0;
+    if (which == BroadcastMessage_discovery_response_tag) disc_to_pb(d, &m.message.discovery_response);
+    pb_ostream_t os = pb_ostream_from_buffer(out, cap);
+    if (!pb_encode(&os, BroadcastMessage_fields, &m)) return -1;
+    return (int)os.bytes_written;
+}
+
+/* pb_decode of one datagram (network.cpp:473-478). Returns 0 / -1. */
+int ref_decode_broadcast(const uint8_t *in, size_t len, uint32_t *magic, int32_t *which,
+                         ref_disc *d)
+{
+    BroadcastMessage m = BroadcastMessage_init_zero;
+    pb_istream_t is = pb_istream_from_buffer(in, len);
+    if (!pb_decode(&is, BroadcastMessage_fields, &m)) return -1;
+    *magic = m.magic_word;
+    *which = m.which_message;
+    if (m.which_message == BroadcastMessage_discovery_response_tag)
+        disc_from_pb(&m.message.discovery_response, d);
+    return 0;
+}
+
+/* which: 0 none, 1 receiver_information, 2 error; pb_encode_delimited as
+ * network.cpp:388-403. Returns bytes or -1. */
+int ref_encode_to_transmitter(int which, const ref_disc *d, uint32_t max_enc, uint32_t max_dec,
+                              int underflow, int decode_error, uint8_t *out, size_t cap)
+{
+    ToTransmitter m = ToTransmitter_init_zero;
+    m.which_message = (pb_size_t)which;
+    if (which == ToTransmitter_receiver_information_tag) {
+        disc_to_pb(d, &m.message.receiver_information.discovery_data);
+        m.message.receiver_information.max_encoded_frame_size = max_enc;
+        m.message.receiver_information.max_decoded_frame_size = max_dec;
+    } else if (which == ToTransmitter_error_tag) {
+        m.message.error.audio_underflow = underflow != 0;
+        m.message.error.audio_decode_error = decode_error != 0;
+    }
+    pb_ostream_t os = pb_ostream_from_buffer(out, cap);
+    if (!pb_encode_delimited(&os, ToTransmitter_fields, &m)) return -1;
+    return (int)os.bytes_written;
+}
+
+/* pb_decode_delimited of one ToTransmitter. Returns 0 / -1. */
+int ref_decode_to_transmitter(const uint8_t *in, size_t len, int32_t *which, ref_disc *d,
+                              uint32_t *max_enc, uint32_t *max_dec, int32_t *underflow,
+                              int32_t *decode_error, size_t *consumed)
+{
+    ToTransmitter m = ToTransmitter_init_zero;
+    pb_istream_t is = pb_istream_from_buffer(in, len);
+    bool ok = pb_decode_delimited(&is, ToTransmitter_fields, &m);
+    *consumed = len - is.bytes_left;
+    if (!ok) return -1;
+    *which = m.which_message;
+    if (m.which_message == ToTransmitter_receiver_information_tag) {
+        disc_from_pb(&m.message.receiver_information.discovery_data, d);
+        *max_enc = m.message.receiver_information.max_encoded_frame_size;
+        *max_dec = m.message.receiver_information.max_decoded_frame_size;
+    } else if (m.which_message == ToTransmitter_error_tag) {
+        *underflow = m.message.error.audio_underflow;
+        *decode_error = m.message.error.audio_decode_error;
+    }
     return 0;
 }

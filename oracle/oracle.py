@@ -234,6 +234,111 @@ def ref_decode(buf: bytes):
     return rc, bytes(out[:pl.value]), int(used.value)
 
 
+class RefDisc(ctypes.Structure):
+    """ref_disc of nanopb_ref_harness.c: a flat DiscoveryResponse (ip.pb.h:17-24)."""
+    _fields_ = [("protocol_version", ctypes.c_uint32), ("mac_address", ctypes.c_uint64),
+                ("device_name", ctypes.c_char * 128), ("currently_streaming", ctypes.c_int32),
+                ("opus_version", ctypes.c_char * 128)]
+
+
+def _ref_session():
+    R = ref_nanopb()
+    if R is not None and not getattr(R, "_session_bound", False):
+        R.ref_encode_broadcast.argtypes = [ctypes.c_int, ctypes.c_uint32, ctypes.c_int,
+                                           ctypes.POINTER(RefDisc), _P, _SZ]
+        R.ref_encode_broadcast.restype = ctypes.c_int
+        R.ref_decode_broadcast.argtypes = [_P, _SZ, ctypes.POINTER(ctypes.c_uint32),
+                                           ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(RefDisc)]
+        R.ref_decode_broadcast.restype = ctypes.c_int
+        R.ref_encode_to_transmitter.argtypes = [ctypes.c_int, ctypes.POINTER(RefDisc),
+                                                ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int,
+                                                ctypes.c_int, _P, _SZ]
+        R.ref_encode_to_transmitter.restype = ctypes.c_int
+        u32p, i32p = ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_int32)
+        R.ref_decode_to_transmitter.argtypes = [_P, _SZ, i32p, ctypes.POINTER(RefDisc), u32p, u32p,
+                                                i32p, i32p, ctypes.POINTER(_SZ)]
+        R.ref_decode_to_transmitter.restype = ctypes.c_int
+        R._session_bound = True
+    return R
+
+
+def _ref_disc(d: dict) -> RefDisc:
+    r = RefDisc()
+    r.protocol_version = d.get("protocol_version", 0)
+    r.mac_address = d.get("mac_address", 0)
+    r.device_name = d.get("device_name", b"")
+    r.currently_streaming = int(bool(d.get("currently_streaming", False)))
+    r.opus_version = d.get("opus_version", b"")
+    return r
+
+
+def _disc_dict(r: RefDisc) -> dict:
+    return {"protocol_version": int(r.protocol_version), "mac_address": int(r.mac_address),
+            "device_name": bytes(r.device_name), "currently_streaming": bool(r.currently_streaming),
+            "opus_version": bytes(r.opus_version)}
+
+
+def ref_broadcast_encode(which: int, magic: int, req: bool = True, d: Optional[dict] = None):
+    """Reference nanopb pb_encode of a BroadcastMessage (network.cpp:486-492)."""
+    R = _ref_session()
+    out = (ctypes.c_uint8 * 1024)()
+    rd = _ref_disc(d or {})
+    n = R.ref_encode_broadcast(which, magic, int(req), ctypes.byref(rd), out, 1024)
+    if n < 0:
+        raise ValueError("nanopb encode failed")
+    return bytes(out[:n])
+
+
+def ref_broadcast_decode(buf: bytes):
+    """Reference pb_decode of one datagram -> (rc, which, magic, discovery dict or None)."""
+    R = _ref_session()
+    src = (ctypes.c_uint8 * max(len(buf), 1)).from_buffer_copy(buf or b"\0")
+    magic, which, rd = ctypes.c_uint32(), ctypes.c_int32(), RefDisc()
+    rc = R.ref_decode_broadcast(src, len(buf), ctypes.byref(magic), ctypes.byref(which),
+                                ctypes.byref(rd))
+    if rc:
+        return rc, None, None, None
+    return 0, int(which.value), int(magic.value), (_disc_dict(rd) if which.value == 3 else None)
+
+
+def ref_to_transmitter_encode(which: int, info: Optional[dict] = None, underflow=False,
+                              decode_error=False) -> bytes:
+    """Reference pb_encode_delimited of a ToTransmitter (network.cpp:388-403)."""
+    R = _ref_session()
+    info = info or {}
+    rd = _ref_disc(info.get("discovery_data", {}))
+    out = (ctypes.c_uint8 * 1024)()
+    n = R.ref_encode_to_transmitter(which, ctypes.byref(rd), info.get("max_encoded_frame_size", 0),
+                                    info.get("max_decoded_frame_size", 0), int(underflow),
+                                    int(decode_error), out, 1024)
+    if n < 0:
+        raise ValueError("nanopb encode failed")
+    return bytes(out[:n])
+
+
+def ref_to_transmitter_decode(buf: bytes):
+    """Reference pb_decode_delimited -> (rc, which, fields dict or None, consumed)."""
+    R = _ref_session()
+    src = (ctypes.c_uint8 * max(len(buf), 1)).from_buffer_copy(buf or b"\0")
+    which, rd = ctypes.c_int32(), RefDisc()
+    me, md = ctypes.c_uint32(), ctypes.c_uint32()
+    uf, de = ctypes.c_int32(), ctypes.c_int32()
+    used = _SZ()
+    rc = R.ref_decode_to_transmitter(src, len(buf), ctypes.byref(which), ctypes.byref(rd),
+                                     ctypes.byref(me), ctypes.byref(md), ctypes.byref(uf),
+                                     ctypes.byref(de), ctypes.byref(used))
+    if rc:
+        return rc, None, None, int(used.value)
+    if which.value == 1:
+        f = {"discovery_data": _disc_dict(rd), "max_encoded_frame_size": int(me.value),
+             "max_decoded_frame_size": int(md.value)}
+    elif which.value == 2:
+        f = {"audio_underflow": bool(uf.value), "audio_decode_error": bool(de.value)}
+    else:
+        f = None
+    return 0, int(which.value), f, int(used.value)
+
+
 # ---- reference FFT (libopus opus_fft_c, oracle/_ref, built by ref.mk) --------
 _ref_kf = None
 

@@ -79,3 +79,90 @@ def test_stereo_pcm_to_frames(A, O, fskrx, mode, k):
     assert got.size == W and ref.size == W
     assert np.array_equal(got, ref)
     assert b"333 samples pending" in r.stderr
+
+
+def test_network_usage_errors(fskrx):
+    # discovery or -1 without a TCP listener, and a device name over 127 bytes
+    assert subprocess.run([fskrx, "-u", "0"], capture_output=True).returncode == 2
+    assert subprocess.run([fskrx, "-1"], capture_output=True).returncode == 2
+    assert subprocess.run([fskrx, "-l", "0", "-N", "x" * 128], capture_output=True).returncode == 2
+
+
+def _start_listener(fskrx, *args):
+    import re
+    p = subprocess.Popen([fskrx, "-l", "0", "-u", "0", "-a", "127.0.0.1", "-1", *args],
+                         stdout=subprocess.PIPE, stderr=subprocess.PIPE)
+    line = p.stderr.readline().decode()
+    m = re.search(r"listening tcp (\d+) udp (\d+)", line)
+    assert m, line
+    return p, int(m.group(1)), int(m.group(2))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("channels", [1, 2])
+def test_network_receiver_session(A, O, fskrx, channels):
+    """fskrx -l: UDP discovery answer (network.cpp:473-492), the ToTransmitter
+    hello on connect (network.cpp:380-403), then AudioData frames of PCM ->
+    symbol frames on stdout equal to the oracle's; a frame nanopb rejects ends
+    the stream (network.cpp:411-421)."""
+    import socket
+    if not _gpu_visible():
+        pytest.skip("no GPU visible")
+    freqs = A.FSK2_FREQS
+    W = 600
+    pcm, _ = O.synth_fsk(freqs, 1024, W, 91 + channels, 8000, 400)
+    mono = np.concatenate([pcm.reshape(-1), pcm.reshape(-1)[:100]])
+    if channels == 2:
+        inter = np.empty(2 * mono.size, np.int16)
+        inter[0::2] = mono
+        inter[1::2] = np.random.default_rng(3).integers(-900, 900, mono.size).astype(np.int16)
+    else:
+        inter = mono
+    p, tport, uport = _start_listener(fskrx, "-c", str(channels), "-m", "left", "-N", "bench-rx")
+    try:
+        u = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+        u.settimeout(0.5)
+        u.sendto(bytes.fromhex("08c5c0f6e2021001"), ("127.0.0.1", uport))   # wrong magic
+        u.sendto(A.broadcast_request_encode(), ("127.0.0.1", uport))
+        which, magic, d = A.broadcast_decode(u.recvfrom(1024)[0])
+        assert (which, magic) == (A.DEMOD_MSG_DISCOVERY_RESPONSE, A.DEMOD_BROADCAST_MAGIC)
+        assert d["device_name"] == b"bench-rx" and d["protocol_version"] == 1
+        assert d["opus_version"] == A.version_string().encode() and not d["currently_streaming"]
+        with pytest.raises(socket.timeout):
+            u.recvfrom(1024)                     # the wrong-magic datagram got no answer
+        t = socket.create_connection(("127.0.0.1", tport), timeout=30)
+        hello = b""
+        while True:
+            hello += t.recv(4096)
+            try:
+                which, info, used = A.to_transmitter_decode(hello)
+                break
+            except A.DemodError as e:
+                assert e.code == A.DEMOD_BUFFER_TOO_SMALL
+        assert which == A.DEMOD_MSG_RECEIVER_INFORMATION and used == len(hello)
+        assert info["max_encoded_frame_size"] == 4096 and info["max_decoded_frame_size"] == 11520
+        # while streaming, discovery reports it
+        u.sendto(A.broadcast_request_encode(), ("127.0.0.1", uport))
+        assert A.broadcast_decode(u.recvfrom(1024)[0])[2]["currently_streaming"]
+        raw = inter.astype("<i2").tobytes()
+        rng = np.random.default_rng(channels)
+        off, wire = 0, b""
+        while off < len(raw):                    # ragged payloads, samples split across frames
+            n = int(rng.integers(1, 4097))
+            wire += A.frame_encode(raw[off:off + n])
+            off += n
+        for i in range(0, len(wire), 1500):      # TCP segments that cut frames
+            t.sendall(wire[i:i + 1500])
+        t.sendall(bytes.fromhex("05") + b"\x0a\x03\x08\x01\x00")  # AudioData without bytes
+        out, err = p.communicate(timeout=60)
+        t.close()
+        u.close()
+    finally:
+        if p.poll() is None:
+            p.kill()
+            p.wait()
+    assert p.returncode == 0, err.decode()
+    assert b"bad frame" in err and b"1 transmitter(s) served" in err
+    got = _symbols(A, out, W, 1)
+    ref, _ = O.goertzel(mono, freqs, 1024)
+    assert got.size == W and np.array_equal(got, ref)
