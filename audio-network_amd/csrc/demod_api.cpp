@@ -31,6 +31,8 @@ struct demod {
     float *d_tw1024 = nullptr;
     int *d_bins = nullptr;
     float coef[kMaxTones] = {};
+    float sgn[kMaxTones] = {};  // plain detector, Reinsch form: sign of cos(w_k)
+    bool reinsch = false;       // plain detector: Reinsch-modified recurrence
     int zcls[kMaxTones] = {};   // residue detector: class each tone reads
     // staging for host-pointer calls
     int16_t *d_in = nullptr;
@@ -195,12 +197,30 @@ static int init_device_state(demod_t *st)
     //             complex s_c = (alpha lo + beta hi) + i gamma hi, folded into
     //             X = lo1 C1 + hi1 C2 + lo2 C3 + hi2 C4 (residue.hip):
     //             C1 = alpha A, C2 = beta A + gamma iA, C3 = -alpha B, C4 = -(beta B + gamma iB)
+    //   Plain bank, Reinsch form (goertzel.hip RS; plans with a tone where
+    //             |sin w| < kReinschSin): coefficient lambda = 2cos w - 2 sgn,
+    //             state (s, d); X += (A - sgn B) s + sgn B d, stored as
+    //             {C1, -C2} so the kernel's A s1 - B s2 form is unchanged.
+    //             fp32 emulation of 64-sample chains: the 2cos(w) form reaches
+    //             4-8e-5 of P at |sin w| ~ 0.01 and ~5e-6 at 0.05-0.08; the
+    //             Reinsch form stays below 1e-6 at every bin.
     const bool residue = st->detector == kDetResidue;
     const double span = (st->detector == kDetFolded || residue) ? 8.0 : 64.0;
+    constexpr double kReinschSin = 0.1;
+    st->reinsch = false;
+    if (st->detector == kDetGoertzel)
+        for (uint32_t k = 0; k < c.k; ++k)
+            if (std::fabs(std::sin(2.0 * M_PI * c.freqs[k] / c.fs)) < kReinschSin) st->reinsch = true;
     std::vector<float4> rot((size_t)c.k * g * (residue ? 2 : 1));
     for (uint32_t k = 0; k < c.k; ++k) {
         const double w = 2.0 * M_PI * c.freqs[k] / c.fs;
+        const double sg = std::cos(w) >= 0.0 ? 1.0 : -1.0;
+        st->sgn[k] = (float)sg;
         st->coef[k] = (float)(2.0 * std::cos(w));
+        if (st->reinsch) {
+            const double h = std::sin(0.5 * w), q = std::cos(0.5 * w);
+            st->coef[k] = (float)(sg > 0 ? -4.0 * h * h : 4.0 * q * q);
+        }
         // residue rho = bin mod 8 -> (class, alpha, beta, gamma); rho and 8 - rho
         // share a class (conjugates), class 0 carries (Z0, Z4)
         static const int kCls[8] = {0, 1, 3, 2, 0, 2, 3, 1};
@@ -211,6 +231,12 @@ static int init_device_state(demod_t *st)
         for (int j = 0; j < g; ++j) {
             const double a = -w * (span * j + span - 1.0), b = -w * (span * j + span);
             const double Ar = std::cos(a), Ai = std::sin(a), Br = std::cos(b), Bi = std::sin(b);
+            if (!residue && st->reinsch) {
+                const double C1r = Ar - sg * Br, C1i = Ai - sg * Bi;
+                rot[(size_t)k * g + j] = make_float4((float)C1r, (float)C1i, (float)(-sg * Br),
+                                                     (float)(-sg * Bi));
+                continue;
+            }
             if (!residue) {
                 rot[(size_t)k * g + j] = make_float4((float)Ar, (float)Ai, (float)Br, (float)Bi);
                 continue;
@@ -359,8 +385,10 @@ static int enqueue_batch(demod_t *st, const int16_t *d_pcm, size_t n_windows, ui
     p.mag = d_mag;
     for (uint32_t k = 0; k < st->cfg.k; ++k) {
         p.coef[k] = st->coef[k];
+        p.sgn[k] = st->sgn[k];
         p.zcls[k] = st->zcls[k];
     }
+    p.reinsch = st->reinsch ? 1 : 0;
     HIP_TRY(launch_detector(st->detector, p, s));
     return (int)n_windows;
 }

@@ -28,7 +28,9 @@ struct GoertzelParams {
     const float4 *rot;       // [k][g] {Ar, Ai, Br, Bi} rotation of each lane segment
     uint8_t *sym;            // [n_windows]
     float *mag;              // [n_windows][k] or nullptr
-    float coef[kMaxTones];   // 2 cos(w_k)
+    float coef[kMaxTones];   // 2 cos(w_k); reinsch: lambda_k = 2 cos(w_k) - 2 sgn_k
+    float sgn[kMaxTones];    // reinsch: sign of cos(w_k) (+1 / -1)
+    int reinsch;             // goertzel.hip: Reinsch-modified recurrence (tones near 0 / fs/2)
     int zcls[kMaxTones];     // residue.hip: residue class (0..3) tone k reads
     int xcd_swizzle;         // 1: blocks b, b+8, b+16.. (one XCD) take adjacent tiles
 };

@@ -64,9 +64,18 @@ __device__ __forceinline__ float group_sum(float v, int log2g)
 //           whole chain after another: issue-stall bound at large K).
 //   WS      window_sum.h epilogue (reduce-scatter, packed-key argmax, one
 //           coalesced magnitude store) at n = 1024.
+//   RS      Reinsch-modified recurrence for tone plans with a tone near 0 or
+//           fs/2, where the fp32 coefficient 2cos(w) cannot resolve w (a tone
+//           at bin 3 of 1024 misses the 1e-5 bar by 4x). With sgn = sign(cos w),
+//           lambda = 2cos(w) - 2 sgn = -4 sin^2(w/2) or 4 cos^2(w/2) (full
+//           relative precision) and d[n] = s[n] - sgn s[n-1]:
+//             d[n] = x[n] + lambda s[n-1] + sgn d[n-1],  s[n] = sgn s[n-1] + d[n]
+//           (3 ops per sample-tone instead of 2). The kernel keeps s in s1 and
+//           d in s2; the host folds s2 = sgn (s1 - d) into the rotation
+//           constants: X += (A - sgn B) s1 + sgn B d.
 template <int K, int LOG2G, int PF = 1, bool NT = true, int WPB = kWavesPerBlock,
           bool DIRECT = false, bool NTS = false, bool PK = false, bool SB = false,
-          bool WS = false>
+          bool WS = false, bool RS = false>
 __global__ __launch_bounds__(64 * WPB) void goertzel_tile_kernel(GoertzelParams p)
 {
     static_assert(PF == 1 || PF == 2, "prefetch depth");
@@ -144,15 +153,19 @@ __global__ __launch_bounds__(64 * WPB) void goertzel_tile_kernel(GoertzelParams 
             // tone pairs in packed fp32 (v_pk_add_f32 + v_pk_fma_f32 per sample
             // per pair); an odd last tone runs as a scalar chain
             constexpr int H = K / 2;
-            f32x2 c2[H], a1[H], a2[H];
-            float cs = 0.f, b1 = 0.f, b2 = 0.f;
+            f32x2 c2[H], sg2[H], a1[H], a2[H];
+            float cs = 0.f, ss = 0.f, b1 = 0.f, b2 = 0.f;
 #pragma unroll
             for (int h = 0; h < H; ++h) {
                 c2[h] = f32x2{p.coef[2 * h], p.coef[2 * h + 1]};
+                if (RS) sg2[h] = f32x2{p.sgn[2 * h], p.sgn[2 * h + 1]};
                 a1[h] = f32x2{0.f, 0.f};
                 a2[h] = f32x2{0.f, 0.f};
             }
-            if (K & 1) cs = p.coef[K - 1];
+            if (K & 1) {
+                cs = p.coef[K - 1];
+                if (RS) ss = p.sgn[K - 1];
+            }
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const u32x4 sj = DIRECT ? cur[j] : *reinterpret_cast<const u32x4 *>(wl + rd_off + j * 16);
@@ -164,14 +177,27 @@ __global__ __launch_bounds__(64 * WPB) void goertzel_tile_kernel(GoertzelParams 
                     const f32x2 xx = f32x2{x, x};
 #pragma unroll
                     for (int h = 0; h < H; ++h) {
-                        const f32x2 a = __builtin_elementwise_fma(c2[h], a1[h], xx - a2[h]);
-                        a2[h] = a1[h];
-                        a1[h] = a;
+                        if constexpr (RS) {  // a1 = s, a2 = d
+                            const f32x2 d = __builtin_elementwise_fma(
+                                c2[h], a1[h], __builtin_elementwise_fma(sg2[h], a2[h], xx));
+                            a1[h] = __builtin_elementwise_fma(sg2[h], a1[h], d);
+                            a2[h] = d;
+                        } else {
+                            const f32x2 a = __builtin_elementwise_fma(c2[h], a1[h], xx - a2[h]);
+                            a2[h] = a1[h];
+                            a1[h] = a;
+                        }
                     }
                     if (K & 1) {
-                        const float a = fmaf(cs, b1, x - b2);
-                        b2 = b1;
-                        b1 = a;
+                        if constexpr (RS) {
+                            const float d = fmaf(cs, b1, fmaf(ss, b2, x));
+                            b1 = fmaf(ss, b1, d);
+                            b2 = d;
+                        } else {
+                            const float a = fmaf(cs, b1, x - b2);
+                            b2 = b1;
+                            b1 = a;
+                        }
                     }
                     if (SB) __builtin_amdgcn_sched_barrier(0);
                 }
@@ -198,16 +224,20 @@ __global__ __launch_bounds__(64 * WPB) void goertzel_tile_kernel(GoertzelParams 
                 const float x0 = (float)(int)(short)(d & 0xFFFFu);
                 const float x1 = (float)((int)d >> 16);
 #pragma unroll
-                for (int k = 0; k < K; ++k) {
-                    const float a = fmaf(p.coef[k], s1[k], x0 - s2[k]);
-                    s2[k] = s1[k];
-                    s1[k] = a;
-                }
+                for (int h = 0; h < 2; ++h) {
+                    const float x = h ? x1 : x0;
 #pragma unroll
-                for (int k = 0; k < K; ++k) {
-                    const float a = fmaf(p.coef[k], s1[k], x1 - s2[k]);
-                    s2[k] = s1[k];
-                    s1[k] = a;
+                    for (int k = 0; k < K; ++k) {
+                        if constexpr (RS) {  // s1 = s, s2 = d
+                            const float dd = fmaf(p.coef[k], s1[k], fmaf(p.sgn[k], s2[k], x));
+                            s1[k] = fmaf(p.sgn[k], s1[k], dd);
+                            s2[k] = dd;
+                        } else {
+                            const float a = fmaf(p.coef[k], s1[k], x - s2[k]);
+                            s2[k] = s1[k];
+                            s1[k] = a;
+                        }
+                    }
                 }
                 if (SB) __builtin_amdgcn_sched_barrier(0);
             }
@@ -268,21 +298,30 @@ __global__ __launch_bounds__(64 * WPB) void goertzel_tile_kernel(GoertzelParams 
 // K = 8: 657 -> 506 us on 2^20 windows; K = 2 is HBM-bound either way) and the
 // window_sum.h epilogue for K >= 3 (K = 8: 484 -> 456 us; neutral at K <= 4,
 // profiles/round1/probe_window_sum.log).
+// RS (Reinsch form) only for plans with a tone near 0 or fs/2 (the host's
+// kReinschSin test): elsewhere the plain form is within the bar at 2 ops.
 template <int K>
-static const void *kernel_for(int log2g)
+static const void *kernel_for(int log2g, bool rs)
 {
     constexpr bool PK = K >= 3;
     if (log2g == 4)
-        return reinterpret_cast<const void *>(
-            &goertzel_tile_kernel<K, 4, 1, true, kPlainWPB, false, false, PK, false, K >= 3>);
-    return reinterpret_cast<const void *>(
-        &goertzel_tile_kernel<K, -1, 1, true, kPlainWPB, false, false, PK>);
+        return rs ? reinterpret_cast<const void *>(
+                        &goertzel_tile_kernel<K, 4, 1, true, kPlainWPB, false, false, PK, false,
+                                              K >= 3, true>)
+                  : reinterpret_cast<const void *>(
+                        &goertzel_tile_kernel<K, 4, 1, true, kPlainWPB, false, false, PK, false,
+                                              K >= 3>);
+    return rs ? reinterpret_cast<const void *>(
+                    &goertzel_tile_kernel<K, -1, 1, true, kPlainWPB, false, false, PK, false,
+                                          false, true>)
+              : reinterpret_cast<const void *>(
+                    &goertzel_tile_kernel<K, -1, 1, true, kPlainWPB, false, false, PK>);
 }
 
-static const void *kernel_ptr(int k, int log2g)
+static const void *kernel_ptr(int k, int log2g, bool rs)
 {
     switch (k) {
-#define FSKD_CASE(K) case K: return kernel_for<K>(log2g);
+#define FSKD_CASE(K) case K: return kernel_for<K>(log2g, rs);
         FSKD_CASE(1) FSKD_CASE(2) FSKD_CASE(3) FSKD_CASE(4)
         FSKD_CASE(5) FSKD_CASE(6) FSKD_CASE(7) FSKD_CASE(8)
         FSKD_CASE(9) FSKD_CASE(10) FSKD_CASE(11) FSKD_CASE(12)
@@ -311,7 +350,7 @@ hipError_t launch_detector(int detector, const GoertzelParams &p, hipStream_t s)
 {
     const void *f = detector == kDetFolded    ? fold_kernel_ptr(p.k, p.log2g)
                   : detector == kDetResidue ? residue_kernel_ptr(p.k, p.log2g)
-                                            : kernel_ptr(p.k, p.log2g);
+                                            : kernel_ptr(p.k, p.log2g, p.reinsch != 0);
     if (!f) return hipErrorInvalidValue;
     const size_t lds = detector == kDetResidue ? residue_lds_bytes(p.k, p.log2g) : 0;
     const int wpb = detector == kDetResidue ? kWavesPerBlock : kPlainWPB;
