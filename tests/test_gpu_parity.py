@@ -47,7 +47,7 @@ def run_case(A, O, freqs, n=1024, W=257, hop=None, seed=1, amplitude=8000, sigma
     return err
 
 
-GOERTZEL, FOLDED, RESIDUE = 1, 3, 4
+GOERTZEL, FFT, FOLDED, RESIDUE = 1, 2, 3, 4
 # 8-FSK on integer bins 32 + 9 i (46.875 Hz spacing): bins 32..95 hit every
 # residue class mod 8, so only the residue detector folds this plan
 FSK8_ODD = tuple(46.875 * (32 + 9 * i) for i in range(8))
@@ -158,6 +158,20 @@ def test_edge_frequencies(A, O, torch, n, method):
         run_case(A, O, freqs, n=n, W=200, seed=n + amp, amplitude=amp, sigma=sigma,
                  method=method, check_truth=False)
     run_case(A, O, freqs, n=n, W=60, hop=max(8, n // 4), seed=n + 1, method=method)
+
+
+@pytest.mark.parametrize("method", [GOERTZEL, FFT])
+def test_dc_and_nyquist_tones(A, O, torch, method):
+    """Tones exactly at 0 Hz and fs/2 (the ABI accepts [0, fs/2]): lambda = 0
+    with sgn = +1 / -1 in the Reinsch form, bins 0 and 512 in the FFT's
+    pair-slot layout."""
+    freqs = (0.0, 1500.0, 24000.0, 3000.0)
+    pcm, _ = O.synth_fsk(freqs, 1024, 300, 42, 8000, 400)
+    with A.Demodulator(freqs=freqs, method=method) as d:
+        sym, mag = d.batch(pcm, mags=True)
+    ref_sym, ref_P = (O.fft_demod if method == FFT else O.goertzel)(pcm, freqs, 1024)
+    assert (sym == ref_sym).all()
+    assert rel_err(mag, ref_P) <= MAG_TOL
 
 
 @pytest.mark.parametrize("n", [256, 1024, 4096])
@@ -414,7 +428,6 @@ def test_golden_stereo_stream_on_gpu(A, torch):
 
 
 # ---- full-spectrum FFT detector (config 4) ---------------------------------
-FFT = 2
 
 
 def _spec_err(spec, ref):
