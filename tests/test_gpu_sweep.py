@@ -4,8 +4,9 @@ so combinations the hand-picked cases of test_gpu_parity.py do not list are
 still covered (every detector behind the same C ABI, demod_batch).
 
 Bar as in test_gpu_parity.py: |X_k|^2 within 1e-5 of the window's max_k P_ref
-(double oracle), symbols bit-exact wherever the oracle's decision is not a tie
-inside that tolerance (hop < n windows straddle two symbols, and two tones can
+(double oracle; of its spectral energy where that is larger, mag_denom),
+symbols bit-exact wherever the oracle's decision is not a tie inside that
+tolerance (hop < n windows straddle two symbols, and two tones can
 then carry near-equal power); such ties must stay rare.
 """
 import numpy as np
@@ -15,7 +16,22 @@ pytestmark = pytest.mark.gpu
 
 MAG_TOL = 1e-5
 FS = 48000.0
-N_CASES = 48
+N_CASES = 120
+
+
+def mag_denom(P, mono, n, hop):
+    """Per-window normaliser of |P_gpu - P_ref|: max_k P_ref, or the window's
+    spectral energy n * sum(x^2) / 2 when that is larger (equal to max_k P for
+    a clean tone). The fp32 error scales with the window's energy, not with the
+    tone powers: where hop < n splices two symbols with unrelated phases, a
+    single tone (K = 1) can cancel to far below the energy, and 1e-5 of that P
+    is below fp32 resolution (as for the degenerate windows of
+    test_gpu_parity.py::test_zero_and_extreme_input)."""
+    x = mono.astype(np.float64)
+    c2 = np.concatenate([[0.0], np.cumsum(x * x)])
+    starts = np.arange(P.shape[0]) * hop
+    energy = n * (c2[starts + n] - c2[starts]) / 2
+    return np.maximum(np.maximum(P.max(axis=1), energy), 1e-30)
 
 
 @pytest.fixture(scope="module")
@@ -76,14 +92,73 @@ def test_random_case(A, O, torch, i):
     else:
         ref_sym, ref_P = O.goertzel(flat, freqs, n, hop, Wh)
     assert sym.shape == ref_sym.shape and mag.shape == ref_P.shape
-    denom = np.maximum(ref_P.max(axis=1), 1e-30)
+    denom = mag_denom(ref_P, flat, n, hop)
     err = (np.abs(mag.astype(np.float64) - ref_P).max(axis=1) / denom).max()
     assert err <= MAG_TOL, (err, c)
     Ps = np.sort(ref_P, axis=1)
     posed = (Ps[:, -1] - Ps[:, -2]) / denom > 4 * MAG_TOL if ref_P.shape[1] > 1 \
         else np.ones(Wh, bool)
     # windows inside one symbol have one clear winner; windows straddling two
-    # symbols (hop not a multiple of n) can split the power evenly
-    assert posed.mean() >= (0.99 if hop % n == 0 else 0.9), c
+    # symbols (hop not a multiple of n) split the power between two tones, and
+    # evenly (a structural tie) wherever a window starts half a symbol in:
+    # every 8th window at n = 1024, hop = 384
+    assert posed.mean() >= (0.99 if hop % n == 0 else 0.75), c
     bad = np.flatnonzero(posed & (sym != ref_sym))
+    assert bad.size == 0, (bad[:8], c)
+
+
+N_STREAM_CASES = 40
+
+
+@pytest.mark.parametrize("i", range(N_STREAM_CASES))
+def test_random_stream(A, O, torch, i):
+    """Streaming demodulate(pcm, n) with random ragged packets: mono or
+    stereo (left, right or (L+R)>>1), any detector, hop <= n, against the
+    oracle's streaming restatement (oracle.Stream): same symbols, same pending
+    count after every call, magnitudes within the bar."""
+    c = draw_case(100 + i)
+    rng = np.random.default_rng(0xABC + i)
+    m = {"auto": A.METHOD_AUTO, "goertzel": A.METHOD_GOERTZEL, "folded": A.METHOD_FOLDED,
+         "residue": A.METHOD_RESIDUE, "fft": A.METHOD_FFT}[c["method"]]
+    n, hop, freqs = c["n"], c["hop"], c["freqs"]
+    W = min(c["W"], 120)
+    channels = int(rng.integers(1, 3))
+    mode = int(rng.integers(0, 3)) if channels == 2 else 0
+    Lc, _ = O.synth_fsk(freqs, n, W, c["seed"], c["amplitude"], c["sigma"])
+    if channels == 1:
+        stream = Lc.reshape(-1)
+    else:
+        Rc, _ = O.synth_fsk(freqs, n, W, c["seed"] + 1, c["amplitude"], c["sigma"])
+        stream = np.stack([Lc.reshape(-1), Rc.reshape(-1)], axis=1).reshape(-1)
+    ref = O.Stream(freqs, n=n, hop=hop, channels=channels, channel_mode=mode)
+    got_s, got_m, want_s, want_P = [], [], [], []
+    total = stream.size // channels
+    with A.Demodulator(n=n, hop=hop, freqs=freqs, method=m, channels=channels,
+                       channel_mode=mode) as d:
+        pos = 0
+        while pos < total:
+            fr = int(rng.choice([0, 1, 7, 2880, int(rng.integers(1, 3 * n))]))
+            chunk = stream[pos * channels:(pos + fr) * channels]
+            pos += fr
+            s, mg = d.demodulate(chunk, mags=True)
+            rs, rP = ref.push(chunk)
+            got_s.append(s), got_m.append(mg), want_s.append(rs), want_P.append(rP)
+            assert d.pending() == ref.pending(), c
+    gs, ws = np.concatenate(got_s), np.concatenate(want_s)
+    gm, wP = np.concatenate(got_m), np.concatenate(want_P)
+    assert gs.size == ws.size == (total - n) // hop + 1, c
+    # oracle.Stream evaluates the Goertzel bank; for the FFT detector that is
+    # the same |X_k|^2, since FFT draws put every tone on an integer bin
+    if channels == 1:
+        mono = stream
+    else:
+        lr = stream.reshape(-1, 2).astype(np.int32)
+        mono = (lr[:, 0], lr[:, 1], (lr[:, 0] + lr[:, 1]) >> 1)[mode]
+    denom = mag_denom(wP, mono, n, hop)
+    err = (np.abs(gm.astype(np.float64) - wP).max(axis=1) / denom).max()
+    assert err <= MAG_TOL, (err, c)
+    Ps = np.sort(wP, axis=1)
+    posed = (Ps[:, -1] - Ps[:, -2]) / denom > 4 * MAG_TOL if wP.shape[1] > 1 \
+        else np.ones(gs.size, bool)
+    bad = np.flatnonzero(posed & (gs != ws))
     assert bad.size == 0, (bad[:8], c)
