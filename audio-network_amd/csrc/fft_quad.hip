@@ -343,7 +343,19 @@ static_assert(4 * kQPow <= 2 * kQSlab, "bin powers of 4 windows must fit the sla
 // FUSE: step 3 as one asm block per two pairs (post_pair2) instead of the
 // cmul2 / pwr2 pieces: 23 -> 8 hazard nops but 142 -> 160 VGPRs, and the same
 // time (interleaved A/B, profiles/round1/probe_fft_fuse.log), so off.
-template <int WPB = 4, int MINW = 0, bool SPLIT = false, bool FUSE = false>
+// FMT: load z[t + 16 n1] with a typed buffer load (DATA_FORMAT 16_16,
+// NUM_FORMAT SSCALED): the texture path converts both int16 halves to fp32,
+// replacing the 64 VALU converts per group (exact for every int16).
+namespace quad {
+typedef int i4 __attribute__((ext_vector_type(4)));
+__device__ f2 raw_buffer_load_format_v2f32(i4 rsrc, int voffset, int soffset, int aux)
+    __asm("llvm.amdgcn.raw.buffer.load.format.v2f32");
+// buffer descriptor word 3: DST_SEL x,y,z,w = 4,5,6,7; NUM_FORMAT 3 (SSCALED);
+// DATA_FORMAT 5 (16_16)
+constexpr int kFmtWord3 = 0xFAC | (3 << 12) | (5 << 15);
+}  // namespace quad
+
+template <int WPB = 4, int MINW = 0, bool SPLIT = false, bool FUSE = false, bool FMT = false>
 __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MINW > 0 ? MINW : 1)))
 void fft1024_quad_kernel(FftParams p)
 {
@@ -375,7 +387,8 @@ void fft1024_quad_kernel(FftParams p)
     const long long n_groups = (p.n_windows + 3) >> 2;
     const long long stride = (long long)gridDim.x * WPB;
     long long g = tile_block(p.xcd_swizzle) * WPB + wave;
-    uint32_t nx[32];
+    uint32_t nx[FMT ? 1 : 32];
+    f2 nxf[FMT ? 32 : 1];
     // One buffer descriptor per group (wave-uniform base = its first window);
     // the lane offset is the window's start + 4 t bytes, and z[t + 16 n1] is
     // the immediate offset 64 n1 (< 4 KiB), so the 32 loads need no address
@@ -389,10 +402,19 @@ void fft1024_quad_kernel(FftParams p)
         __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
             (void *)(p.pcm + w0 * p.hop), (short)0, (int)bytes, 0x00020000);
         const int voff = (int)(wq * p.hop * 2) + 4 * t;
+        if constexpr (FMT) {
+            const unsigned long long base = (unsigned long long)(p.pcm + w0 * p.hop);
+            const i4 rf = {(int)(unsigned)base, (int)((base >> 32) & 0xFFFF), (int)bytes, kFmtWord3};
 #pragma unroll
-        for (int n1 = 0; n1 < 32; ++n1)
-            if (half == 2 || ((n1 & 3) < 2) == (half == 0))
-                nx[n1] = __builtin_amdgcn_raw_buffer_load_b32(rs, voff + 64 * n1, 0, 2);
+            for (int n1 = 0; n1 < 32; ++n1)
+                if (half == 2 || ((n1 & 3) < 2) == (half == 0))
+                    nxf[n1] = raw_buffer_load_format_v2f32(rf, voff + 64 * n1, 0, 2);
+        } else {
+#pragma unroll
+            for (int n1 = 0; n1 < 32; ++n1)
+                if (half == 2 || ((n1 & 3) < 2) == (half == 0))
+                    nx[n1] = __builtin_amdgcn_raw_buffer_load_b32(rs, voff + 64 * n1, 0, 2);
+        }
     };
     if (g < n_groups) load_group(g, 2);
     for (; g < n_groups; g += stride) {
@@ -400,7 +422,11 @@ void fft1024_quad_kernel(FftParams p)
         f2 a[32];
 #pragma unroll
         for (int n1 = 0; n1 < 32; ++n1) {
-            a[n1] = (f2){(float)(int)(short)(nx[n1] & 0xFFFFu), (float)((int)nx[n1] >> 16)};
+            if constexpr (FMT) {
+                a[n1] = nxf[n1];
+                continue;
+            }
+            a[n1] = (f2){(float)(int)(short)(nx[FMT ? 0 : n1] & 0xFFFFu), (float)((int)nx[FMT ? 0 : n1] >> 16)};
             // opaque: otherwise the compiler rewrites (float)a + (float)b as
             // (float)(a + b) and the first butterflies become 2 integer ops +
             // 2 converts each instead of one packed add
@@ -522,13 +548,13 @@ void fft1024_quad_kernel(FftParams p)
 
 // Persistent grid: as many blocks as fit the chip, each wave strides over
 // groups of 4 windows (the LDS twiddle tables are built once per block).
-template <int WPB, int MINW, bool SPLIT = false, bool FUSE = false>
+template <int WPB, int MINW, bool SPLIT = false, bool FUSE = false, bool FMT = false>
 hipError_t launch_fft_quad_t(const FftParams &p, hipStream_t s)
 {
     int dev = 0, cus = 256, per_cu = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fft1024_quad_kernel<WPB, MINW, SPLIT, FUSE>,
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fft1024_quad_kernel<WPB, MINW, SPLIT, FUSE, FMT>,
                                                      64 * WPB, 0) != hipSuccess ||
         per_cu < 1)
         per_cu = 1;
@@ -536,7 +562,7 @@ hipError_t launch_fft_quad_t(const FftParams &p, hipStream_t s)
     long long blocks = (groups + WPB - 1) / WPB;
     blocks = std::min<long long>(blocks, (long long)cus * per_cu);
     if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL((fft1024_quad_kernel<WPB, MINW, SPLIT, FUSE>), dim3((unsigned)blocks), dim3(64 * WPB), 0,
+    hipLaunchKernelGGL((fft1024_quad_kernel<WPB, MINW, SPLIT, FUSE, FMT>), dim3((unsigned)blocks), dim3(64 * WPB), 0,
                        s, p);
     return hipGetLastError();
 }

@@ -385,7 +385,7 @@ int main(int argc, char **argv)
         CK(hipMemcpy(d2, t2.data(), 4096, hipMemcpyHostToDevice));
         CK(hipMemcpy(db, hb, 8, hipMemcpyHostToDevice));
         for (int hop : {1024, 256}) {
-            for (int swz : {2, 4, 8, 7, 4, 8}) {
+            for (int swz : {4, 9, 4, 9}) {
                 FftParams fp{};
                 fp.pcm = pcm;
                 fp.hop = hop;
@@ -400,7 +400,8 @@ int main(int argc, char **argv)
                 Variant v;
                 v.name = "fft1024 K=2 hop=" + std::to_string(hop) + " swz=" + std::to_string(swz & 1) +
                          (swz == 2 || swz == 3 ? " QUAD-r1" : swz == 6 ? " QUAD-new-4w" :
-                          swz == 7 ? " QUAD-split" : swz == 8 ? " QUAD-fuse" : " QUAD-new") +
+                          swz == 7 ? " QUAD-split" : swz == 8 ? " QUAD-fuse" :
+                          swz == 9 ? " QUAD-fmt" : " QUAD-new") +
                          " windows=" + std::to_string(fp.n_windows);
                 v.bytes = (double)W * 2048 + fp.n_windows * 9.0;  // stream bytes read once
                 if (hop == 1024) v.sym = fp.sym;  // same windows as the Goertzel K=2 variants
@@ -412,6 +413,8 @@ int main(int argc, char **argv)
                     v.run = [fp](hipStream_t s) { CK((launch_fft_quad_t<4, 0, true>(fp, s))); };
                 else if (swz == 8)
                     v.run = [fp](hipStream_t s) { CK((launch_fft_quad_t<4, 0, false, true>(fp, s))); };
+                else if (swz == 9)
+                    v.run = [fp](hipStream_t s) { CK((launch_fft_quad_t<4, 0, false, false, true>(fp, s))); };
                 else
                     v.run = [fp](hipStream_t s) { CK(launch_fft_quad(fp, s)); };
                 vs.push_back(v);
