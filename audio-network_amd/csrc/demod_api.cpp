@@ -33,6 +33,8 @@ struct demod {
     float coef[kMaxTones] = {};
     float sgn[kMaxTones] = {};  // plain detector, Reinsch form: sign of cos(w_k)
     bool reinsch = false;       // plain detector: Reinsch-modified recurrence
+    bool dcls = false;          // residue detector: compile-time classes, slots permuted
+    unsigned long long perm = 0;  // DCLS: nibble s = tone index of kernel slot s
     int zcls[kMaxTones] = {};   // residue detector: class each tone reads
     // staging for host-pointer calls
     int16_t *d_in = nullptr;
@@ -211,41 +213,66 @@ static int init_device_state(demod_t *st)
     if (st->detector == kDetGoertzel)
         for (uint32_t k = 0; k < c.k; ++k)
             if (std::fabs(std::sin(2.0 * M_PI * c.freqs[k] / c.fs)) < kReinschSin) st->reinsch = true;
+    // residue rho = bin mod 8 -> (class, alpha, beta, gamma); rho and 8 - rho
+    // share a class (conjugates), class 0 carries (Z0, Z4)
+    static const int kCls[8] = {0, 1, 3, 2, 0, 2, 3, 1};
+    static const double kGam[8] = {0, 1, -1, 1, 0, -1, 1, -1};
+    // Residue detector, DCLS (residue.hip): at n = 1024 and K = 8 or 16 with
+    // K / 4 tones in every class (e.g. 8 tones on an odd bin spacing hit every
+    // residue once), kernel tone slot s holds tone slot_tone[s] with
+    // (s / 2) % 4 = its class, so the kernel selects classes at compile time
+    // (no LDS class file); the window_sum epilogue maps slots back (perm).
+    std::vector<uint32_t> slot_tone(c.k);
+    for (uint32_t sl = 0; sl < c.k; ++sl) slot_tone[sl] = sl;
+    st->dcls = false;
+    st->perm = 0;
+    if (residue && st->log2g == 4 && (c.k == 8 || c.k == 16)) {
+        std::vector<uint32_t> by_cls[4];
+        for (uint32_t k = 0; k < c.k; ++k) by_cls[kCls[integer_bin(c, k) % 8]].push_back(k);
+        bool balanced = true;
+        for (int cl = 0; cl < 4; ++cl) balanced = balanced && by_cls[cl].size() == c.k / 4;
+        if (balanced) {
+            size_t next[4] = {0, 0, 0, 0};
+            for (uint32_t sl = 0; sl < c.k; ++sl) {
+                const int cl = (int)((sl / 2) % 4);
+                slot_tone[sl] = by_cls[cl][next[cl]++];
+                st->perm |= (unsigned long long)slot_tone[sl] << (4 * sl);
+            }
+            st->dcls = true;
+        }
+    }
     std::vector<float4> rot((size_t)c.k * g * (residue ? 2 : 1));
-    for (uint32_t k = 0; k < c.k; ++k) {
+    for (uint32_t sl = 0; sl < c.k; ++sl) {
+        const uint32_t k = slot_tone[sl];  // rows below are kernel slots (= tones unless DCLS)
         const double w = 2.0 * M_PI * c.freqs[k] / c.fs;
         const double sg = std::cos(w) >= 0.0 ? 1.0 : -1.0;
-        st->sgn[k] = (float)sg;
-        st->coef[k] = (float)(2.0 * std::cos(w));
+        st->sgn[sl] = (float)sg;
+        st->coef[sl] = (float)(2.0 * std::cos(w));
         if (st->reinsch) {
             const double h = std::sin(0.5 * w), q = std::cos(0.5 * w);
-            st->coef[k] = (float)(sg > 0 ? -4.0 * h * h : 4.0 * q * q);
+            st->coef[sl] = (float)(sg > 0 ? -4.0 * h * h : 4.0 * q * q);
         }
-        // residue rho = bin mod 8 -> (class, alpha, beta, gamma); rho and 8 - rho
-        // share a class (conjugates), class 0 carries (Z0, Z4)
-        static const int kCls[8] = {0, 1, 3, 2, 0, 2, 3, 1};
-        static const double kGam[8] = {0, 1, -1, 1, 0, -1, 1, -1};
         const int rho = residue ? (int)(integer_bin(c, k) % 8) : 0;
         const double al = rho == 4 ? 0.0 : 1.0, be = rho == 4 ? 1.0 : 0.0, ga = kGam[rho];
-        st->zcls[k] = kCls[rho];
+        st->zcls[sl] = kCls[rho];
         for (int j = 0; j < g; ++j) {
             const double a = -w * (span * j + span - 1.0), b = -w * (span * j + span);
             const double Ar = std::cos(a), Ai = std::sin(a), Br = std::cos(b), Bi = std::sin(b);
             if (!residue && st->reinsch) {
                 const double C1r = Ar - sg * Br, C1i = Ai - sg * Bi;
-                rot[(size_t)k * g + j] = make_float4((float)C1r, (float)C1i, (float)(-sg * Br),
-                                                     (float)(-sg * Bi));
+                rot[(size_t)sl * g + j] = make_float4((float)C1r, (float)C1i, (float)(-sg * Br),
+                                                      (float)(-sg * Bi));
                 continue;
             }
             if (!residue) {
-                rot[(size_t)k * g + j] = make_float4((float)Ar, (float)Ai, (float)Br, (float)Bi);
+                rot[(size_t)sl * g + j] = make_float4((float)Ar, (float)Ai, (float)Br, (float)Bi);
                 continue;
             }
             // iA = (-Ai, Ar)
-            rot[((size_t)k * g + j) * 2] =
+            rot[((size_t)sl * g + j) * 2] =
                 make_float4((float)(al * Ar), (float)(al * Ai), (float)(be * Ar - ga * Ai),
                             (float)(be * Ai + ga * Ar));
-            rot[((size_t)k * g + j) * 2 + 1] =
+            rot[((size_t)sl * g + j) * 2 + 1] =
                 make_float4((float)(-al * Br), (float)(-al * Bi), (float)(-(be * Br - ga * Bi)),
                             (float)(-(be * Bi + ga * Br)));
         }
@@ -389,6 +416,8 @@ static int enqueue_batch(demod_t *st, const int16_t *d_pcm, size_t n_windows, ui
         p.zcls[k] = st->zcls[k];
     }
     p.reinsch = st->reinsch ? 1 : 0;
+    p.dcls = st->dcls ? 1 : 0;
+    p.perm = st->perm;
     HIP_TRY(launch_detector(st->detector, p, s));
     return (int)n_windows;
 }

@@ -31,6 +31,8 @@ struct GoertzelParams {
     float coef[kMaxTones];   // 2 cos(w_k); reinsch: lambda_k = 2 cos(w_k) - 2 sgn_k
     float sgn[kMaxTones];    // reinsch: sign of cos(w_k) (+1 / -1)
     int reinsch;             // goertzel.hip: Reinsch-modified recurrence (tones near 0 / fs/2)
+    int dcls;                // residue.hip: tone slot s reads class (s / 2) % 4 from registers
+    unsigned long long perm; // residue.hip DCLS: nibble s = the host's index of tone slot s
     int zcls[kMaxTones];     // residue.hip: residue class (0..3) tone k reads
     int xcd_swizzle;         // 1: blocks b, b+8, b+16.. (one XCD) take adjacent tiles
 };
@@ -95,7 +97,7 @@ constexpr int kDetResidue = 4;   // residue.hip: per-residue-class folding (any 
 
 hipError_t launch_detector(int detector, const GoertzelParams &p, hipStream_t s);
 // residue.hip: rotation table is [k][g][2] float4 {C1, C2}, {C3, C4}
-const void *residue_kernel_ptr(int k, int log2g);
+const void *residue_kernel_ptr(int k, int log2g, bool dcls = false);
 size_t residue_lds_bytes(int k, int log2g, int qp = 2);
 int tile_grid(long long n_windows, int log2g, int wpb = kWavesPerBlock);
 hipError_t launch_synth(const SynthParams &p, hipStream_t s);

@@ -349,7 +349,7 @@ const void *fold_kernel_ptr(int k, int log2g);
 hipError_t launch_detector(int detector, const GoertzelParams &p, hipStream_t s)
 {
     const void *f = detector == kDetFolded    ? fold_kernel_ptr(p.k, p.log2g)
-                  : detector == kDetResidue ? residue_kernel_ptr(p.k, p.log2g)
+                  : detector == kDetResidue ? residue_kernel_ptr(p.k, p.log2g, p.dcls != 0)
                                             : kernel_ptr(p.k, p.log2g, p.reinsch != 0);
     if (!f) return hipErrorInvalidValue;
     const size_t lds = detector == kDetResidue ? residue_lds_bytes(p.k, p.log2g) : 0;

@@ -127,9 +127,13 @@ constexpr int kResidueQP = 2;  // shipped: two sample pairs per LDS round
 //         instruction, as the plain bank does, and regroup it through the
 //         wave's LDS slice (linear chunk q at 16 q; the class pairs reuse the
 //         slice afterwards) instead of the direct per-lane layout.
+//   DCLS  tone slot k reads class (k / 2) % 4 straight from registers (no LDS
+//         class file): for plans the host has permuted so that slot pairs
+//         (2c, 2c + 1) are the two residues of class c (every residue once at
+//         K = 8, e.g. any odd bin spacing).
 template <int K, int LOG2G, int WPB = kWavesPerBlock, bool ASM = true, bool ROTV = false,
           int MINW = (K <= 8 ? 4 : 0), int QP = kResidueQP, bool PF = false, bool WS = true,
-          bool LDST = false>
+          bool LDST = false, bool DCLS = false>
 __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MINW > 0 ? MINW : 1)))
 void residue_tile_kernel(GoertzelParams p)
 {
@@ -244,10 +248,25 @@ void residue_tile_kernel(GoertzelParams p)
                     residue_classes(x[0], c[0][0], c[0][1], c[0][2], c[0][3]);
                     residue_classes(x[1], c[1][0], c[1][1], c[1][2], c[1][3]);
                 }
+                if constexpr (DCLS) {
+#pragma unroll
+                    for (int k = 0; k < K; ++k) {
+                        const int cl = (k / 2) % 4;
+                        const f2 cc = f2{p.coef[k], p.coef[k]};
+                        f2 a = __builtin_elementwise_fma(cc, s1[k], c[0][cl] - s2[k]);
+                        s2[k] = s1[k];
+                        s1[k] = a;
+                        a = __builtin_elementwise_fma(cc, s1[k], c[1][cl] - s2[k]);
+                        s2[k] = s1[k];
+                        s1[k] = a;
+                    }
+                    continue;
+                }
 #pragma unroll
                 for (int cl = 0; cl < 4; ++cl)
                     zw[(cl * QP + qp) * 64] = f4{c[0][cl].x, c[0][cl].y, c[1][cl].x, c[1][cl].y};
             }
+            if (DCLS) continue;
 #pragma unroll
             for (int k = 0; k < K; ++k) {
                 const f4 *zk = zw + p.zcls[k] * (QP * 64);
@@ -279,9 +298,10 @@ void residue_tile_kernel(GoertzelParams p)
         }
         const long long w = wbase + win_in_tile;
         if constexpr (WS && LOG2G == 4) {
-            window_sum_decide<K>(xr, xi, lane, w, w < p.n_windows, p.sym, p.mag);
+            window_sum_decide<K, DCLS>(xr, xi, lane, w, w < p.n_windows, p.sym, p.mag, p.perm);
             continue;
         }
+        static_assert(!DCLS || (WS && LOG2G == 4), "DCLS un-permutes in the window_sum epilogue");
         float best = -1.f;
         int arg = 0;
         float P[K];
@@ -308,17 +328,27 @@ size_t residue_lds_bytes(int k, int log2g, int qp)
     return ((size_t)k * (1u << log2g) * 2 + (size_t)kWavesPerBlock * 4 * qp * 64) * sizeof(f4);
 }
 
+// DCLS (K = 8, 16 at n = 1024, host-permuted plans with K / 4 tones per
+// class): 356-362 -> 312 us at K = 8 on bins 32 + 9i, the box's read ceiling
+// (profiles/round1/probe_dcls.log).
 template <int K>
-static const void *residue_kernel_for(int log2g)
+static const void *residue_kernel_for(int log2g, bool dcls)
 {
-    if (log2g == 4) return reinterpret_cast<const void *>(&residue_tile_kernel<K, 4>);
+    if (log2g == 4) {
+        if constexpr (K == 8 || K == 16)
+            if (dcls)
+                return reinterpret_cast<const void *>(
+                    &residue_tile_kernel<K, 4, kWavesPerBlock, true, false, (K <= 8 ? 4 : 0),
+                                         kResidueQP, false, true, false, true>);
+        return reinterpret_cast<const void *>(&residue_tile_kernel<K, 4>);
+    }
     return reinterpret_cast<const void *>(&residue_tile_kernel<K, -1>);
 }
 
-const void *residue_kernel_ptr(int k, int log2g)
+const void *residue_kernel_ptr(int k, int log2g, bool dcls)
 {
     switch (k) {
-#define FSKD_CASE(K) case K: return residue_kernel_for<K>(log2g);
+#define FSKD_CASE(K) case K: return residue_kernel_for<K>(log2g, dcls);
         FSKD_CASE(1) FSKD_CASE(2) FSKD_CASE(3) FSKD_CASE(4)
         FSKD_CASE(5) FSKD_CASE(6) FSKD_CASE(7) FSKD_CASE(8)
         FSKD_CASE(9) FSKD_CASE(10) FSKD_CASE(11) FSKD_CASE(12)

@@ -86,10 +86,13 @@ __device__ __forceinline__ void ws_stage(float (&v)[V], int lane)
 
 // X[k] = this lane's partial (re, im) of tone k. Writes the symbol of window
 // w (lane j == 0) and, if mag, its K magnitudes; `live` = w is a real window.
-template <int K>
+// PERM: the kernel's tone slot s holds the host's tone (perm >> 4 s) & 15
+// (residue.hip DCLS); magnitudes, the tie rule and the symbol use that index.
+template <int K, bool PERM = false>
 __device__ __forceinline__ void window_sum_decide(const float (&re)[K], const float (&im)[K],
                                                   int lane, long long w, bool live,
-                                                  uint8_t *sym, float *mag)
+                                                  uint8_t *sym, float *mag,
+                                                  unsigned long long perm = 0)
 {
     static_assert(K >= 1 && K <= 16, "tones");
     constexpr int KP = K <= 1 ? 1 : K <= 2 ? 2 : K <= 4 ? 4 : K <= 8 ? 8 : 16;
@@ -119,13 +122,15 @@ __device__ __forceinline__ void window_sum_decide(const float (&re)[K], const fl
     }
     const bool ok0 = re_lane && t0 < K;
     const bool ok1 = V > 16 && re_lane && t0 + 8 < K;
+    const int o0 = PERM ? (int)((perm >> (4 * t0)) & 15u) : t0;
+    const int o1 = PERM ? (int)((perm >> (4 * ((t0 + 8) & 15))) & 15u) : t0 + 8;
     if (live && mag) {
-        if (ok0) mag[w * K + t0] = P0;
-        if (ok1) mag[w * K + t0 + 8] = P1;
+        if (ok0) mag[w * K + o0] = P0;
+        if (ok1) mag[w * K + o1] = P1;
     }
-    unsigned key = ok0 ? ((__float_as_uint(P0) & ~15u) | (unsigned)(15 - t0)) : 0u;
+    unsigned key = ok0 ? ((__float_as_uint(P0) & ~15u) | (unsigned)(15 - o0)) : 0u;
     if constexpr (V > 16) {
-        const unsigned k1 = ok1 ? ((__float_as_uint(P1) & ~15u) | (unsigned)(15 - (t0 + 8))) : 0u;
+        const unsigned k1 = ok1 ? ((__float_as_uint(P1) & ~15u) | (unsigned)(15 - o1)) : 0u;
         key = key > k1 ? key : k1;
     }
     key = max(key, ws_dpp_u<0xB1>(key));

@@ -292,6 +292,23 @@ int main(int argc, char **argv)
 #define RZA(K) reinterpret_cast<const void *>(&residue_tile_kernel<K, 4, 4, true, false, (K <= 8 ? 4 : 0), 2, false, false>)
         static double bo[16];
         for (int i = 0; i < 16; ++i) bo[i] = 32 + 9 * i;  // every class mod 8
+        // the same 8 bins permuted so slot pairs (2c, 2c+1) share class c (DCLS)
+        static const double bp[8] = {32, 68, 41, 95, 59, 77, 50, 86};
+        static GoertzelParams r8p = p8;
+        make_res(8, bp, r8p);
+        add_variant(vs, reinterpret_cast<const void *>(&residue_tile_kernel<8, 4>), 4,
+                    "residue perm", r8p, 8, cus, 1, residue_lds_bytes(8, 4, 2), "o");
+        add_variant(vs, reinterpret_cast<const void *>(
+                        &residue_tile_kernel<8, 4, 4, true, false, 4, 2, false, true, false, true>),
+                    4, "residue DCLS perm", r8p, 8, cus, 1, residue_lds_bytes(8, 4, 2), "o");
+        add_variant(vs, reinterpret_cast<const void *>(
+                        &residue_tile_kernel<8, 4, 4, true, false, 0, 2, false, true, false, true>),
+                    4, "residue DCLS rotLDSonly perm", r8p, 8, cus, 1, 8 * 16 * 2 * 16, "o");
+        add_variant(vs, reinterpret_cast<const void *>(&residue_tile_kernel<8, 4>), 4,
+                    "residue perm", r8p, 8, cus, 1, residue_lds_bytes(8, 4, 2), "o");
+        add_variant(vs, reinterpret_cast<const void *>(
+                        &residue_tile_kernel<8, 4, 4, true, false, 4, 2, false, true, false, true>),
+                    4, "residue DCLS perm", r8p, 8, cus, 1, residue_lds_bytes(8, 4, 2), "o");
         static GoertzelParams r8s = p8, r3 = p8, r4 = p8, r8 = p8, r16 = p8, g3 = p8, g4 = p8, g8 = p8;
         make_res(8, b8, r8s);
         make_res(3, bo, r3);

@@ -81,6 +81,30 @@ def test_residue_tone_counts_integer_bins(A, O, torch, k):
     run_case(A, O, freqs, W=333, seed=k, method=RESIDUE)
 
 
+@pytest.mark.parametrize("bins,hop", [
+    ([32 + 9 * i for i in range(8)][::-1], 1024),          # every residue once, reversed
+    ([95 - 9 * i for i in (3, 0, 6, 1, 7, 2, 5, 4)], 1024),  # same set, scrambled
+    ([8, 16, 9, 17, 11, 19, 10, 18], 1024),                 # residues 0,0,1,1,3,3,2,2
+    ([40, 44, 33, 39, 35, 37, 42, 46], 256),                # 0,4,1,7,3,5,2,6 (pairs share a class)
+    ([32 + 9 * i for i in range(16)], 1024),                # K = 16: every class 4 times
+    ([200 - 9 * i for i in range(16)], 512),
+])
+def test_residue_compile_time_classes(A, O, torch, bins, hop):
+    """Plans with K / 4 tones in every residue class (n = 1024, K = 8 or 16):
+    the residue detector permutes the tones so each kernel slot reads a fixed
+    class from registers (residue.hip DCLS) and the window_sum epilogue maps
+    magnitudes, the tie rule and the symbol back to the caller's tone order."""
+    freqs = tuple(b * 46.875 for b in bins)
+    run_case(A, O, freqs, W=700, hop=hop, seed=sum(bins), method=RESIDUE)
+    # exact ties (all-zero window) still go to the caller's lowest tone index
+    x = np.zeros((3, 1024), np.int16)
+    x[1] = np.round(8000 * np.cos(2 * np.pi * bins[5] * np.arange(1024) / 1024))
+    with A.Demodulator(freqs=freqs, method=RESIDUE) as d:
+        sym, mag = d.batch(x, mags=True)
+    assert sym[0] == 0 and sym[2] == 0 and (mag[0] == 0).all()
+    assert sym[1] == 5 and int(np.argmax(mag[1])) == 5
+
+
 @pytest.mark.parametrize("n", [64, 128, 256, 512, 1024, 2048, 4096])
 @pytest.mark.parametrize("hop_div", [1, 4])
 def test_residue_all_lengths(A, O, torch, n, hop_div):
