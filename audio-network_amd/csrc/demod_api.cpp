@@ -34,6 +34,7 @@ struct demod {
     float sgn[kMaxTones] = {};  // plain detector, Reinsch form: sign of cos(w_k)
     bool reinsch = false;       // plain detector: Reinsch-modified recurrence
     bool dcls = false;          // residue detector: compile-time classes, slots permuted
+    bool f16 = false;           // fold detector: fold by 16, slots permuted (Z0 tones, Z8 tones)
     unsigned long long perm = 0;  // DCLS: nibble s = tone index of kernel slot s
     int zcls[kMaxTones] = {};   // residue detector: class each tone reads
     // staging for host-pointer calls
@@ -241,6 +242,23 @@ static int init_device_state(demod_t *st)
             st->dcls = true;
         }
     }
+    // Fold detector, F16 (fold.hip): n = 1024, K = 8 on multiples of 8 bins
+    // with four tones on multiples of 16 (read Z0) and four on odd multiples
+    // of 8 (read Z8), e.g. the survey's 8-FSK plan; slots 0-3 hold the Z0
+    // tones, 4-7 the Z8 tones, and lane j of a window covers folded positions
+    // 8 (j & 7) .. +7 of the N/16-sample fold.
+    st->f16 = false;
+    if (st->detector == kDetFolded && st->log2g == 4 && c.k == 8) {
+        std::vector<uint32_t> z0, z8;
+        for (uint32_t k = 0; k < c.k; ++k) ((integer_bin(c, k) / 8) % 2 ? z8 : z0).push_back(k);
+        if (z0.size() == 4 && z8.size() == 4) {
+            for (uint32_t sl = 0; sl < 8; ++sl) {
+                slot_tone[sl] = sl < 4 ? z0[sl] : z8[sl - 4];
+                st->perm |= (unsigned long long)slot_tone[sl] << (4 * sl);
+            }
+            st->f16 = true;
+        }
+    }
     std::vector<float4> rot((size_t)c.k * g * (residue ? 2 : 1));
     for (uint32_t sl = 0; sl < c.k; ++sl) {
         const uint32_t k = slot_tone[sl];  // rows below are kernel slots (= tones unless DCLS)
@@ -256,7 +274,8 @@ static int init_device_state(demod_t *st)
         const double al = rho == 4 ? 0.0 : 1.0, be = rho == 4 ? 1.0 : 0.0, ga = kGam[rho];
         st->zcls[sl] = kCls[rho];
         for (int j = 0; j < g; ++j) {
-            const double a = -w * (span * j + span - 1.0), b = -w * (span * j + span);
+            const double pos = st->f16 ? (double)(j & 7) : (double)j;  // F16: lanes j, j + 8 share positions
+            const double a = -w * (span * pos + span - 1.0), b = -w * (span * pos + span);
             const double Ar = std::cos(a), Ai = std::sin(a), Br = std::cos(b), Bi = std::sin(b);
             if (!residue && st->reinsch) {
                 const double C1r = Ar - sg * Br, C1i = Ai - sg * Bi;
@@ -417,6 +436,7 @@ static int enqueue_batch(demod_t *st, const int16_t *d_pcm, size_t n_windows, ui
     }
     p.reinsch = st->reinsch ? 1 : 0;
     p.dcls = st->dcls ? 1 : 0;
+    p.f16 = st->f16 ? 1 : 0;
     p.perm = st->perm;
     HIP_TRY(launch_detector(st->detector, p, s));
     return (int)n_windows;

@@ -32,7 +32,8 @@ struct GoertzelParams {
     float sgn[kMaxTones];    // reinsch: sign of cos(w_k) (+1 / -1)
     int reinsch;             // goertzel.hip: Reinsch-modified recurrence (tones near 0 / fs/2)
     int dcls;                // residue.hip: tone slot s reads class (s / 2) % 4 from registers
-    unsigned long long perm; // residue.hip DCLS: nibble s = the host's index of tone slot s
+    unsigned long long perm; // DCLS / F16: nibble s = the host's index of tone slot s
+    int f16;                 // fold.hip: fold by 16 (K = 8, four tones each on Z0 / Z8)
     int zcls[kMaxTones];     // residue.hip: residue class (0..3) tone k reads
     int xcd_swizzle;         // 1: blocks b, b+8, b+16.. (one XCD) take adjacent tiles
 };

@@ -53,8 +53,18 @@ __device__ __forceinline__ float group_sum_f(float v, int log2g)
 //       slice (linear: chunk q at 16 q, conflict-free for both the 64-chunk
 //       writes and the j + 16 m reads), instead of the direct per-lane
 //       layout whose instructions each touch four 256-byte pieces.
+//   F16: (K = 8, n = 1024, LDST) fold by 16. Tones on multiples of 16 bins
+//       read Z0[r] = sum_{m<16} x[r + 64 m], tones on odd multiples of 8 read
+//       Z8[r] = sum (-1)^m x[r + 64 m] (W^{64 b} = +1 / -1). Lane j < 8 of a
+//       window holds the even-m half E of folded positions 8(j & 7) .. +7,
+//       lane j + 8 the odd half O, so one DPP row_ror:8 gives both lanes
+//       E + O (lanes < 8) and E - O (lanes >= 8); the host permutes the plan
+//       so slots 0-3 are Z0 tones and 4-7 Z8 tones (4 each), and lanes < 8
+//       run slots 0-3, lanes >= 8 slots 4-7: half the recurrences and
+//       rotations per lane, and the first reduce-scatter stage is already done
+//       (window_sum_decide_split8; perm maps slots back to the caller's tones).
 template <int K, int LOG2G, bool NT = true, int WPB = 4, bool ROTLDS = false, bool NTS = false,
-          bool WS = false, bool PK = false, bool LDST = false>
+          bool WS = false, bool PK = false, bool LDST = false, bool F16 = false>
 __global__ __launch_bounds__(64 * WPB) void fold_tile_kernel(GoertzelParams p)
 {
     const int lane = threadIdx.x & 63;
@@ -67,9 +77,19 @@ __global__ __launch_bounds__(64 * WPB) void fold_tile_kernel(GoertzelParams p)
     const long long wins_per_tile = 64 >> log2g;
     const long long n_tiles = (p.n_windows + wins_per_tile - 1) / wins_per_tile;
 
+    static_assert(!F16 || (K == 8 && LOG2G == 4 && LDST && WS && !ROTLDS), "F16: K = 8, n = 1024");
     float4 r[ROTLDS ? 1 : K];
     __shared__ float4 rot_lds[ROTLDS ? K * 64 : 1];
-    if (ROTLDS) {
+    float c16[4];
+    if constexpr (F16) {
+        // lane j runs slots 4 * (j >= 8) + s; rotation rows are per slot and lane
+        const bool up = (lane & 8) != 0;
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+            c16[s4] = up ? p.coef[4 + s4] : p.coef[s4];
+            r[s4] = p.rot[(s4 + (up ? 4 : 0)) * 16 + (lane & 15)];
+        }
+    } else if (ROTLDS) {
         for (int i = threadIdx.x; i < K * g; i += 64 * WPB) rot_lds[i] = p.rot[i];
         __syncthreads();
     } else {
@@ -129,6 +149,29 @@ __global__ __launch_bounds__(64 * WPB) void fold_tile_kernel(GoertzelParams p)
 #pragma unroll
         for (int q = 0; q < 8; ++q) xf[q] = (float)acc[q];
 
+        if constexpr (F16) {
+            const float sg = (lane & 8) ? -1.f : 1.f;
+            float y[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q)  // lanes < 8: E + O = Z0; lanes >= 8: E - O = Z8
+                y[q] = fmaf(sg, xf[q], dppf_<0x128>(xf[q]));
+            float xr[4], xi[4];
+#pragma unroll
+            for (int s4 = 0; s4 < 4; ++s4) {
+                float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const float a = fmaf(c16[s4], s1, y[q] - s2);
+                    s2 = s1;
+                    s1 = a;
+                }
+                xr[s4] = r[s4].x * s1 - r[s4].z * s2;
+                xi[s4] = r[s4].y * s1 - r[s4].w * s2;
+            }
+            const long long w = wbase + win_in_tile;
+            window_sum_decide_split8<true>(xr, xi, lane, w, w < p.n_windows, p.sym, p.mag, p.perm);
+            continue;
+        }
         if constexpr (WS && LOG2G == 4) {
             float xr[K], xi[K];
             float t1[K], t2[K];
@@ -204,8 +247,12 @@ __global__ __launch_bounds__(64 * WPB) void fold_tile_kernel(GoertzelParams p)
 }
 
 template <int K>
-static const void *fold_kernel_for(int log2g)
+static const void *fold_kernel_for(int log2g, bool f16)
 {
+    if constexpr (K == 8)
+        if (log2g == 4 && f16)
+            return reinterpret_cast<const void *>(
+                &fold_tile_kernel<8, 4, true, kPlainWPB, false, false, true, false, true, true>);
     // n = 1024: window_sum.h epilogue (K = 8: 352 -> 347 us, K = 2: 335 -> 329 us)
     // and LDS regrouping of contiguous loads (K = 8: 345.8 -> 339.9 us, K = 2:
     // 338.5 -> 319.9 us; profiles/round1/probe_ldst.log)
@@ -215,10 +262,10 @@ static const void *fold_kernel_for(int log2g)
     return reinterpret_cast<const void *>(&fold_tile_kernel<K, -1, true, kPlainWPB>);
 }
 
-const void *fold_kernel_ptr(int k, int log2g)
+const void *fold_kernel_ptr(int k, int log2g, bool f16)
 {
     switch (k) {
-#define FSKD_CASE(K) case K: return fold_kernel_for<K>(log2g);
+#define FSKD_CASE(K) case K: return fold_kernel_for<K>(log2g, f16);
         FSKD_CASE(1) FSKD_CASE(2) FSKD_CASE(3) FSKD_CASE(4)
         FSKD_CASE(5) FSKD_CASE(6) FSKD_CASE(7) FSKD_CASE(8)
         FSKD_CASE(9) FSKD_CASE(10) FSKD_CASE(11) FSKD_CASE(12)

@@ -344,11 +344,11 @@ int tile_grid(long long n_windows, int log2g, int wpb)
     return (int)blocks;
 }
 
-const void *fold_kernel_ptr(int k, int log2g);
+const void *fold_kernel_ptr(int k, int log2g, bool f16);
 
 hipError_t launch_detector(int detector, const GoertzelParams &p, hipStream_t s)
 {
-    const void *f = detector == kDetFolded    ? fold_kernel_ptr(p.k, p.log2g)
+    const void *f = detector == kDetFolded    ? fold_kernel_ptr(p.k, p.log2g, p.f16 != 0)
                   : detector == kDetResidue ? residue_kernel_ptr(p.k, p.log2g, p.dcls != 0)
                                             : kernel_ptr(p.k, p.log2g, p.reinsch != 0);
     if (!f) return hipErrorInvalidValue;

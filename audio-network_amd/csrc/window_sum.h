@@ -140,4 +140,41 @@ __device__ __forceinline__ void window_sum_decide(const float (&re)[K], const fl
     if (live && j == 0) sym[w] = (uint8_t)(15 - (key & 15u));
 }
 
+// The same epilogue for K = 8 when the kernel has already split the tones by
+// lane bit 3 (fold.hip F16: lanes 0-7 of a window hold tones 0-3, lanes 8-15
+// tones 4-7, each over the whole window): that is the state after the first
+// reduce-scatter stage, so only stages 2, 1, 0 run (21 instead of 45
+// instructions). re/im = this lane's 4 tones (slots 4 * bit3 + s).
+template <bool PERM = false>
+__device__ __forceinline__ void window_sum_decide_split8(const float (&re)[4], const float (&im)[4],
+                                                         int lane, long long w, bool live,
+                                                         uint8_t *sym, float *mag,
+                                                         unsigned long long perm = 0)
+{
+    constexpr int K = 8;
+    float v[8];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        v[2 * k] = re[k];
+        v[2 * k + 1] = im[k];
+    }
+    ws_stage<2>(v, lane);
+    ws_stage<1>(v, lane);
+    ws_stage<0>(v, lane);
+    // lane j holds value (j & 15) of the 16-value list: re_t in lane 2t, im_t in 2t + 1
+    const int j = lane & 15;
+    const bool re_lane = (j & 1) == 0;
+    const int t0 = j >> 1;
+    const float sq = v[0] * v[0];
+    const float P0 = sq + ws_dpp<0xB1>(sq);
+    const int o0 = PERM ? (int)((perm >> (4 * t0)) & 15u) : t0;
+    if (live && mag && re_lane) mag[w * K + o0] = P0;
+    unsigned key = re_lane ? ((__float_as_uint(P0) & ~15u) | (unsigned)(15 - o0)) : 0u;
+    key = max(key, ws_dpp_u<0xB1>(key));
+    key = max(key, ws_dpp_u<0x4E>(key));
+    key = max(key, ws_dpp_u<0x141>(key));
+    key = max(key, ws_dpp_u<0x140>(key));
+    if (live && j == 0) sym[w] = (uint8_t)(15 - (key & 15u));
+}
+
 }  // namespace fskd
