@@ -255,6 +255,32 @@ int main(int argc, char **argv)
     add_variant(vs, FDWT(8, 2), 2, "fold WS LDST", f8, 8, cus, 1);
     add_variant(vs, FDWT(8, 4), 4, "fold WS LDST", f8, 8, cus, 1);
     add_variant(vs, FDWT(2, 2), 2, "fold WS LDST", f2, 2, cus, 1);
+    {
+        // F16 (survey 8-FSK plan: bins 32..88 step 8 -> slots: Z0 tones 32,48,64,80; Z8 tones 40,56,72,88)
+        static GoertzelParams f16 = f8;
+        static const double b16[8] = {32, 48, 64, 80, 40, 56, 72, 88};
+        std::vector<float4> rot(8 * 16);
+        for (int k = 0; k < 8; ++k) {
+            const double w = 2 * M_PI * b16[k] / 1024.0;
+            f16.coef[k] = (float)(2 * std::cos(w));
+            for (int j = 0; j < 16; ++j) {
+                const double a = -w * (8.0 * (j & 7) + 7), b = -w * (8.0 * (j & 7) + 8);
+                rot[k * 16 + j] = make_float4(std::cos(a), std::sin(a), std::cos(b), std::sin(b));
+            }
+        }
+        float4 *d;
+        CK(hipMalloc(&d, rot.size() * sizeof(float4)));
+        CK(hipMemcpy(d, rot.data(), rot.size() * sizeof(float4), hipMemcpyHostToDevice));
+        f16.rot = d;
+        f16.perm = 0x75316420ull;  // nibble s = tone index (bins 32 + 8 i) of slot s
+#define FD16(B) reinterpret_cast<const void *>(&fold_tile_kernel<8, 4, true, B, false, false, true, false, true, true>)
+        add_variant(vs, FD16(2), 2, "fold F16", f16, 8, cus, 1);
+        add_variant(vs, FD16(2), 2, "fold F16", f16, 8, cus, 2);
+        add_variant(vs, FD16(2), 2, "fold F16", f16, 8, cus, 4);
+        GoertzelParams f16n = f16;
+        f16n.mag = nullptr;
+        add_variant(vs, FD16(2), 2, "fold F16 nomag", f16n, 8, cus, 1);
+    }
     add_variant(vs, reinterpret_cast<const void *>(&fold_tile_kernel<8, 4, true, 2, false, false, true, true, true>),
                 2, "fold WS PK LDST", f8, 8, cus, 1);
     add_variant(vs, GZWB(8, 2), 2, "goertzel PK WS", p8, 8, cus, 1);
@@ -517,8 +543,28 @@ int main(int argc, char **argv)
     for (int i = 0; i < 200; ++i) vs[0].run(nullptr);
     for (auto &v : vs) v.run(nullptr);
     CK(hipDeviceSynchronize());
+    // PROBE_B2B=1: each variant's reps launch back to back (events between
+    // launches, one sync per batch), as bench.py runs them; default: a host
+    // sync after every launch.
+    const bool b2b = std::getenv("PROBE_B2B") != nullptr;
+    std::vector<hipEvent_t> evs(reps + 1);
+    for (auto &e : evs) CK(hipEventCreate(&e));
     for (int r = 0; r < rounds; ++r)
-        for (auto &v : vs)
+        for (auto &v : vs) {
+            if (b2b) {
+                CK(hipEventRecord(evs[0], nullptr));
+                for (int i = 0; i < reps; ++i) {
+                    v.run(nullptr);
+                    CK(hipEventRecord(evs[i + 1], nullptr));
+                }
+                CK(hipEventSynchronize(evs[reps]));
+                for (int i = 0; i < reps; ++i) {
+                    float ms;
+                    CK(hipEventElapsedTime(&ms, evs[i], evs[i + 1]));
+                    v.ms.push_back(ms);
+                }
+                continue;
+            }
             for (int i = 0; i < reps; ++i) {
                 CK(hipEventRecord(a, nullptr));
                 v.run(nullptr);
@@ -528,6 +574,7 @@ int main(int argc, char **argv)
                 CK(hipEventElapsedTime(&ms, a, b));
                 v.ms.push_back(ms);
             }
+        }
     // cross-check symbols of every variant against the first variant of the same K
     std::vector<std::pair<std::string, std::vector<uint8_t>>> refs;
     std::vector<uint8_t> cur(W);
