@@ -33,15 +33,24 @@ __device__ __forceinline__ unsigned tile_value(const short *p, long long t, int 
     return acc ^ (unsigned)__shfl_xor((int)acc, 32);
 }
 
-template <bool W>
+// W: 0 = no write, 1 = 128 B per tile (8-FSK magnitudes), 2 = 32 B per tile
+// (2-FSK magnitudes), 3 = 4 B per tile (the symbols of its 4 windows)
+template <int W>
 __global__ __launch_bounds__(128) void kA(const short *p, long long n_tiles, unsigned *out)
 {
     const int lane = threadIdx.x & 63;
     const long long t = (long long)blockIdx.x * 2 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (t >= n_tiles) return;
-    const unsigned v = tile_value(p, t, lane);
-    if (W) {
+    unsigned v = tile_value(p, t, lane);
+    if (W == 1) {
         if (lane < 32) out[t * 32 + lane] = v;
+    } else if (W == 2) {
+        v ^= (unsigned)__shfl_xor((int)v, 8) ^ (unsigned)__shfl_xor((int)v, 16);
+        if (lane < 8) out[t * 8 + lane] = v;
+    } else if (W == 3) {
+        v ^= (unsigned)__shfl_xor((int)v, 1) ^ (unsigned)__shfl_xor((int)v, 2) ^ (unsigned)__shfl_xor((int)v, 4) ^
+             (unsigned)__shfl_xor((int)v, 8) ^ (unsigned)__shfl_xor((int)v, 16);
+        if (lane == 0) out[t] = v;
     } else if (v == 0x9E3779B9u) out[0] = v;
 }
 
@@ -130,8 +139,10 @@ int main()
     const long long T = (n_tiles + waves - 1) / waves;
     struct V { const char *name; std::function<void()> run; std::vector<float> ms; };
     std::vector<V> vs;
-    vs.push_back({"A one tile/wave, no write", [&] { hipLaunchKernelGGL(kA<false>, dim3(n_tiles / 2), dim3(128), 0, 0, in, n_tiles, out); }, {}});
-    vs.push_back({"A one tile/wave, 128 B write", [&] { hipLaunchKernelGGL(kA<true>, dim3(n_tiles / 2), dim3(128), 0, 0, in, n_tiles, out); }, {}});
+    vs.push_back({"A one tile/wave, no write", [&] { hipLaunchKernelGGL(kA<0>, dim3(n_tiles / 2), dim3(128), 0, 0, in, n_tiles, out); }, {}});
+    vs.push_back({"A one tile/wave, 128 B write", [&] { hipLaunchKernelGGL(kA<1>, dim3(n_tiles / 2), dim3(128), 0, 0, in, n_tiles, out); }, {}});
+    vs.push_back({"A one tile/wave, 32 B write", [&] { hipLaunchKernelGGL(kA<2>, dim3(n_tiles / 2), dim3(128), 0, 0, in, n_tiles, out); }, {}});
+    vs.push_back({"A one tile/wave, 4 B write", [&] { hipLaunchKernelGGL(kA<3>, dim3(n_tiles / 2), dim3(128), 0, 0, in, n_tiles, out); }, {}});
     vs.push_back({"A4 one tile/wave, 128 B as 8 x dwordx4", [&] { hipLaunchKernelGGL(kA4, dim3(n_tiles / 2), dim3(128), 0, 0, in, n_tiles, out); }, {}});
     vs.push_back({"P persistent, no write", [&] { hipLaunchKernelGGL((kP<false, false>), dim3(waves / 4), dim3(256), 0, 0, in, n_tiles, T, out); }, {}});
     vs.push_back({"C persistent, 128 B write per tile", [&] { hipLaunchKernelGGL((kP<true, false>), dim3(waves / 4), dim3(256), 0, 0, in, n_tiles, T, out); }, {}});
