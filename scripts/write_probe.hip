@@ -54,6 +54,37 @@ __global__ __launch_bounds__(128) void kA(const short *p, long long n_tiles, uns
     } else if (v == 0x9E3779B9u) out[0] = v;
 }
 
+// 2-FSK pattern: per tile 4 B of symbols + 32 B of magnitudes into two arrays.
+// S16: blocks of 16 waves stage both in LDS and write them as one 64 B and one
+// 512 B contiguous store after a block barrier; S1: every wave writes its own.
+template <bool STAGE>
+__global__ __launch_bounds__(1024) void kS(const short *p, long long n_tiles, unsigned *sym, unsigned *mag)
+{
+    __shared__ unsigned ss[16], sm[16 * 8];
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const long long t = (long long)blockIdx.x * 16 + wv;
+    unsigned v = t < n_tiles ? tile_value(p, t, lane) : 0u;
+    v ^= (unsigned)__shfl_xor((int)v, 8) ^ (unsigned)__shfl_xor((int)v, 16);
+    if (!STAGE) {
+        if (t < n_tiles) {
+            if (lane < 8) mag[t * 8 + lane] = v;
+            if (lane == 0) sym[t] = v >> 3;
+        }
+        return;
+    }
+    if (lane < 8) sm[wv * 8 + lane] = v;
+    if (lane == 0) ss[wv] = v >> 3;
+    __syncthreads();
+    const long long t0 = (long long)blockIdx.x * 16;
+    if (wv == 0) {
+        if (lane < 16 && t0 + lane < n_tiles) sym[t0 + lane] = ss[lane];
+    } else if (wv == 1) {
+        for (int i = lane; i < 128; i += 64)
+            if (t0 + i / 8 < n_tiles) mag[t0 * 8 + i] = sm[i];
+    }
+}
+
 // A4: as A, the 128 B written by 8 lanes as dwordx4
 __global__ __launch_bounds__(128) void kA4(const short *p, long long n_tiles, unsigned *out)
 {
@@ -143,6 +174,10 @@ int main()
     vs.push_back({"A one tile/wave, 128 B write", [&] { hipLaunchKernelGGL(kA<1>, dim3(n_tiles / 2), dim3(128), 0, 0, in, n_tiles, out); }, {}});
     vs.push_back({"A one tile/wave, 32 B write", [&] { hipLaunchKernelGGL(kA<2>, dim3(n_tiles / 2), dim3(128), 0, 0, in, n_tiles, out); }, {}});
     vs.push_back({"A one tile/wave, 4 B write", [&] { hipLaunchKernelGGL(kA<3>, dim3(n_tiles / 2), dim3(128), 0, 0, in, n_tiles, out); }, {}});
+    unsigned *sym2;
+    CK(hipMalloc(&sym2, n_tiles * 4));
+    vs.push_back({"S1 2-FSK pattern, each wave its 4 B + 32 B", [&] { hipLaunchKernelGGL(kS<false>, dim3(n_tiles / 16), dim3(1024), 0, 0, in, n_tiles, sym2, out); }, {}});
+    vs.push_back({"S16 2-FSK pattern, 16-wave block stages, 64 B + 512 B", [&] { hipLaunchKernelGGL(kS<true>, dim3(n_tiles / 16), dim3(1024), 0, 0, in, n_tiles, sym2, out); }, {}});
     vs.push_back({"A4 one tile/wave, 128 B as 8 x dwordx4", [&] { hipLaunchKernelGGL(kA4, dim3(n_tiles / 2), dim3(128), 0, 0, in, n_tiles, out); }, {}});
     vs.push_back({"P persistent, no write", [&] { hipLaunchKernelGGL((kP<false, false>), dim3(waves / 4), dim3(256), 0, 0, in, n_tiles, T, out); }, {}});
     vs.push_back({"C persistent, 128 B write per tile", [&] { hipLaunchKernelGGL((kP<true, false>), dim3(waves / 4), dim3(256), 0, 0, in, n_tiles, T, out); }, {}});
