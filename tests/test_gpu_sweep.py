@@ -165,3 +165,54 @@ def test_random_stream(A, O, torch, i):
         else np.ones(gs.size, bool)
     bad = np.flatnonzero(posed & (gs != ws))
     assert bad.size == 0, (bad[:8], c)
+
+
+N_STRUCT_CASES = 24
+
+
+@pytest.mark.parametrize("i", range(N_STRUCT_CASES))
+def test_random_permuted_plans(A, O, torch, i):
+    """Plans that take the permuted-slot kernels at n = 1024 (DESIGN.md §4.2,
+    §4.3): fold by 16 (K = 8, four tones on multiples of 16 bins and four on
+    odd multiples of 8) and the residue kernel's compile-time classes (K = 8
+    or 16 with K / 4 tones per class), in random tone order, hop and level;
+    magnitudes and symbols in the caller's tone order."""
+    rng = np.random.default_rng(0xC1A55 + i)
+    kind = ("fold16", "residue8", "residue16")[i % 3]
+    if kind == "fold16":
+        z0 = rng.choice(np.arange(1, 31) * 16, 4, replace=False)
+        z8 = rng.choice(np.arange(0, 31) * 16 + 8, 4, replace=False)
+        bins = np.concatenate([z0, z8])
+        method = A.METHOD_FOLDED
+    else:
+        K = 8 if kind == "residue8" else 16
+        cls_of = {0: 0, 4: 0, 1: 1, 7: 1, 3: 2, 5: 2, 2: 3, 6: 3}
+        bins = []
+        for c in range(4):
+            rhos = [r for r, cc in cls_of.items() if cc == c]
+            pool = [b for b in range(8, 505) if b % 8 in rhos and b not in bins]
+            bins += list(rng.choice(pool, K // 4, replace=False))
+        bins = np.array(bins)
+        method = A.METHOD_RESIDUE
+    bins = rng.permutation(bins)
+    freqs = tuple(float(b) * 46.875 for b in bins)
+    hop = 1024 if rng.random() < 0.5 else 8 * int(rng.integers(1, 129))
+    W = int(rng.integers(1, 500))
+    pcm, _ = O.synth_fsk(freqs, 1024, W, 7000 + i, int(rng.choice([300, 8000, 30000])),
+                         int(rng.choice([0, 400, 1500])))
+    flat = pcm.reshape(-1)
+    Wh = min((flat.size - 1024) // hop + 1, 3000)
+    flat = flat[:(Wh - 1) * hop + 1024]
+    with A.Demodulator(hop=hop, freqs=freqs, method=method) as d:
+        assert d.method == method
+        sym, mag = d.batch(flat, n_windows=Wh, mags=True)
+    ref_sym, ref_P = O.goertzel(flat, freqs, 1024, hop, Wh)
+    denom = mag_denom(ref_P, flat, 1024, hop)
+    err = (np.abs(mag.astype(np.float64) - ref_P).max(axis=1) / denom).max()
+    assert err <= MAG_TOL, (err, kind, list(bins))
+    Ps = np.sort(ref_P, axis=1)
+    posed = (Ps[:, -1] - Ps[:, -2]) / denom > 4 * MAG_TOL
+    bad = np.flatnonzero(posed & (sym != ref_sym))
+    assert bad.size == 0, (bad[:8], kind, list(bins))
+    if hop == 1024:
+        assert posed.mean() >= 0.99
