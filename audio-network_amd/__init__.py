@@ -40,6 +40,7 @@ DEMOD_NO_DEVICE = -9
 DEMOD_FRAME_TOO_LARGE = -10
 
 DEMOD_MAX_TONES = 16
+DEMOD_OPUS_LOOKAHEAD = 312  # Opus decoder delay at 48 kHz (OpusEncoder.kt:65-67)
 DEMOD_MAX_FRAME_PAYLOAD = 4096
 
 CH_LEFT, CH_RIGHT, CH_DOWNMIX = 0, 1, 2
@@ -61,7 +62,7 @@ class DemodCfg(ctypes.Structure):
         ("channel_mode", ctypes.c_int32),
         ("device", ctypes.c_int32),
         ("method", ctypes.c_int32),
-        ("reserved", ctypes.c_uint32),
+        ("lead_in", ctypes.c_uint32),
         ("freqs", ctypes.c_double * DEMOD_MAX_TONES),
     ]
 
@@ -206,7 +207,7 @@ def version_string() -> str:
 def make_cfg(fs: float = 48000.0, n: int = 1024, hop: Optional[int] = None,
              freqs: Sequence[float] = FSK2_FREQS, channels: int = 1,
              channel_mode: int = CH_LEFT, device: int = 0,
-             method: int = METHOD_AUTO) -> DemodCfg:
+             method: int = METHOD_AUTO, lead_in: int = 0) -> DemodCfg:
     cfg = DemodCfg()
     load_library().demod_cfg_default(ctypes.byref(cfg))
     cfg.fs = float(fs)
@@ -219,6 +220,7 @@ def make_cfg(fs: float = 48000.0, n: int = 1024, hop: Optional[int] = None,
     cfg.channel_mode = int(channel_mode)
     cfg.device = int(device)
     cfg.method = int(method)
+    cfg.lead_in = int(lead_in)
     for i in range(DEMOD_MAX_TONES):
         cfg.freqs[i] = float(freqs[i]) if i < len(freqs) else 0.0
     return cfg
@@ -231,6 +233,32 @@ def _ptr(a) -> int:
     if isinstance(a, np.ndarray):
         return a.ctypes.data
     return int(a.data_ptr())
+
+
+_DTYPE_BYTES = {"int16": 2, "uint8": 1, "float32": 4}
+
+
+def _check_dev(t, what: str, dtype: str, min_numel: int, device: Optional[int] = None,
+               nullable: bool = False) -> None:
+    """Validate a device tensor handed to the C ABI as a raw pointer: a short,
+    strided, wrong-dtype or wrong-device tensor would otherwise become silent
+    out-of-bounds device writes. Raises DemodError(DEMOD_BAD_ARG)."""
+    if t is None:
+        if nullable or min_numel == 0:
+            return
+        raise DemodError(DEMOD_BAD_ARG, f"{what}: required")
+    if isinstance(t, int):
+        raise DemodError(DEMOD_BAD_ARG, f"{what}: pass a device tensor, not a raw address")
+    if not hasattr(t, "is_contiguous") or not hasattr(t, "device"):
+        raise DemodError(DEMOD_BAD_ARG, f"{what}: expected a torch device tensor")
+    if str(t.dtype) != "torch." + dtype:
+        raise DemodError(DEMOD_BAD_ARG, f"{what}: dtype {t.dtype}, need torch.{dtype}")
+    if not t.is_contiguous():
+        raise DemodError(DEMOD_BAD_ARG, f"{what}: not contiguous")
+    if t.device.type != "cuda" or (device is not None and t.device.index != device):
+        raise DemodError(DEMOD_BAD_ARG, f"{what}: on {t.device}, need cuda:{device}")
+    if t.numel() < min_numel:
+        raise DemodError(DEMOD_BAD_ARG, f"{what}: {t.numel()} elements, need >= {min_numel}")
 
 
 class Demodulator:
@@ -329,8 +357,21 @@ class Demodulator:
             raise DemodError(rc, "demod_batch")
         return (sym[:rc], mag[:rc]) if mags else sym[:rc]
 
+    def _check_batch(self, d_pcm, n_windows: int, d_sym, d_mag, d_spec=None) -> None:
+        n_windows = int(n_windows)
+        if n_windows < 0:
+            raise DemodError(DEMOD_BAD_ARG, "n_windows < 0")
+        dev = int(self.cfg.device)
+        need = (n_windows - 1) * self.hop + self.n if n_windows else 0
+        _check_dev(d_pcm, "d_pcm", "int16", need, dev)
+        _check_dev(d_sym, "d_sym", "uint8", n_windows, dev)
+        _check_dev(d_mag, "d_mag", "float32", n_windows * self.k, dev, nullable=True)
+        _check_dev(d_spec, "d_spec", "float32", n_windows * (self.n // 2 + 1), dev, nullable=True)
+
     def batch_device(self, d_pcm, n_windows: int, d_sym, d_mag=None) -> int:
-        """Synchronous batch on device pointers/tensors."""
+        """Synchronous batch on device tensors (checked: dtype, contiguity,
+        device, size)."""
+        self._check_batch(d_pcm, n_windows, d_sym, d_mag)
         rc = self._lib.demod_batch(self._h, _ptr(d_pcm), n_windows, _ptr(d_sym), _ptr(d_mag))
         if rc < 0:
             raise DemodError(rc, "demod_batch")
@@ -339,6 +380,7 @@ class Demodulator:
     def batch_async(self, d_pcm, n_windows: int, d_sym, d_mag=None, stream: int = 0) -> int:
         """Enqueue on a HIP stream (raw hipStream_t as int; 0 = default stream,
         e.g. torch.cuda.current_stream().cuda_stream)."""
+        self._check_batch(d_pcm, n_windows, d_sym, d_mag)
         rc = self._lib.demod_batch_async(self._h, _ptr(d_pcm), n_windows, _ptr(d_sym),
                                          _ptr(d_mag), stream or None)
         if rc < 0:
@@ -348,6 +390,7 @@ class Demodulator:
     def batch_spectrum_async(self, d_pcm, n_windows: int, d_sym, d_mag=None, d_spec=None,
                              stream: int = 0) -> int:
         """FFT handles: symbols, tone-bin |X|^2 and the full |X[b]|^2 spectrum."""
+        self._check_batch(d_pcm, n_windows, d_sym, d_mag, d_spec)
         rc = self._lib.demod_batch_spectrum_async(self._h, _ptr(d_pcm), n_windows, _ptr(d_sym),
                                                   _ptr(d_mag), _ptr(d_spec), stream or None)
         if rc < 0:
@@ -358,6 +401,8 @@ class Demodulator:
 def synth_fsk(cfg: DemodCfg, seed: int, n_windows: int, amplitude: int, sigma: int,
               d_pcm, d_sym=None, stream: int = 0, w0: int = 0) -> None:
     """Device generator of the seeded FSK test signal into device buffers."""
+    _check_dev(d_pcm, "d_pcm", "int16", int(n_windows) * int(cfg.n), int(cfg.device))
+    _check_dev(d_sym, "d_sym", "uint8", int(n_windows), int(cfg.device), nullable=True)
     rc = load_library().demod_synth_fsk(ctypes.byref(cfg), ctypes.c_uint64(seed),
                                          ctypes.c_uint64(w0), n_windows,
                                          amplitude, sigma, _ptr(d_pcm), _ptr(d_sym),
@@ -368,6 +413,8 @@ def synth_fsk(cfg: DemodCfg, seed: int, n_windows: int, amplitude: int, sigma: i
 
 def read_ceiling_async(d_buf, n_bytes: int, stream: int = 0) -> None:
     """Read-only reference stream over a device buffer (demod_read_ceiling_async)."""
+    if not hasattr(d_buf, "numel") or d_buf.numel() * d_buf.element_size() < n_bytes:
+        raise DemodError(DEMOD_BAD_ARG, "read_ceiling_async: buffer smaller than n_bytes")
     rc = load_library().demod_read_ceiling_async(_ptr(d_buf), n_bytes, stream or None)
     if rc < 0:
         raise DemodError(rc, "demod_read_ceiling_async")
@@ -549,6 +596,11 @@ def frame_streams_async(d_symbols, n_streams: int, n: int, bits: int, d_out,
                         max_payload: int = DEMOD_MAX_FRAME_PAYLOAD, stream: int = 0) -> int:
     """Device framing of [n_streams][n] symbols: stream s's frames (as
     frame_symbols would make them) at d_out[s * stride]; returns stride."""
+    stride = frame_symbols_size(n, bits, max_payload)
+    _check_dev(d_symbols, "d_symbols", "uint8", int(n_streams) * int(n))
+    _check_dev(d_out, "d_out", "uint8", int(n_streams) * stride)
+    if d_symbols is not None and d_out is not None and d_symbols.device != d_out.device:
+        raise DemodError(DEMOD_BAD_ARG, "d_symbols and d_out on different devices")
     rc = int(load_library().demod_frame_streams_async(_ptr(d_symbols), n_streams, n, bits,
                                                       max_payload, _ptr(d_out), stream or None))
     if rc < 0:

@@ -54,8 +54,32 @@ struct demod {
     // streaming carry (mono samples not yet consumed by a complete window)
     std::vector<int16_t> carry;
     std::vector<int16_t> scratch;
-    // synth
-    int16_t *d_lut = nullptr;
+    // lead-in: mono frames still to drop at the start of the stream (cfg.lead_in
+    // after demod_create / demod_reset)
+    size_t skip = 0;
+};
+
+// Makes `dev` current for the scope of an entry point and restores the
+// caller's current device on return (the ABI must not leave the calling
+// thread on another device).
+struct DeviceGuard {
+    int prev = -1;
+    hipError_t err = hipSuccess;
+    explicit DeviceGuard(int dev)
+    {
+        if (hipGetDevice(&prev) != hipSuccess) {
+            (void)hipGetLastError();
+            prev = -1;
+        }
+        if (prev != dev) err = hipSetDevice(dev);
+    }
+    ~DeviceGuard()
+    {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+    DeviceGuard(const DeviceGuard &) = delete;
+    DeviceGuard &operator=(const DeviceGuard &) = delete;
 };
 
 #define HIP_TRY(x)                                                 \
@@ -128,7 +152,7 @@ static int validate(const demod_cfg_t *c)
         c->method != DEMOD_METHOD_RESIDUE)
         return DEMOD_UNIMPLEMENTED;
     if (c->method == DEMOD_METHOD_FFT && c->n != 1024) return DEMOD_UNIMPLEMENTED;
-    if (c->reserved != 0) return DEMOD_BAD_ARG;
+    if (c->lead_in > 0x7FFFFFFFu) return DEMOD_BAD_ARG;
     if (c->method == DEMOD_METHOD_FOLDED && !fold_eligible(*c)) return DEMOD_BAD_ARG;
     if (c->method == DEMOD_METHOD_RESIDUE && !residue_eligible(*c)) return DEMOD_BAD_ARG;
     for (uint32_t i = 0; i < c->k; ++i)
@@ -146,6 +170,7 @@ static int init_device_state(demod_t *st)
         return DEMOD_NO_DEVICE;
     }
     if (c.device < 0 || c.device >= ndev) return DEMOD_NO_DEVICE;
+    if (c.device >= kMaxDevices) return DEMOD_BAD_ARG;
     HIP_TRY(hipSetDevice(c.device));
     hipDeviceProp_t prop;
     HIP_TRY(hipGetDeviceProperties(&prop, c.device));
@@ -320,7 +345,6 @@ static void free_state(demod_t *st)
         if (st->consumed[b]) (void)hipEventDestroy(st->consumed[b]);
     }
     if (st->copy_stream) (void)hipStreamDestroy(st->copy_stream);
-    if (st->d_lut) (void)hipFree(st->d_lut);
     if (st->stream) (void)hipStreamDestroy(st->stream);
 }
 
@@ -337,6 +361,7 @@ demod_t *demod_create(const demod_cfg_t *cfg, int *error)
         return nullptr;
     }
     st->cfg = *cfg;
+    DeviceGuard guard(cfg->device >= 0 ? cfg->device : 0);
     rc = init_device_state(st);
     if (rc != DEMOD_OK) {
         free_state(st);
@@ -345,6 +370,7 @@ demod_t *demod_create(const demod_cfg_t *cfg, int *error)
         return nullptr;
     }
     st->carry.reserve(cfg->n);
+    st->skip = cfg->lead_in;
     if (error) *error = DEMOD_OK;
     return st;
 }
@@ -352,7 +378,7 @@ demod_t *demod_create(const demod_cfg_t *cfg, int *error)
 void demod_destroy(demod_t *st)
 {
     if (!st) return;
-    (void)hipSetDevice(st->device);
+    DeviceGuard guard(st->device);
     free_state(st);
     delete st;
 }
@@ -361,6 +387,7 @@ int demod_reset(demod_t *st)
 {
     if (!st) return DEMOD_BAD_ARG;
     st->carry.clear();
+    st->skip = st->cfg.lead_in;
     return DEMOD_OK;
 }
 
@@ -388,7 +415,8 @@ static size_t windows_for(const demod_t *st, size_t total)
 int demod_max_symbols(const demod_t *st, size_t n_frames)
 {
     if (!st) return DEMOD_BAD_ARG;
-    size_t w = windows_for(st, st->carry.size() + n_frames);
+    const size_t fresh = n_frames > st->skip ? n_frames - st->skip : 0;
+    size_t w = windows_for(st, st->carry.size() + fresh);
     return w > 0x7FFFFFFF ? 0x7FFFFFFF : (int)w;
 }
 
@@ -417,7 +445,6 @@ static int enqueue_batch(demod_t *st, const int16_t *d_pcm, size_t n_windows, ui
                          float *d_mag, hipStream_t s)
 {
     if (n_windows == 0) return 0;
-    HIP_TRY(hipSetDevice(st->device));
     if (st->detector == kDetFft) return enqueue_fft(st, d_pcm, n_windows, d_sym, d_mag, nullptr, s);
     GoertzelParams p;
     std::memset(&p, 0, sizeof(p));
@@ -519,7 +546,7 @@ static int run_host_small(demod_t *st, const int16_t *pcm, size_t n_samples, siz
     int rc;
     if ((rc = ensure_dev(st, n_samples, n_windows, mags != nullptr)) != DEMOD_OK) return rc;
     if ((rc = ensure_host(st, kSmallHostSamples, kSmallHostSamples / 8)) != DEMOD_OK) return rc;
-    std::memcpy(st->h_in, pcm, n_samples * sizeof(int16_t));
+    if (pcm != st->h_in) std::memcpy(st->h_in, pcm, n_samples * sizeof(int16_t));
     HIP_TRY(hipMemcpyAsync(st->d_in, st->h_in, n_samples * sizeof(int16_t), hipMemcpyHostToDevice,
                            st->stream));
     rc = enqueue_batch(st, st->d_in, n_windows, st->d_sym, mags ? st->d_mag : nullptr, st->stream);
@@ -581,7 +608,8 @@ int demod_batch(demod_t *st, const int16_t *pcm, size_t n_windows, uint8_t *symb
     if (n_windows > 0x7FFFFFFF) return DEMOD_BAD_ARG;
     if (n_windows == 0) return 0;
     if (((uintptr_t)pcm & 15) != 0) return DEMOD_BAD_ARG;
-    HIP_TRY(hipSetDevice(st->device));
+    DeviceGuard guard(st->device);
+    HIP_TRY(guard.err);
     const size_t n_samples = (n_windows - 1) * st->cfg.hop + st->cfg.n;
     const bool din = is_device_ptr(pcm), dsym = is_device_ptr(symbols);
     const bool dmag = mags ? is_device_ptr(mags) : dsym;
@@ -601,6 +629,9 @@ int demod_batch_async(demod_t *st, const int16_t *d_pcm, size_t n_windows, uint8
     if (!st || (!d_pcm && n_windows) || (!d_symbols && n_windows)) return DEMOD_BAD_ARG;
     if (n_windows > 0x7FFFFFFF) return DEMOD_BAD_ARG;
     if (((uintptr_t)d_pcm & 15) != 0) return DEMOD_BAD_ARG;
+    if (n_windows == 0) return 0;
+    DeviceGuard guard(st->device);
+    HIP_TRY(guard.err);
     return enqueue_batch(st, d_pcm, n_windows, d_symbols, d_mags, (hipStream_t)stream);
 }
 
@@ -612,7 +643,8 @@ int demod_batch_spectrum_async(demod_t *st, const int16_t *d_pcm, size_t n_windo
     if (n_windows > 0x7FFFFFFF) return DEMOD_BAD_ARG;
     if (((uintptr_t)d_pcm & 15) != 0) return DEMOD_BAD_ARG;
     if (n_windows == 0) return 0;
-    HIP_TRY(hipSetDevice(st->device));
+    DeviceGuard guard(st->device);
+    HIP_TRY(guard.err);
     return enqueue_fft(st, d_pcm, n_windows, d_symbols, d_mags, d_spectrum, (hipStream_t)stream);
 }
 
@@ -621,17 +653,35 @@ int demodulate_mags(demod_t *st, const int16_t *pcm, size_t n_frames, uint8_t *s
 {
     if (!st || (!pcm && n_frames)) return DEMOD_BAD_ARG;
     const demod_cfg_t &c = st->cfg;
+    // lead-in (cfg.lead_in): the first frames of a stream are dropped, e.g. the
+    // Opus decoder delay (OPUS_GET_LOOKAHEAD, 312 samples at 48 kHz for the
+    // transmitter's settings, OpusEncoder.kt:65-67), so windows line up with
+    // the transmitter's symbol boundaries
+    const size_t drop = std::min(st->skip, n_frames);
+    pcm += drop * c.channels;
+    n_frames -= drop;
     const size_t have = st->carry.size();
     const size_t total = have + n_frames;
     const size_t W = windows_for(st, total);
     if (W > max_symbols) return DEMOD_BUFFER_TOO_SMALL;
     if (W && !symbols) return DEMOD_BAD_ARG;
     if (W > 0x7FFFFFFF) return DEMOD_BAD_ARG;
+    DeviceGuard guard(st->device);
+    HIP_TRY(guard.err);
     // Mono view: carried samples followed by the new frames' selected channel.
-    std::vector<int16_t> &m = st->scratch;
-    m.resize(total);
-    if (have) std::memcpy(m.data(), st->carry.data(), have * sizeof(int16_t));
-    int16_t *dst = m.data() + have;
+    // Packet-sized calls (the playback.cpp:118 position: 2880 frames) build it
+    // straight in the pinned staging buffer the small-call path copies from.
+    int16_t *m = nullptr;
+    if (W && total <= kSmallHostSamples) {
+        int rc = ensure_host(st, kSmallHostSamples, kSmallHostSamples / 8);
+        if (rc != DEMOD_OK) return rc;
+        m = st->h_in;
+    } else {
+        st->scratch.resize(total);
+        m = st->scratch.data();
+    }
+    if (have) std::memcpy(m, st->carry.data(), have * sizeof(int16_t));
+    int16_t *dst = m + have;
     if (c.channels == 1) {
         if (n_frames) std::memcpy(dst, pcm, n_frames * sizeof(int16_t));
     } else if (c.channel_mode == DEMOD_CH_DOWNMIX) {
@@ -642,13 +692,13 @@ int demodulate_mags(demod_t *st, const int16_t *pcm, size_t n_frames, uint8_t *s
         for (size_t i = 0; i < n_frames; ++i) dst[i] = pcm[2 * i + ch];
     }
     if (W) {
-        HIP_TRY(hipSetDevice(st->device));
         const size_t used = (W - 1) * c.hop + c.n;
-        int rc = run_host(st, m.data(), used, W, symbols, mags);
+        int rc = run_host(st, m, used, W, symbols, mags);
         if (rc < 0) return rc;  // nothing consumed on failure
     }
     const size_t consumed = W * c.hop;
-    st->carry.assign(m.begin() + consumed, m.end());
+    st->carry.assign(m + consumed, m + total);
+    st->skip -= drop;
     return (int)W;
 }
 
@@ -665,17 +715,10 @@ int demod_synth_fsk(const demod_cfg_t *cfg, uint64_t seed, uint64_t w0, size_t n
     if (!(cfg->fs > 0.0) || !d_pcm || ((uintptr_t)d_pcm & 15)) return DEMOD_BAD_ARG;
     if (amplitude < 0 || amplitude > 32767 || sigma < 0 || sigma > 32767) return DEMOD_BAD_ARG;
     if (n_windows == 0) return DEMOD_OK;
-    static int16_t *d_lut[64] = {nullptr};
-    int dev = 0;
-    HIP_TRY(hipGetDevice(&dev));
-    if (dev < 0 || dev >= 64) return DEMOD_BAD_ARG;
-    if (!d_lut[dev]) {
-        std::vector<int16_t> lut(16384);
-        for (int i = 0; i < 16384; ++i)
-            lut[i] = (int16_t)std::lrint(32767.0 * std::sin(2.0 * M_PI * (double)i / 16384.0));
-        HIP_TRY(hipMalloc(&d_lut[dev], lut.size() * sizeof(int16_t)));
-        HIP_TRY(hipMemcpy(d_lut[dev], lut.data(), lut.size() * sizeof(int16_t), hipMemcpyHostToDevice));
-    }
+    if (cfg->device < 0 || cfg->device >= kMaxDevices) return DEMOD_BAD_ARG;
+    DeviceGuard guard(cfg->device);
+    HIP_TRY(guard.err);
+    HIP_TRY(synth_prepare());  // sine table on the current device (once, locked)
     SynthParams p;
     std::memset(&p, 0, sizeof(p));
     p.seed = seed;
@@ -685,7 +728,6 @@ int demod_synth_fsk(const demod_cfg_t *cfg, uint64_t seed, uint64_t w0, size_t n
     p.k = (int)cfg->k;
     p.amplitude = amplitude;
     p.sigma = sigma;
-    p.lut = d_lut[dev];
     p.pcm = d_pcm;
     p.sym = d_symbols;
     for (uint32_t t = 0; t < cfg->k; ++t)
@@ -738,13 +780,7 @@ int demod_read_ceiling_async(const void *d_buf, size_t n_bytes, void *stream)
 {
     if (!d_buf || ((uintptr_t)d_buf & 15) || (n_bytes % 8192)) return DEMOD_BAD_ARG;
     if (n_bytes == 0) return DEMOD_OK;
-    static unsigned *d_sink[64] = {nullptr};
-    int dev = 0;
-    HIP_TRY(hipGetDevice(&dev));
-    if (dev < 0 || dev >= 64) return DEMOD_BAD_ARG;
-    if (!d_sink[dev]) HIP_TRY(hipMalloc(&d_sink[dev], 64));
-    HIP_TRY(launch_read_ceiling((const int16_t *)d_buf, (long long)n_bytes, d_sink[dev],
-                                (hipStream_t)stream));
+    HIP_TRY(launch_read_ceiling((const int16_t *)d_buf, (long long)n_bytes, (hipStream_t)stream));
     return DEMOD_OK;
 }
 

@@ -17,6 +17,7 @@ constexpr int kPlainWPB = 2;
 constexpr int kLdsSegStride = 144;    // bytes: 128 B segment + 16 B pad (conflict-free b128 reads)
 constexpr int kLdsWaveBytes = 64 * kLdsSegStride;
 constexpr int kMaxTones = 16;
+constexpr int kMaxDevices = 64;       // device ordinals the module tables cover
 
 // Uniform per-launch parameters (kernarg -> SGPRs).
 struct GoertzelParams {
@@ -84,7 +85,6 @@ struct SynthParams {
     int k;
     int amplitude;
     int sigma;
-    const int16_t *lut;      // 16384-entry Q15 sine table (device)
     int16_t *pcm;
     uint8_t *sym;
     uint32_t inc[kMaxTones];  // phase increment per sample, 2^32 / cycle
@@ -101,8 +101,9 @@ hipError_t launch_detector(int detector, const GoertzelParams &p, hipStream_t s)
 const void *residue_kernel_ptr(int k, int log2g, bool dcls = false);
 size_t residue_lds_bytes(int k, int log2g, int qp = 2);
 int tile_grid(long long n_windows, int log2g, int wpb = kWavesPerBlock);
+hipError_t synth_prepare();  // upload the sine table to the current device (once, locked)
 hipError_t launch_synth(const SynthParams &p, hipStream_t s);
-hipError_t launch_read_ceiling(const int16_t *p, long long n_bytes, unsigned *sink, hipStream_t s);
+hipError_t launch_read_ceiling(const int16_t *p, long long n_bytes, hipStream_t s);
 hipError_t launch_fft_quad(const FftParams &p, hipStream_t s);  // 16 lanes / window (fft_quad.hip)
 // ip.proto framing of [n_streams][n] symbols, one frame run per stream (frame_gpu.hip)
 long long frame_streams_size(long long n, int bits, long long max_payload, unsigned *per,

@@ -4,9 +4,40 @@
 // (DESIGN.md §Synthetic input), evaluated 8 samples per thread: splitmix64 is
 // counter-based, so any sample is generated independently and the bytes are
 // identical to the CPU generator's (tests/test_gpu_parity.py checks this).
+#include <cmath>
+#include <mutex>
+#include <vector>
+
 #include "demod_internal.h"
 
 namespace fskd {
+
+// Module-scope device tables: one copy per device, owned (and freed) by the
+// HIP runtime with the code object, so the library keeps no process-global
+// heap allocations. The sine table is filled once per device under a lock
+// (synth_prepare); the sink only keeps the read-ceiling loads alive.
+__device__ int16_t g_sine_lut[16384];
+__device__ unsigned g_ceiling_sink[16];
+
+hipError_t synth_prepare()
+{
+    static std::mutex mu;
+    static bool ready[kMaxDevices] = {};
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    if (dev < 0 || dev >= kMaxDevices) return hipErrorInvalidDevice;
+    std::lock_guard<std::mutex> lock(mu);
+    if (ready[dev]) return hipSuccess;
+    // the Q15 sine table of oracle/fsk_oracle.c:oracle_sine_lut
+    std::vector<int16_t> lut(16384);
+    for (int i = 0; i < 16384; ++i)
+        lut[i] = (int16_t)std::lrint(32767.0 * std::sin(2.0 * M_PI * (double)i / 16384.0));
+    e = hipMemcpyToSymbol(HIP_SYMBOL(g_sine_lut), lut.data(), lut.size() * sizeof(int16_t), 0,
+                          hipMemcpyHostToDevice);
+    if (e == hipSuccess) ready[dev] = true;
+    return e;
+}
 
 __device__ __forceinline__ uint64_t mix64(uint64_t z)
 {
@@ -38,7 +69,7 @@ __global__ __launch_bounds__(256) void synth_kernel(SynthParams p)
     for (int r = 0; r < 8; ++r) {
         const uint32_t s = (uint32_t)(s0 + r);
         const uint32_t ph = phase0 + s * inc;
-        const int32_t tone = (p.amplitude * (int32_t)p.lut[ph >> 18] + 16384) >> 15;
+        const int32_t tone = (p.amplitude * (int32_t)g_sine_lut[ph >> 18] + 16384) >> 15;
         const uint64_t d = mix64(ns + ((uint64_t)s + 1) * gamma);
         const int64_t u = (int64_t)((d & 0xFFFF) + ((d >> 16) & 0xFFFF) +
                                     ((d >> 32) & 0xFFFF) + (d >> 48));
@@ -75,8 +106,7 @@ typedef unsigned int u32x4s __attribute__((ext_vector_type(4)));
 // non-temporal buffer loads and discards it, i.e. the tile kernels' access
 // pattern with no compute and no stores. Its bandwidth on the box at hand is
 // the practical ceiling the detector kernels are compared with.
-__global__ __launch_bounds__(256) void read_ceiling_kernel(const int16_t *p, long long n_tiles,
-                                                           unsigned *sink)
+__global__ __launch_bounds__(256) void read_ceiling_kernel(const int16_t *p, long long n_tiles)
 {
     const int lane = threadIdx.x & 63;
     const long long t = (long long)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -89,16 +119,16 @@ __global__ __launch_bounds__(256) void read_ceiling_kernel(const int16_t *p, lon
         const u32x4s v = __builtin_amdgcn_raw_buffer_load_b128(rs, (64 * i + lane) * 16, 0, 2);
         acc ^= v.x ^ v.y ^ v.z ^ v.w;
     }
-    if (acc == 0x9E3779B9u) sink[0] = acc;  // keeps the loads; practically never stores
+    if (acc == 0x9E3779B9u) g_ceiling_sink[lane & 15] = acc;  // keeps the loads; practically never stores
 }
 
-hipError_t launch_read_ceiling(const int16_t *p, long long n_bytes, unsigned *sink, hipStream_t s)
+hipError_t launch_read_ceiling(const int16_t *p, long long n_bytes, hipStream_t s)
 {
     const long long n_tiles = n_bytes / 8192;
     if (n_tiles <= 0) return hipSuccess;
     const long long blocks = (n_tiles + 3) / 4;
     if (blocks > 0x7FFFFFFFLL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(read_ceiling_kernel, dim3((unsigned)blocks), dim3(256), 0, s, p, n_tiles, sink);
+    hipLaunchKernelGGL(read_ceiling_kernel, dim3((unsigned)blocks), dim3(256), 0, s, p, n_tiles);
     return hipGetLastError();
 }
 

@@ -11,15 +11,18 @@
 // 8 + 4 + 2 + 1 pairs x (2 selects + 1 DPP add) = 45 instructions instead of
 // 64, and lane l ends with the window total of value l (re_k in lane 2k, im_k
 // in lane 2k + 1): |X_k|^2 is one square plus one DPP add for all tones, the
-// magnitudes go out as one coalesced store, and the argmax is 4 DPP max
-// steps on a packed (power, tone) key.
+// magnitudes go out as one coalesced store, and the argmax is two passes of
+// 4 DPP max steps (ws_argmax).
 //
-// Decision key: the power's IEEE bits (non-negative, so unsigned order is
-// numeric order) with the low 4 mantissa bits replaced by 15 - k, so the
-// unsigned max picks the largest power and, among powers equal in their top
-// 28 bits, the lowest tone (the oracle's tie rule). Two powers within 2^-19
-// relative of each other (2e-6, below the fp32 error of the powers
-// themselves) are treated as a tie.
+// Decision (ws_argmax): the exact argmax of the fp32 powers the kernel
+// stores, ties to the lowest tone index — the same rule as the K <= 2 path's
+// sequential `P > best` and the oracle's (oracle/fsk_oracle.c
+// goertzel_window_d). Two DPP max passes over the 16-lane row: the largest
+// power's IEEE bits (P >= 0, so unsigned order is numeric order), then the
+// lowest tone among the lanes holding exactly that power. (Round 1 packed
+// both into one key by overwriting the low 4 mantissa bits with the tone, which
+// resolved powers within 2^-19 relative to the lower tone even when the
+// higher one was strictly larger.)
 #pragma once
 #include "demod_internal.h"
 
@@ -84,6 +87,30 @@ __device__ __forceinline__ void ws_stage(float (&v)[V], int lane)
     }
 }
 
+// Exact argmax over a 16-lane row (one window): lane candidates (bits of a
+// power P >= 0, ok, tone index o); a second candidate per lane when TWO (K > 8).
+// Returns the winning tone in every lane of the row: the largest P, and among
+// equal P the lowest o.
+template <bool TWO>
+__device__ __forceinline__ unsigned ws_argmax(unsigned pb0, bool ok0, int o0, unsigned pb1 = 0u,
+                                              bool ok1 = false, int o1 = 0)
+{
+    unsigned m = ok0 ? pb0 : 0u;
+    if constexpr (TWO) m = max(m, ok1 ? pb1 : 0u);
+    m = max(m, ws_dpp_u<0xB1>(m));
+    m = max(m, ws_dpp_u<0x4E>(m));
+    m = max(m, ws_dpp_u<0x141>(m));
+    m = max(m, ws_dpp_u<0x140>(m));
+    // every lane now holds the row's max; key 16 - o marks the lanes holding it
+    unsigned key = (ok0 && pb0 == m) ? (unsigned)(16 - o0) : 0u;
+    if constexpr (TWO) key = max(key, (ok1 && pb1 == m) ? (unsigned)(16 - o1) : 0u);
+    key = max(key, ws_dpp_u<0xB1>(key));
+    key = max(key, ws_dpp_u<0x4E>(key));
+    key = max(key, ws_dpp_u<0x141>(key));
+    key = max(key, ws_dpp_u<0x140>(key));
+    return 16u - key;
+}
+
 // X[k] = this lane's partial (re, im) of tone k. Writes the symbol of window
 // w (lane j == 0) and, if mag, its K magnitudes; `live` = w is a real window.
 // PERM: the kernel's tone slot s holds the host's tone (perm >> 4 s) & 15
@@ -128,16 +155,9 @@ __device__ __forceinline__ void window_sum_decide(const float (&re)[K], const fl
         if (ok0) mag[w * K + o0] = P0;
         if (ok1) mag[w * K + o1] = P1;
     }
-    unsigned key = ok0 ? ((__float_as_uint(P0) & ~15u) | (unsigned)(15 - o0)) : 0u;
-    if constexpr (V > 16) {
-        const unsigned k1 = ok1 ? ((__float_as_uint(P1) & ~15u) | (unsigned)(15 - o1)) : 0u;
-        key = key > k1 ? key : k1;
-    }
-    key = max(key, ws_dpp_u<0xB1>(key));
-    key = max(key, ws_dpp_u<0x4E>(key));
-    key = max(key, ws_dpp_u<0x141>(key));
-    key = max(key, ws_dpp_u<0x140>(key));
-    if (live && j == 0) sym[w] = (uint8_t)(15 - (key & 15u));
+    const unsigned arg = ws_argmax<(V > 16)>(__float_as_uint(P0), ok0, o0, __float_as_uint(P1),
+                                             ok1, o1);
+    if (live && j == 0) sym[w] = (uint8_t)arg;
 }
 
 // The same epilogue for K = 8 when the kernel has already split the tones by
@@ -169,12 +189,8 @@ __device__ __forceinline__ void window_sum_decide_split8(const float (&re)[4], c
     const float P0 = sq + ws_dpp<0xB1>(sq);
     const int o0 = PERM ? (int)((perm >> (4 * t0)) & 15u) : t0;
     if (live && mag && re_lane) mag[w * K + o0] = P0;
-    unsigned key = re_lane ? ((__float_as_uint(P0) & ~15u) | (unsigned)(15 - o0)) : 0u;
-    key = max(key, ws_dpp_u<0xB1>(key));
-    key = max(key, ws_dpp_u<0x4E>(key));
-    key = max(key, ws_dpp_u<0x141>(key));
-    key = max(key, ws_dpp_u<0x140>(key));
-    if (live && j == 0) sym[w] = (uint8_t)(15 - (key & 15u));
+    const unsigned arg = ws_argmax<false>(__float_as_uint(P0), re_lane, o0);
+    if (live && j == 0) sym[w] = (uint8_t)arg;
 }
 
 }  // namespace fskd

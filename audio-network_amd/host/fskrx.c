@@ -7,14 +7,17 @@
  * protobuf_async.kt:110-114).
  *
  *   fskrx [-c 1|2] [-m left|right|downmix] [-f f1,f2,...] [-n N] [-H hop]
- *         [-M auto|goertzel|folded|fft] [-p frames_per_read] [-b] < pcm > frames
- *   fskrx [same options] -l tcp_port [-u udp_port] [-a addr] [-N name] [-1] > frames
+ *         [-M auto|goertzel|folded|fft] [-L lead_in] [-p frames_per_read] [-b] < pcm > frames
+ *   fskrx [same options] -l tcp_port -r [-u udp_port] [-a addr] [-N name] [-1] > frames
  *
  * Default: 48 kHz mono, N = hop = 1024, 2-FSK at 1500/3000 Hz, reads of 2880
  * frames (one 60 ms packet) each passed to demodulate(). -b reads all input
  * first and makes one demodulate() call (the chunked host-buffer path).
- * Symbols are framed MSB-first, ceil(log2 K) bits each, 4096-byte payloads;
- * the final partial payload is flushed at EOF. Statistics go to stderr.
+ * -L drops the stream's first lead_in frames (demod_cfg_t.lead_in, e.g. 312
+ * for PCM that came out of an Opus decoder, DEMOD_OPUS_LOOKAHEAD).
+ * Symbols are framed MSB-first, ceil(log2 K) bits each, 4096-byte payloads
+ * (one demod_frame_symbols call per payload); the final partial payload is
+ * flushed at EOF. Statistics go to stderr.
  * Exit status: 0 ok, 2 usage, 3 demod_create failed (e.g. no gfx950 device:
  * there is no CPU fallback), 4 demodulation / framing error, 5 I/O error.
  *
@@ -26,12 +29,19 @@
  * ToReceiver frames until the transmitter closes or sends a frame nanopb
  * would reject (network.cpp:409-430). One transmitter at a time, like the
  * firmware. With -u it also answers UDP discovery requests
- * (network.cpp:449-494). The AudioData bytes are taken as raw int16 LE PCM of
- * the configured channel layout: Opus decoding is outside this build (the
- * reference libopus needs an ESP32 header this image lacks),
- * so a transmitter feeds PCM through the same frame layout. -1 exits after
- * the first transmitter disconnects. The bound ports are printed on stderr
- * as "fskrx: listening tcp <port> udp <port>".
+ * (network.cpp:449-494). In the reference the AudioData bytes are an Opus
+ * packet (MulticastAudioOutput.kt:124-130); Opus decoding is outside this
+ * build (the reference libopus needs an ESP32 header this image lacks,
+ * DESIGN.md §8), so a transmitter can only feed raw int16 LE PCM of the
+ * configured channel layout through the same frame layout, and only when -r
+ * says so. Without -r the first AudioData frame is refused — ToTransmitter
+ * {error{audio_decode_error}} (ip.proto:56-61), then the connection is
+ * closed — instead of demodulating Opus bytes as noise. With -r a payload
+ * that is not a whole number of PCM frames (an Opus packet, or a torn
+ * sample) is refused the same way (reported as DEMOD_BAD_ARG). A refused
+ * stream makes the exit status 4. -1 exits after the first transmitter
+ * disconnects. The bound ports are printed on stderr as
+ * "fskrx: listening tcp <port> udp <port>".
  */
 #define _POSIX_C_SOURCE 200112L
 #include <arpa/inet.h>
@@ -51,9 +61,12 @@
 static int usage(void)
 {
     fprintf(stderr, "usage: fskrx [-c 1|2] [-m left|right|downmix] [-f f1,f2,...] [-n N] "
-                    "[-H hop] [-M auto|goertzel|folded|residue|fft] [-p frames] [-b] < pcm > frames\n"
-                    "       fskrx [options] -l tcp_port [-u udp_port] [-a addr] [-N name] [-1] "
-                    "> frames\n");
+                    "[-H hop] [-M auto|goertzel|folded|residue|fft] [-L lead_in] [-p frames] [-b] "
+                    "< pcm > frames\n"
+                    "       fskrx [options] -l tcp_port -r [-u udp_port] [-a addr] [-N name] [-1] "
+                    "> frames\n"
+                    "  -r: AudioData payloads are raw int16 PCM (this receiver does not decode "
+                    "Opus; without -r audio is refused)\n");
     return 2;
 }
 
@@ -67,17 +80,22 @@ struct sink {
     unsigned long long frames, bytes, symbols;
 };
 
+/* Frame the first cnt buffered symbols, one payload (<= per symbols) per
+ * demod_frame_symbols call, so s->frame only ever holds one frame. */
 static int sink_emit(struct sink *s, size_t cnt)
 {
-    long long w = demod_frame_symbols(s->sym, cnt, s->bits, DEMOD_MAX_FRAME_PAYLOAD, s->frame,
-                                      s->frame_cap);
-    if (w < 0) {
-        fprintf(stderr, "fskrx: framing: %s\n", demod_strerror((int)w));
-        return 4;
+    for (size_t at = 0; at < cnt; at += s->per) {
+        const size_t c = cnt - at < s->per ? cnt - at : s->per;
+        long long w = demod_frame_symbols(s->sym + at, c, s->bits, DEMOD_MAX_FRAME_PAYLOAD,
+                                          s->frame, s->frame_cap);
+        if (w < 0) {
+            fprintf(stderr, "fskrx: framing: %s\n", demod_strerror((int)w));
+            return 4;
+        }
+        if (fwrite(s->frame, 1, (size_t)w, stdout) != (size_t)w) return 5;
+        s->frames += 1;
+        s->bytes += (unsigned long long)w;
     }
-    if (fwrite(s->frame, 1, (size_t)w, stdout) != (size_t)w) return 5;
-    s->frames += (cnt + s->per - 1) / s->per;
-    s->bytes += (unsigned long long)w;
     memmove(s->sym, s->sym + cnt, s->n - cnt);
     s->n -= cnt;
     return 0;
@@ -106,6 +124,7 @@ struct net {
     int tcp_port, udp_port; /* udp_port < 0: no discovery responder */
     const char *name;
     int once;
+    int raw_pcm; /* -r: AudioData payloads are raw PCM (else audio is refused) */
 };
 
 static int bind_socket(int type, const char *addr, int port, int *bound)
@@ -194,7 +213,7 @@ static int serve(demod_t *st, const demod_cfg_t *cfg, struct sink *s, const stru
     uint8_t *in = malloc(in_cap), *pcm = malloc(pcm_cap), *sym = NULL;
     size_t sym_cap = 0;
     int cfd = -1, rc = (in && pcm) ? 0 : 4, done = 0;
-    unsigned long long clients = 0, answered = 0;
+    unsigned long long clients = 0, answered = 0, refused = 0;
     while (!rc && !done) {
         struct pollfd pf[2];
         int np = 0;
@@ -262,6 +281,25 @@ static int serve(demod_t *st, const demod_cfg_t *cfg, struct sink *s, const stru
                 end_stream = 1;
                 break;
             }
+            if (!nt->raw_pcm || pl_len % frame_bytes) {
+                /* Opus bytes (or a torn PCM frame): refuse rather than
+                 * demodulate noise; tell the transmitter (ip.proto:56-61) */
+                if (!nt->raw_pcm)
+                    fprintf(stderr, "fskrx: AudioData carries Opus in the reference and this "
+                                    "receiver does not decode Opus (-r: raw PCM payloads); "
+                                    "refusing the stream\n");
+                else
+                    fprintf(stderr, "fskrx: AudioData payload of %zu bytes is not whole %zu-byte "
+                                    "PCM frames (%s); refusing the stream\n",
+                            pl_len, frame_bytes, demod_strerror(DEMOD_BAD_ARG));
+                demod_receiver_error_t re = {0, 1};
+                uint8_t eb[16];
+                int w = demod_receiver_error_encode(&re, eb, sizeof eb);
+                if (w > 0) (void)send_all(cfd, eb, (size_t)w);
+                ++refused;
+                end_stream = 1;
+                break;
+            }
             if (pcm_len + pl_len > pcm_cap) {
                 uint8_t *p = realloc(pcm, pcm_cap * 2 + pl_len);
                 if (!p) { rc = 4; break; }
@@ -287,8 +325,10 @@ static int serve(demod_t *st, const demod_cfg_t *cfg, struct sink *s, const stru
             done = nt->once;
         }
     }
-    fprintf(stderr, "fskrx: %llu transmitter(s) served, %llu discovery request(s) answered\n",
-            clients, answered);
+    fprintf(stderr,
+            "fskrx: %llu transmitter(s) served, %llu refused, %llu discovery request(s) answered\n",
+            clients, refused, answered);
+    if (!rc && refused) rc = 4;
     if (cfd >= 0) close(cfd);
     close(lfd);
     if (ufd >= 0) close(ufd);
@@ -304,12 +344,13 @@ int main(int argc, char **argv)
     demod_cfg_default(&cfg);
     size_t per_read = 2880; /* one 60 ms packet at 48 kHz (playback.cpp:10) */
     int batch = 0;
-    struct net nt = {"0.0.0.0", -1, -1, "", 0};
+    struct net nt = {"0.0.0.0", -1, -1, "", 0, 0};
     for (int i = 1; i < argc; ++i) {
         const char *a = argv[i];
         const char *v = i + 1 < argc ? argv[i + 1] : NULL;
         if (!strcmp(a, "-b")) { batch = 1; continue; }
         if (!strcmp(a, "-1")) { nt.once = 1; continue; }
+        if (!strcmp(a, "-r")) { nt.raw_pcm = 1; continue; }
         if (!v) return usage();
         ++i;
         if (!strcmp(a, "-c")) cfg.channels = (uint32_t)atoi(v);
@@ -320,6 +361,7 @@ int main(int argc, char **argv)
         else if (!strcmp(a, "-n")) cfg.n = (uint32_t)atoi(v);
         else if (!strcmp(a, "-H")) cfg.hop = (uint32_t)atoi(v);
         else if (!strcmp(a, "-p")) per_read = (size_t)strtoull(v, NULL, 10);
+        else if (!strcmp(a, "-L")) cfg.lead_in = (uint32_t)strtoul(v, NULL, 10);
         else if (!strcmp(a, "-m")) {
             if (!strcmp(v, "left")) cfg.channel_mode = DEMOD_CH_LEFT;
             else if (!strcmp(v, "right")) cfg.channel_mode = DEMOD_CH_RIGHT;
@@ -346,7 +388,7 @@ int main(int argc, char **argv)
             return usage();
         }
     }
-    if (per_read == 0 || (nt.tcp_port < 0 && (nt.udp_port >= 0 || nt.once)) ||
+    if (per_read == 0 || (nt.tcp_port < 0 && (nt.udp_port >= 0 || nt.once || nt.raw_pcm)) ||
         strlen(nt.name) >= DEMOD_INFO_STRING_CAP)
         return usage();
 
@@ -360,7 +402,7 @@ int main(int argc, char **argv)
     memset(&s, 0, sizeof s);
     s.bits = demod_bits_per_symbol(cfg.k);
     s.per = (size_t)DEMOD_MAX_FRAME_PAYLOAD * 8 / (size_t)s.bits;
-    s.frame_cap = demod_frame_size(DEMOD_MAX_FRAME_PAYLOAD) * 2 + 64;
+    s.frame_cap = demod_frame_size(DEMOD_MAX_FRAME_PAYLOAD); /* one frame per call */
     s.frame = malloc(s.frame_cap);
     int rc = s.frame ? 0 : 4;
 

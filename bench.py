@@ -17,14 +17,22 @@ roofline = algorithmic bytes per launch (2048 B in + 1 B symbol + 4K B
 magnitudes per window) / mean kernel duration from HIP events
 recorded on the launch stream, vs the 8 TB/s HBM peak. traffic = HBM bytes per
 launch from the committed rocprofv3 PMC summary (profiles/), or null.
-cpu_baseline = the oracle's C restatement (OpenMP over the host cores) on a
-bounded sample of the same windows (rank 0, N = 1 only), which also re-checks
-parity of the timed GPU output on that sample.
+cpu_baseline = the oracle's C restatement (OpenMP over the host cores this
+process may use) on a bounded sample of the same windows (rank 0, N = 1 only),
+median of >= 5 timed repetitions; its output doubles as a parity check of the
+timed GPU output on that sample (parity_sample, with the top-2 decision-margin
+histogram SURVEY §7 asks for, at sigma 400 and at the sigma 2000 stress level).
+
+At N = 1 the default run also measures configs[2] (8-FSK) and configs[3]
+(sliding FFT, hop 256) with the same steps/warmup and reports them under
+"fsk8" and "fft_hop256" (no CPU baseline for those).
 """
 import argparse
 import importlib.util
 import json
+import math
 import os
+import socket
 import sys
 import time
 
@@ -35,6 +43,7 @@ HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 VALU_PEAK_TFLOPS = 157.3  # MI355X fp32 vector peak (MI355X_MICROARCH.md)
 METRIC = "PCM Msamples/s demodulated + symbol-error-rate vs reference, 1/2/4/8 MI355X"
 MIN_WARMUP = 64
+MARGIN_BAND = 4e-5  # 4 x the 1e-5 magnitude bar: decisions closer than this are fp32-ill-posed
 
 
 def load_pkg():
@@ -74,10 +83,51 @@ def cpu_model() -> str:
     return "unknown"
 
 
-def cpu_baseline(A, d_pcm, d_sym, d_mag, freqs, seconds: float, threads: int, fft: bool,
-                 hop: int):
+def cpu_share():
+    """(cpus this process may run on, cgroup CPU quota in cores or None,
+    threads to use, why). The GPU box hands each GPU a share of the host:
+    os.cpu_count() shows the whole machine, sched_getaffinity and the cgroup
+    quota show what this process can actually use."""
+    visible = os.cpu_count() or 1
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = visible
+    quota = None
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(p)
+    except (OSError, ValueError):
+        pass
+    threads = affinity
+    why = "all cpus in this process's affinity mask"
+    if quota is not None and math.ceil(quota) < threads:
+        threads = max(1, math.ceil(quota))
+        why = f"cgroup cpu.max quota of {quota:g} cores (more threads would only be throttled)"
+    return visible, affinity, quota, threads, why
+
+
+def margin_stats(P: np.ndarray) -> dict:
+    """Top-2 decision margin (P1 - P2) / P1 per window: min, count inside the
+    fp32-ill-posed band, and a log-binned histogram."""
+    if P.shape[1] < 2 or not len(P):
+        return {}
+    Ps = np.sort(P, axis=1)
+    m = (Ps[:, -1] - Ps[:, -2]) / np.maximum(Ps[:, -1], 1e-300)
+    edges = [0.0, 1e-6, 1e-5, 1e-4, 1e-3, 1e-2, 1e-1, 1.0 + 1e-12]
+    hist, _ = np.histogram(m, bins=edges)
+    return {"windows": int(m.size), "min_margin": float(m.min()),
+            "below_4e-5": int((m < MARGIN_BAND).sum()),
+            "hist_edges": ["0", "1e-6", "1e-5", "1e-4", "1e-3", "1e-2", "1e-1", "1"],
+            "hist_counts": [int(c) for c in hist]}
+
+
+def cpu_baseline(d_pcm, d_sym, d_mag, freqs, seconds: float, threads: int, fft: bool, hop: int,
+                 reps: int = 7):
     """Oracle (C, OpenMP) on a bounded sample of the timed windows: the first
-    S stream windows (Goertzel) or the FFT windows over the first S*n samples."""
+    S stream windows (Goertzel) or the FFT windows over the first S*n samples.
+    Rate = median over `reps` repetitions of ~seconds/reps each."""
     sys.path.insert(0, ROOT)
     from oracle import oracle as O
 
@@ -88,46 +138,330 @@ def cpu_baseline(A, d_pcm, d_sym, d_mag, freqs, seconds: float, threads: int, ff
     gsym = d_sym[:n_win].cpu().numpy()
     gmag = d_mag[:n_win].cpu().numpy().astype(np.float64) if d_mag is not None else None
 
-    def run():
+    def run(x, th):
         if fft:
-            return O.fft_demod(flat, freqs, n, hop, threads=threads)
-        return O.goertzel(flat, freqs, n, hop, threads=threads)
+            return O.fft_demod(x, freqs, n, hop, threads=th)
+        return O.goertzel(x, freqs, n, hop, threads=th)
 
-    def timed(fn, budget):
-        passes, t0 = 0, time.perf_counter()
-        while True:
-            fn()
-            passes += 1
-            el = time.perf_counter() - t0
-            if el >= budget:
-                return passes, el
+    def rep_rates(fn, samples, budget, nrep):
+        rates = []
+        for _ in range(nrep):
+            passes, t0 = 0, time.perf_counter()
+            while True:
+                fn()
+                passes += 1
+                el = time.perf_counter() - t0
+                if el >= budget:
+                    break
+            rates.append(passes * samples / el / 1e6)
+        return rates
 
-    sym, P = run()  # warm + parity reference
-    passes, el = timed(run, seconds)
-    msps = passes * S * n / el / 1e6
-    # single-thread rate on a slice of the same sample (SURVEY §8d asks for both)
+    sym, P = run(flat, threads)  # warm + parity reference
+    rates = rep_rates(lambda: run(flat, threads), S * n, seconds / reps, reps)
+    # single-thread double and fp32 rates on a slice of the same sample
     S1 = max(1, S // 16)
     flat1 = flat[:S1 * n]
-    fn1 = ((lambda: O.fft_demod(flat1, freqs, n, hop, threads=1)) if fft else
-           (lambda: O.goertzel(flat1, freqs, n, hop, threads=1)))
-    p1, el1 = timed(fn1, max(1.0, seconds / 5))
-    msps1 = p1 * S1 * n / el1 / 1e6
-    # ... and the fp32 variant of the scalar recurrence, hop = n only
-    msps1_f32 = None
+    r1 = rep_rates(lambda: run(flat1, 1), S1 * n, max(0.2, seconds / 25), 5)
+    r1f = None
     if not fft and hop == n:
-        pf, elf = timed(lambda: O.goertzel_f32(flat1, freqs, n), max(1.0, seconds / 5))
-        msps1_f32 = round(pf * S1 * n / elf / 1e6, 3)
+        r1f = rep_rates(lambda: O.goertzel_f32(flat1, freqs, n), S1 * n, max(0.2, seconds / 25), 5)
     parity = {"windows_checked": int(n_win), "symbol_mismatches": int((sym != gsym).sum())}
     if gmag is not None:
         parity["max_rel_mag_err"] = float((np.abs(gmag - P).max(1) / P.max(1)).max())
+    parity["margin"] = margin_stats(P)
     what = ("double radix-2 FFT, argmax over tone bins" if fft else "double Goertzel")
-    base = {"value": round(msps, 3), "unit": "Msamples/s", "cores": int(threads),
-            "kind": "port", "single_thread_value": round(msps1, 3),
-            "single_thread_fp32_value": msps1_f32,
-            "host_cpu": cpu_model(), "host_cpus_visible": os.cpu_count(),
+    med = float(np.median(rates))
+    base = {"value": round(med, 3), "unit": "Msamples/s", "cores": int(threads),
+            "kind": "port", "reps": len(rates),
+            "rep_values": [round(r, 1) for r in rates],
+            "single_thread_value": round(float(np.median(r1)), 3),
+            "single_thread_fp32_value": round(float(np.median(r1f)), 3) if r1f else None,
+            "host_cpu": cpu_model(),
             "sample": f"first {S * n} samples ({n_win} windows, hop {hop}) of the timed batch, "
-                      f"{passes} passes in {el:.1f} s, oracle/fsk_oracle.c {what}, OpenMP"}
+                      f"median of {len(rates)} reps of {seconds / reps:.1f} s, "
+                      f"oracle/fsk_oracle.c {what}, OpenMP {threads} threads"}
     return base, parity
+
+
+def stress_parity(A, O, cfg, freqs, sigma: int, W: int, dev, torch, threads: int):
+    """GPU vs oracle on a fresh W-window sample at noise sigma (the σ = 2000
+    stress level of SURVEY §8d): symbol mismatches, magnitude error, margins."""
+    d_pcm = torch.empty((W, 1024), dtype=torch.int16, device=dev)
+    d_true = torch.empty(W, dtype=torch.uint8, device=dev)
+    d_sym = torch.empty(W, dtype=torch.uint8, device=dev)
+    d_mag = torch.empty((W, len(freqs)), dtype=torch.float32, device=dev)
+    A.synth_fsk(cfg, A.BENCH_SEED ^ sigma, W, 8000, sigma, d_pcm, d_true)
+    with A.Demodulator(cfg) as d:
+        d.batch_device(d_pcm, W, d_sym, d_mag)
+    sym, P = O.goertzel(d_pcm.cpu().numpy(), freqs, 1024, threads=threads)
+    gs, gm = d_sym.cpu().numpy(), d_mag.cpu().numpy().astype(np.float64)
+    out = {"sigma": sigma, "windows_checked": W, "symbol_mismatches": int((gs != sym).sum()),
+           "transmitted_symbol_errors": int((gs != d_true.cpu().numpy()).sum()),
+           "max_rel_mag_err": float((np.abs(gm - P).max(1) / P.max(1)).max()),
+           "margin": margin_stats(P)}
+    return out
+
+
+def free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def run_config(A, D, torch, dist, args, config, rank, world, local, use_dist, steps, warmup,
+               plan="survey", method_name="auto", hop_fft=256, no_mags=False):
+    """Allocate, synthesise, warm up and time one workload; returns a dict."""
+    freqs = A.FSK8_FREQS if config == "fsk8" else A.FSK2_FREQS
+    if config == "fsk8" and plan == "odd":
+        freqs = tuple(46.875 * (32 + 9 * i) for i in range(8))
+    K = len(freqs)
+    n = 1024
+    method = {"auto": A.METHOD_AUTO, "goertzel": A.METHOD_GOERTZEL,
+              "folded": A.METHOD_FOLDED, "residue": A.METHOD_RESIDUE}[method_name]
+    hop = n
+    if config == "fft":
+        method, hop = A.METHOD_FFT, int(hop_fft)
+    if config == "streams":
+        # config 5: 1024 independent streams x 2^21 samples (2048 windows each);
+        # rank r demodulates the contiguous stream shard D.shard_range(1024, r, N)
+        n_streams, wps = 1024, 2048
+        s_first, s_count = D.shard_range(n_streams, rank, world)
+        W, w0, total_windows = s_count * wps, s_first * wps, n_streams * wps
+    else:
+        W = int(args.windows)
+        w0, total_windows = rank * W, world * W
+    # windows the detector evaluates over the rank's W x n-sample stream slice
+    n_eval = (W * n - n) // hop + 1
+    cfg = A.make_cfg(freqs=freqs, n=n, hop=hop, device=local, method=method)
+    dev = torch.device("cuda", local)
+    d_pcm = torch.empty((W, n), dtype=torch.int16, device=dev)
+    d_true = torch.empty(W, dtype=torch.uint8, device=dev)
+    d_sym = torch.empty(n_eval, dtype=torch.uint8, device=dev)
+    d_mag = None if no_mags else torch.empty((n_eval, K), dtype=torch.float32, device=dev)
+    A.synth_fsk(cfg, A.BENCH_SEED, W, 8000, 400, d_pcm, d_true, w0=w0)
+    torch.cuda.synchronize()
+    demod = A.Demodulator(cfg)
+    main = torch.cuda.current_stream()
+    gunits, gunit = (n_streams, wps) if config == "streams" else (world, W)
+    # With the gather: kernels run on a compute stream into double-buffered
+    # symbol slots; the RCCL gather of step t-1's symbols is issued on the
+    # default stream (waiting only for step t-1's kernel) and so overlaps step
+    # t's kernel.
+    comp = torch.cuda.Stream(device=dev) if use_dist else main
+    slots = [d_sym, torch.empty_like(d_sym)] if use_dist else [d_sym]
+    # config 5: every rank frames its own streams on the device (one
+    # ToReceiver run per stream, demod_frame_streams_async) and RCCL gathers
+    # the frames; the other configs gather symbols and rank 0 frames them.
+    dev_framing = config == "streams"
+    if dev_framing:
+        bits = A.bits_per_symbol(K)
+        fstride = A.frame_symbols_size(wps, bits)
+        fslots = [torch.empty(max(s_count * fstride, 1), dtype=torch.uint8, device=dev)
+                  for _ in slots]
+    kdone = [torch.cuda.Event() for _ in slots]   # kernel wrote the slot
+    gdone = [torch.cuda.Event() for _ in slots]   # gather finished reading the slot
+    st = {"i": 0, "prev": None, "used": [False] * len(slots), "gev": None}
+
+    def gather(slot):
+        main.wait_event(kdone[slot])
+        ge = st["gev"]
+        if ge is not None:
+            ge[0].record(main)
+        if dev_framing:
+            out = D.gather_symbols(fslots[slot][:s_count * fstride], gunits, world, unit=fstride)
+        else:
+            out = D.gather_symbols(slots[slot], gunits, world, unit=gunit)
+        if ge is not None:
+            ge[1].record(main)
+        gdone[slot].record(main)
+        return out
+
+    def step(ev=None, gev=None):
+        slot = st["i"] % len(slots)
+        st["i"] += 1
+        if st["used"][slot]:
+            comp.wait_event(gdone[slot])
+        if ev is not None:
+            ev[0].record(comp)
+        demod.batch_async(d_pcm, n_eval, slots[slot], d_mag, stream=comp.cuda_stream)
+        if ev is not None:
+            ev[1].record(comp)
+        if dev_framing:
+            A.frame_streams_async(slots[slot], s_count, wps, bits, fslots[slot],
+                                  stream=comp.cuda_stream)
+            if ev is not None:
+                ev[2].record(comp)
+        out = None
+        if use_dist:
+            kdone[slot].record(comp)
+            st["gev"] = gev
+            if st["prev"] is not None:
+                out = gather(st["prev"])
+            st["prev"] = slot
+            st["used"][slot] = True
+        return out
+
+    def flush(gev=None):
+        out = None
+        if use_dist and st["prev"] is not None:
+            st["gev"] = gev
+            out = gather(st["prev"])
+            st["prev"] = None
+        return out
+
+    def mk(k):
+        return tuple(torch.cuda.Event(enable_timing=True) for _ in range(k))
+
+    # Sustained HBM streaming shows a power-management transient: launch
+    # times rise ~25 % after ~10 launches and settle back by ~60 (dispatch
+    # series in profiles/round1/, DESIGN.md §Measurement). Warm up for at least
+    # MIN_WARMUP launches so the K timed steps see the steady state.
+    warm = max(warmup, MIN_WARMUP)
+    for _ in range(warm):
+        step()
+    flush()
+    evs = [mk(3) for _ in range(steps)]
+    gevs = [mk(2) for _ in range(steps)] if use_dist else None
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        # the gather issued in step i carries step i-1's symbols
+        step(evs[i], gevs[i - 1] if (gevs and i > 0) else None)
+    all_sym = flush(gevs[steps - 1] if gevs else None)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    kts = np.array([a.elapsed_time(b) for a, b, _ in evs])
+    kernel_ms = float(kts.mean())
+    ms_per_step = elapsed / steps * 1e3
+    frame_ms = (float(np.mean([b.elapsed_time(c) for _, b, c in evs])) if dev_framing else None)
+    gather_ms = (float(np.mean([a.elapsed_time(b) for a, b in gevs])) if gevs else None)
+
+    # Practical read ceiling of this box for the same access pattern: the
+    # read-only reference stream (8 KiB per wave, 16 B/lane nt loads, no
+    # compute; demod_read_ceiling_async) over the same input buffer, after the
+    # timed region, median of 20 launches (HIP events on the launch stream).
+    ceil_gbps = None
+    if config != "fft":
+        nb = (d_pcm.numel() * 2) // 8192 * 8192
+        cev = [mk(2) for _ in range(20)]
+        for _ in range(8):
+            A.read_ceiling_async(d_pcm, nb, stream=comp.cuda_stream)
+        for a, b in cev:
+            a.record(comp)
+            A.read_ceiling_async(d_pcm, nb, stream=comp.cuda_stream)
+            b.record(comp)
+        torch.cuda.synchronize()
+        ceil_gbps = nb / (float(np.median([a.elapsed_time(b) for a, b in cev])) / 1e3) / 1e9
+
+    # correctness of the timed output: every symbol vs the transmitted one
+    # (sliding windows straddle two symbols: compare the aligned ones only)
+    d_sym = slots[(st["i"] - 1) % len(slots)]
+    if hop == n:
+        sym_err = int((d_sym != d_true).sum().item())
+    else:
+        step_w = n // hop
+        sym_err = int((d_sym[::step_w][:W] != d_true).sum().item())
+    framed = None
+    if dev_framing:
+        # frames of the last step: gathered (with the gather) or this rank's own
+        frames = all_sym if use_dist else fslots[(st["i"] - 1) % len(slots)][:s_count * fstride]
+        all_true = D.gather_symbols(d_true, gunits, world, unit=gunit) if world > 1 else d_true
+        if rank == 0:
+            fb = frames.cpu().numpy()
+            back = np.concatenate([D.unframe_symbols(A, fb[i * fstride:(i + 1) * fstride].tobytes(),
+                                                     wps, K) for i in range(gunits)])
+            sym_err = int((back != all_true.cpu().numpy()).sum())
+            framed = {"frames_bytes": int(fb.size), "frame_bytes_per_stream": fstride,
+                      "bits_per_symbol": bits, "framing": "device (demod_frame_streams_async)",
+                      "gathered": ("frames (RCCL all_gather_into_tensor, %d rank%s)"
+                                   % (world, "" if world == 1 else "s")) if use_dist else "no",
+                      "roundtrip_ok": sym_err == 0}
+    elif use_dist:
+        all_true = D.gather_symbols(d_true, gunits, world, unit=gunit) if world > 1 else d_true
+        sym_err = int((all_sym != all_true).sum().item())
+        if rank == 0:
+            # rank 0 frames the gathered symbols as ip.proto ToReceiver messages
+            stream_bytes = D.frame_symbols(A, all_sym.cpu().numpy(), K)
+            back = D.unframe_symbols(A, stream_bytes, all_sym.numel(), K)
+            framed = {"frames_bytes": len(stream_bytes), "bits_per_symbol": A.bits_per_symbol(K),
+                      "roundtrip_ok": bool((back == all_sym.cpu().numpy()).all())}
+
+    alg_bytes = W * 2 * n + n_eval * (1 + (0 if no_mags else 4 * K))
+    achieved = alg_bytes / (kernel_ms / 1e3) / 1e9
+    kname = ("fft1024_quad_kernel<4>" if demod.method == A.METHOD_FFT else
+             ("fold_tile_kernel<%d,4>" if demod.method == A.METHOD_FOLDED
+              else "residue_tile_kernel<%d,4>" if demod.method == A.METHOD_RESIDUE
+              else "goertzel_tile_kernel<%d,4>") % K)
+    pmc_name = "fsk8odd" if (config == "fsk8" and plan == "odd") else config
+    r = {
+        "config": config, "freqs": freqs, "K": K, "n": n, "hop": hop, "W": W, "n_eval": n_eval,
+        "total_windows": total_windows, "ms_per_step": ms_per_step, "kernel_ms": kernel_ms,
+        "kts": kts, "sym_err": sym_err, "framed": framed, "warm": warm,
+        "detector": {A.METHOD_GOERTZEL: "goertzel", A.METHOD_FOLDED: "folded",
+                     A.METHOD_RESIDUE: "residue",
+                     A.METHOD_FFT: "fft1024"}.get(demod.method, str(demod.method)),
+        "roofline": {
+            "bound": "hbm",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBPS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBPS, 4),
+            "traffic": pmc_traffic(pmc_name, W),
+            "alg_bytes_per_launch": alg_bytes,
+            # this box's read-only ceiling for the same access pattern
+            # (see above) and the kernel's achieved rate as a fraction of it
+            "read_ceiling": round(ceil_gbps, 1) if ceil_gbps else None,
+            "frac_of_read_ceiling": round(achieved / ceil_gbps, 4) if ceil_gbps else None,
+            "kernel": kname,
+        },
+        "d_pcm": d_pcm, "d_sym": d_sym, "d_mag": d_mag, "cfg": cfg,
+    }
+    if dev_framing or use_dist:
+        # per-step cost above the detector kernel (DESIGN.md §6): the frame
+        # kernel and the gather (overlapped with the next kernel), HIP events
+        r["overhead"] = {"frame_kernel_ms": round(frame_ms, 4) if frame_ms is not None else None,
+                         "gather_ms": round(gather_ms, 4) if gather_ms is not None else None,
+                         "step_minus_kernel_ms": round(ms_per_step - kernel_ms, 4)}
+    if config == "fft":
+        # SURVEY §8d: the FFT is reported against the VALU roof too.
+        # Algorithmic flops per window: 2.5 N log2 N for the real N-point
+        # FFT + 3 per |X[b]|^2 over the N/2+1 bins.
+        fpw = 2.5 * n * 10 + 3 * (n // 2 + 1)
+        tf = fpw * n_eval / (kernel_ms / 1e3) / 1e12
+        r["roofline_valu"] = {"bound": "valu", "achieved": round(tf, 2),
+                              "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
+                              "frac": round(tf / VALU_PEAK_TFLOPS, 4),
+                              "flop_per_window": fpw}
+    demod.close()
+    return r
+
+
+def summary(r) -> dict:
+    """The extra-config entry of the bench line."""
+    out = {"workload": (f"configs[2]: 8-FSK Goertzel, {r['W']} x 1024 windows" if r["config"] == "fsk8"
+                        else f"configs[3]: sliding 1024-pt FFT, hop {r['hop']}, {r['n_eval']} windows"),
+           "detector": r["detector"], "ms_per_step": round(r["ms_per_step"], 4),
+           "kernel_ms": round(r["kernel_ms"], 4),
+           "kernel_ms_p10_p50_p90": [round(float(np.percentile(r["kts"], q)), 4) for q in (10, 50, 90)],
+           "value": round(r["W"] * 1024 / (r["ms_per_step"] / 1e3) / 1e6, 1), "unit": "Msamples/s",
+           "symbol_errors": r["sym_err"]}
+    if r["config"] == "fft":
+        out["roofline"] = r["roofline_valu"]
+        out["roofline_hbm_frac"] = round(
+            r["W"] * 2048 / (r["kernel_ms"] / 1e3) / 1e9 / HBM_PEAK_GBPS, 4)
+    else:
+        out["roofline"] = r["roofline"]
+    return out
 
 
 def main():
@@ -148,9 +482,14 @@ def main():
                     help="fsk8 tone plan: survey = SURVEY §8 (1500 + 375 i Hz, multiples of 8 "
                          "bins), odd = integer bins 32 + 9 i (every residue class mod 8: the "
                          "generic integer-bin path, DESIGN.md §4.3)")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-seconds", type=float, default=14.0)
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="skip the configs[2] / configs[3] entries of the default N = 1 run")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="initialise torch.distributed and run the gather even at N = 1 "
+                         "(exercises the RCCL path on one GPU)")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="nccl (= RCCL over xGMI) on the real node; gloo only to rehearse the "
                          "multi-rank path with several ranks sharing one GPU")
@@ -164,187 +503,42 @@ def main():
     if args.dist_backend == "gloo":
         local = local % torch.cuda.device_count()  # rehearsal: ranks may share a GPU
     torch.cuda.set_device(local)
+    use_dist = world > 1 or args.force_dist
     dist = None
-    if world > 1:
+    if use_dist:
         import torch.distributed as dist
+        init = {}
+        if world == 1 and "MASTER_PORT" not in os.environ:
+            init = {"init_method": f"tcp://127.0.0.1:{free_port()}", "rank": 0, "world_size": 1}
         if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local), **init)
         else:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", **init)
 
     A, D = load_pkg()
-    freqs = A.FSK8_FREQS if args.config == "fsk8" else A.FSK2_FREQS
-    if args.config == "fsk8" and args.plan == "odd":
-        freqs = tuple(46.875 * (32 + 9 * i) for i in range(8))
-    K = len(freqs)
-    n = 1024
-    method = {"auto": A.METHOD_AUTO, "goertzel": A.METHOD_GOERTZEL,
-              "folded": A.METHOD_FOLDED, "residue": A.METHOD_RESIDUE}[args.method]
-    hop = n
-    if args.config == "fft":
-        method, hop = A.METHOD_FFT, int(args.hop)
-    if args.config == "streams":
-        # config 5: 1024 independent streams x 2^21 samples (2048 windows each);
-        # rank r demodulates the contiguous stream shard D.shard_range(1024, r, N)
-        n_streams, wps = 1024, 2048
-        s_first, s_count = D.shard_range(n_streams, rank, world)
-        W, w0, total_windows = s_count * wps, s_first * wps, n_streams * wps
-    else:
-        W = int(args.windows)
-        w0, total_windows = rank * W, world * W
-    # windows the detector evaluates over the rank's W x n-sample stream slice
-    n_eval = (W * n - n) // hop + 1
-    cfg = A.make_cfg(freqs=freqs, n=n, hop=hop, device=local, method=method)
-    dev = torch.device("cuda", local)
-    d_pcm = torch.empty((W, n), dtype=torch.int16, device=dev)
-    d_true = torch.empty(W, dtype=torch.uint8, device=dev)
-    d_sym = torch.empty(n_eval, dtype=torch.uint8, device=dev)
-    d_mag = None if args.no_mags else torch.empty((n_eval, K), dtype=torch.float32, device=dev)
-    A.synth_fsk(cfg, A.BENCH_SEED, W, 8000, 400, d_pcm, d_true, w0=w0)
-    torch.cuda.synchronize()
-    demod = A.Demodulator(cfg)
-    main = torch.cuda.current_stream()
-    gunits, gunit = (n_streams, wps) if args.config == "streams" else (world, W)
-    # N > 1: kernels run on a compute stream into double-buffered symbol slots;
-    # the RCCL gather of step t-1's symbols is issued on the default stream
-    # (waiting only for step t-1's kernel) and so overlaps step t's kernel.
-    comp = torch.cuda.Stream(device=dev) if world > 1 else main
-    slots = [d_sym, torch.empty_like(d_sym)] if world > 1 else [d_sym]
-    # config 5: every rank frames its own streams on the device (one
-    # ToReceiver run per stream, demod_frame_streams_async) and RCCL gathers
-    # the frames; the other configs gather symbols and rank 0 frames them.
-    dev_framing = args.config == "streams"
-    if dev_framing:
-        bits = A.bits_per_symbol(K)
-        fstride = A.frame_symbols_size(wps, bits)
-        fslots = [torch.empty(max(s_count * fstride, 1), dtype=torch.uint8, device=dev)
-                  for _ in slots]
-    kdone = [torch.cuda.Event() for _ in slots]   # kernel wrote the slot
-    gdone = [torch.cuda.Event() for _ in slots]   # gather finished reading the slot
-    st = {"i": 0, "prev": None, "used": [False] * len(slots)}
+    r = run_config(A, D, torch, dist, args, args.config, rank, world, local, use_dist,
+                   args.steps, args.warmup, plan=args.plan, method_name=args.method,
+                   hop_fft=args.hop, no_mags=args.no_mags)
 
-    def gather(slot):
-        main.wait_event(kdone[slot])
-        if dev_framing:
-            out = D.gather_symbols(fslots[slot][:s_count * fstride], gunits, world, unit=fstride)
-        else:
-            out = D.gather_symbols(slots[slot], gunits, world, unit=gunit)
-        gdone[slot].record(main)
-        return out
-
-    def step(ev=None):
-        slot = st["i"] % len(slots)
-        st["i"] += 1
-        if st["used"][slot]:
-            comp.wait_event(gdone[slot])
-        if ev is not None:
-            ev[0].record(comp)
-        demod.batch_async(d_pcm, n_eval, slots[slot], d_mag, stream=comp.cuda_stream)
-        if ev is not None:
-            ev[1].record(comp)
-        if dev_framing:
-            A.frame_streams_async(slots[slot], s_count, wps, bits, fslots[slot],
-                                  stream=comp.cuda_stream)
-        out = None
-        if world > 1:
-            kdone[slot].record(comp)
-            if st["prev"] is not None:
-                out = gather(st["prev"])
-            st["prev"] = slot
-            st["used"][slot] = True
-        return out
-
-    def flush():
-        out = None
-        if world > 1 and st["prev"] is not None:
-            out = gather(st["prev"])
-            st["prev"] = None
-        return out
-
-    # Sustained HBM streaming shows a power-management transient: launch
-    # times rise ~25 % after ~10 launches and settle back by ~60 (dispatch
-    # series in profiles/round1/). Warm up for at least
-    # MIN_WARMUP launches so the K timed steps see the steady state.
-    warmup = max(args.warmup, MIN_WARMUP)
-    for _ in range(warmup):
-        step()
-    flush()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(args.steps)]
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(evs[i])
-    all_sym = flush()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    kts = np.array([a.elapsed_time(b) for a, b in evs])
-    kernel_ms = float(kts.mean())
-    ms_per_step = elapsed / args.steps * 1e3
-
-    # Practical read ceiling of this box for the same access pattern: the
-    # read-only reference stream (8 KiB per wave, 16 B/lane nt loads, no
-    # compute; demod_read_ceiling_async) over the same input buffer, after the
-    # timed region, median of 20 launches (HIP events on the launch stream).
-    ceil_gbps = None
-    if args.config != "fft":
-        nb = (d_pcm.numel() * 2) // 8192 * 8192
-        cev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-               for _ in range(20)]
-        for _ in range(8):
-            A.read_ceiling_async(d_pcm, nb, stream=comp.cuda_stream)
-        for a, b in cev:
-            a.record(comp)
-            A.read_ceiling_async(d_pcm, nb, stream=comp.cuda_stream)
-            b.record(comp)
-        torch.cuda.synchronize()
-        ceil_gbps = nb / (float(np.median([a.elapsed_time(b) for a, b in cev])) / 1e3) / 1e9
-
-    # correctness of the timed output: every symbol vs the transmitted one
-    # (sliding windows straddle two symbols: compare the aligned ones only)
-    d_sym = slots[(st["i"] - 1) % len(slots)]
-    if hop == n:
-        sym_err = int((d_sym != d_true).sum().item())
-    else:
-        step_w = n // hop
-        sym_err = int((d_sym[::step_w][:W] != d_true).sum().item())
-    framed = None
-    if dev_framing:
-        # frames of the last step: gathered (N > 1) or this rank's own (N = 1)
-        frames = all_sym if world > 1 else fslots[(st["i"] - 1) % len(slots)][:s_count * fstride]
-        all_true = D.gather_symbols(d_true, gunits, world, unit=gunit) if world > 1 else d_true
-        if rank == 0:
-            fb = frames.cpu().numpy()
-            back = np.concatenate([D.unframe_symbols(A, fb[i * fstride:(i + 1) * fstride].tobytes(),
-                                                     wps, K) for i in range(gunits)])
-            sym_err = int((back != all_true.cpu().numpy()).sum())
-            framed = {"frames_bytes": int(fb.size), "frame_bytes_per_stream": fstride,
-                      "bits_per_symbol": bits, "framing": "device (demod_frame_streams_async)",
-                      "gathered": "frames" if world > 1 else "n/a (1 rank)",
-                      "roundtrip_ok": sym_err == 0}
-    elif world > 1:
-        all_true = D.gather_symbols(d_true, gunits, world, unit=gunit)
-        sym_err = int((all_sym != all_true).sum().item())
-        if rank == 0:
-            # rank 0 frames the gathered symbols as ip.proto ToReceiver messages
-            stream_bytes = D.frame_symbols(A, all_sym.cpu().numpy(), K)
-            back = D.unframe_symbols(A, stream_bytes, all_sym.numel(), K)
-            framed = {"frames_bytes": len(stream_bytes), "bits_per_symbol": A.bits_per_symbol(K),
-                      "roundtrip_ok": bool((back == all_sym.cpu().numpy()).all())}
+    extras = {}
+    if (world == 1 and args.config == "fsk2" and not args.no_extras and not args.force_dist
+            and args.method == "auto" and not args.no_mags):
+        # configs[2] and configs[3], same steps / warmup, in their own buffers
+        # (the main run's stay alive for the CPU baseline's parity sample)
+        main_keep = {k: r[k] for k in ("d_pcm", "d_sym", "d_mag")}
+        for key, cfgname in (("fsk8", "fsk8"), ("fft_hop256", "fft")):
+            rr = run_config(A, D, torch, dist, args, cfgname, rank, world, local, False,
+                            args.steps, args.warmup, hop_fft=256)
+            extras[key] = summary(rr)
+            del rr
+            torch.cuda.empty_cache()
+        r.update(main_keep)
 
     if rank == 0:
-        samples = total_windows * n  # stream samples demodulated (each counted once)
-        value = samples / (ms_per_step / 1e3) / 1e6
-        alg_bytes = W * 2 * n + n_eval * (1 + (0 if args.no_mags else 4 * K))
-        achieved = alg_bytes / (kernel_ms / 1e3) / 1e9
+        samples = r["total_windows"] * r["n"]  # stream samples demodulated (each counted once)
+        value = samples / (r["ms_per_step"] / 1e3) / 1e6
+        config, K, hop, W, n_eval = r["config"], r["K"], r["hop"], r["W"], r["n_eval"]
+        dev_framing = config == "streams"
         out = {
             "metric": METRIC,
             "value": round(value, 1),
@@ -352,78 +546,65 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "warmup_effective": warmup,
-            "ms_per_step": round(ms_per_step, 4),
+            "warmup_effective": r["warm"],
+            "ms_per_step": round(r["ms_per_step"], 4),
             "higher_is_better": True,
-            "scaling": "strong" if args.config == "streams" else "weak",
+            "scaling": "strong" if config == "streams" else "weak",
             "vs_baseline": None,
             "dtype": "fp32",
             "data": "synthetic (seeded splitmix64 FSK, A=8000, Irwin-Hall noise sigma=400)",
             "config": {
                 "workload": ("configs[4]: 1024 streams x 2048 windows (2^21 samples each), "
                              f"sharded by stream over {world} GPU(s), 2-FSK"
-                             if args.config == "streams" else
+                             if config == "streams" else
                              f"configs[3]: sliding 1024-pt full-spectrum FFT, hop {hop}, "
-                             f"{n_eval} windows over a {W * n}-sample int16 stream per GPU"
-                             if args.config == "fft" else
+                             f"{n_eval} windows over a {W * 1024}-sample int16 stream per GPU"
+                             if config == "fft" else
                              ("configs[1]: 2-FSK" if K == 2 else
                               "configs[2]: 8-FSK" + (" (integer bins 32 + 9 i)" if args.plan == "odd"
                                                      else ""))
-                             + f" Goertzel, {W} x {n}-sample int16 windows per GPU, HBM-resident"),
-                "tones_hz": list(freqs),
+                             + f" Goertzel, {W} x 1024-sample int16 windows per GPU, HBM-resident"),
+                "tones_hz": list(r["freqs"]),
                 "windows_per_gpu": n_eval,
                 "hop": hop,
-                "n": n,
+                "n": r["n"],
                 "outputs": "symbols" + ("" if args.no_mags else " + |X_k|^2"),
                 "parallelism": (f"dp{world} (stream shards; per-rank device framing, RCCL "
                                 "all-gather of ToReceiver frames)" if dev_framing else
                                 f"dp{world} (independent window shards, RCCL symbol all-gather)"),
             },
-            "detector": {A.METHOD_GOERTZEL: "goertzel", A.METHOD_FOLDED: "folded",
-                         A.METHOD_RESIDUE: "residue",
-                         A.METHOD_FFT: "fft1024"}.get(demod.method, str(demod.method)),
-            "kernel_ms_p10_p50_p90": [round(float(np.percentile(kts, q)), 4) for q in (10, 50, 90)],
-            "symbol_errors": sym_err,
-            "symbol_error_rate": sym_err / float(total_windows),
-            "kernel_ms": round(kernel_ms, 4),
-            "roofline": {
-                "bound": "hbm",
-                "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBPS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                "traffic": pmc_traffic(args.config if args.plan == "survey" else "fsk8odd", W),
-                "alg_bytes_per_launch": alg_bytes,
-                # this box's read-only ceiling for the same access pattern
-                # (see above) and the kernel's achieved rate as a fraction of it
-                "read_ceiling": round(ceil_gbps, 1) if ceil_gbps else None,
-                "frac_of_read_ceiling": round(achieved / ceil_gbps, 4) if ceil_gbps else None,
-                "kernel": ("fft1024_quad_kernel<4>" if demod.method == A.METHOD_FFT else
-                           ("fold_tile_kernel<%d,4>" if demod.method == A.METHOD_FOLDED
-                            else "residue_tile_kernel<%d,4>" if demod.method == A.METHOD_RESIDUE
-                            else "goertzel_tile_kernel<%d,4>") % K),
-            },
+            "detector": r["detector"],
+            "kernel_ms_p10_p50_p90": [round(float(np.percentile(r["kts"], q)), 4)
+                                      for q in (10, 50, 90)],
+            "symbol_errors": r["sym_err"],
+            "symbol_error_rate": r["sym_err"] / float(r["total_windows"]),
+            "kernel_ms": round(r["kernel_ms"], 4),
+            "roofline": r["roofline"],
         }
-        if args.config == "fft":
-            # the FFT is reported against the VALU roof too.
-            # Algorithmic flops per window: 2.5 N log2 N for the real N-point
-            # FFT + 3 per |X[b]|^2 over the N/2+1 bins.
-            fpw = 2.5 * n * 10 + 3 * (n // 2 + 1)
-            tf = fpw * n_eval / (kernel_ms / 1e3) / 1e12
-            out["roofline_valu"] = {"bound": "valu", "achieved": round(tf, 2),
-                                    "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
-                                    "frac": round(tf / VALU_PEAK_TFLOPS, 4),
-                                    "flop_per_window": fpw}
-        if framed:
-            out["framing"] = framed
+        if "roofline_valu" in r:
+            out["roofline_valu"] = r["roofline_valu"]
+        if "overhead" in r:
+            out["overhead"] = r["overhead"]
+        if r["framed"]:
+            out["framing"] = r["framed"]
+        out.update(extras)
         if world == 1 and not args.no_cpu_baseline:
-            threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-            base, parity = cpu_baseline(A, d_pcm, d_sym, d_mag, freqs, args.cpu_seconds, threads,
-                                        args.config == "fft", hop)
+            visible, affinity, quota, threads, why = cpu_share()
+            if args.cpu_threads:
+                threads, why = args.cpu_threads, "--cpu-threads"
+            base, parity = cpu_baseline(r["d_pcm"], r["d_sym"], r["d_mag"], r["freqs"],
+                                        args.cpu_seconds, threads, config == "fft", hop)
+            base.update({"host_cpus_visible": visible, "cpus_in_affinity": affinity,
+                         "cgroup_quota_cores": quota, "threads_why": why})
             out["cpu_baseline"] = base
+            if config in ("fsk2", "fsk8"):
+                sys.path.insert(0, ROOT)
+                from oracle import oracle as O
+                parity = {"sigma400": parity,
+                          "sigma2000": stress_parity(A, O, r["cfg"], r["freqs"], 2000, 65536,
+                                                     r["d_pcm"].device, torch, threads)}
             out["parity_sample"] = parity
         print(json.dumps(out), flush=True)
-    demod.close()
     if dist is not None:
         dist.destroy_process_group()
 

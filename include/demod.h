@@ -50,6 +50,10 @@ extern "C" {
 #define DEMOD_FRAME_TOO_LARGE  -10  /* payload > max encoded frame (network.cpp:24,223) */
 
 #define DEMOD_MAX_TONES         16
+/* Opus decoder delay of the transmitter's encoder settings at 48 kHz
+ * (OPUS_GET_LOOKAHEAD; computed but never used by the reference,
+ * transmitter OpusEncoder.kt:46-47,65-67; measured in SURVEY.md §8 a7). */
+#define DEMOD_OPUS_LOOKAHEAD    312
 #define DEMOD_MAX_FRAME_PAYLOAD 4096 /* MAX_ENCODED_FRAME_SIZE, network.cpp:24 */
 
 /* channel handling for interleaved input (channels == 2) */
@@ -79,7 +83,10 @@ typedef struct demod_cfg {
     int32_t  channel_mode;           /* DEMOD_CH_* (ignored for mono) */
     int32_t  device;                 /* HIP device ordinal */
     int32_t  method;                 /* DEMOD_METHOD_* */
-    uint32_t reserved;               /* must be 0 */
+    uint32_t lead_in;                /* mono frames demodulate() drops at the start of a
+                                        stream (after demod_create / demod_reset), e.g.
+                                        DEMOD_OPUS_LOOKAHEAD to absorb the Opus decoder
+                                        delay; 0 = none. < 2^31. Batch calls ignore it. */
     double   freqs[DEMOD_MAX_TONES]; /* tone frequencies, Hz; symbol i <-> freqs[i] */
 } demod_cfg_t;
 
@@ -95,8 +102,9 @@ demod_t *demod_create(const demod_cfg_t *cfg, int *error);
 /* Replaces opus_decoder_destroy (opus.h:512). NULL is accepted. */
 void demod_destroy(demod_t *st);
 
-/* Drop carried samples; the next demodulate() starts a new stream.
- * Mirrors playback_start_new_stream (playback.cpp:67-74). */
+/* Drop carried samples and re-arm cfg.lead_in; the next demodulate() starts a
+ * new stream. Mirrors playback_start_new_stream (playback.cpp:67-74), which
+ * recreates the Opus decoder (and with it its delay) per stream. */
 int demod_reset(demod_t *st);
 
 /* Detector the handle runs (DEMOD_METHOD_GOERTZEL / _FOLDED / _RESIDUE / _FFT). */
@@ -112,7 +120,8 @@ int demod_max_symbols(const demod_t *st, size_t n_frames);
  * Streaming entry point: demodulate(pcm, n) -> symbols.
  * pcm: host pointer to n_frames frames of `channels` interleaved int16
  * samples (48 kHz int16 LE, the format opus_decode writes at
- * playback.cpp:118). Samples are appended to the handle's carry buffer;
+ * playback.cpp:118). The stream's first cfg.lead_in frames are dropped; the
+ * rest are appended to the handle's carry buffer;
  * one symbol is emitted per complete window (advance `hop`).
  * Returns the number of symbols written to symbols[0..], or a negative code.
  * If max_symbols is too small nothing is consumed and

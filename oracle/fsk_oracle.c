@@ -258,6 +258,7 @@ struct oracle_stream {
     double c[64];
     int16_t *buf;
     uint32_t fill;
+    uint32_t skip;  /* lead-in frames still to drop */
 };
 
 oracle_stream_t *oracle_stream_create(uint32_t n, uint32_t hop,
@@ -285,6 +286,8 @@ void oracle_stream_destroy(oracle_stream_t *st)
 
 int oracle_stream_pending(const oracle_stream_t *st) { return (int)st->fill; }
 
+void oracle_stream_set_lead_in(oracle_stream_t *st, uint32_t frames) { st->skip = frames; }
+
 static int16_t channel_sample(const oracle_stream_t *st, const int16_t *f)
 {
     if (st->channels == 1) return f[0];
@@ -298,6 +301,10 @@ long oracle_stream_push(oracle_stream_t *st, const int16_t *pcm,
 {
     long out = 0;
     for (size_t i = 0; i < n_frames; ++i) {
+        if (st->skip) {
+            --st->skip;
+            continue;
+        }
         st->buf[st->fill++] = channel_sample(st, pcm + i * st->channels);
         if (st->fill == st->n) {
             if ((size_t)out >= cap) return -2;

@@ -74,6 +74,9 @@ long oracle_stream_push(oracle_stream_t *st, const int16_t *pcm,
                         size_t n_frames, uint8_t *sym, double *P,
                         size_t cap);
 int oracle_stream_pending(const oracle_stream_t *st);
+/* Drop the next `frames` input frames before any window is formed (the
+ * demod_cfg_t.lead_in contract: e.g. the 312-sample Opus decoder delay). */
+void oracle_stream_set_lead_in(oracle_stream_t *st, uint32_t frames);
 
 #ifdef __cplusplus
 }

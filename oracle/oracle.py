@@ -70,6 +70,7 @@ def lib() -> ctypes.CDLL:
         L.oracle_stream_push.restype = ctypes.c_long
         L.oracle_stream_pending.argtypes = [_P]
         L.oracle_stream_pending.restype = ctypes.c_int
+        L.oracle_stream_set_lead_in.argtypes = [_P, ctypes.c_uint32]
         _lib = L
     return _lib
 
@@ -166,10 +167,13 @@ def fft_demod(x: np.ndarray, freqs: Sequence[float], n: int, hop: Optional[int] 
 class Stream:
     """Streaming restatement of demodulate(pcm, n)."""
 
-    def __init__(self, freqs, n=1024, hop=None, channels=1, channel_mode=0, fs=48000.0):
+    def __init__(self, freqs, n=1024, hop=None, channels=1, channel_mode=0, fs=48000.0,
+                 lead_in=0):
         self.k = len(freqs)
         self._h = lib().oracle_stream_create(n, n if hop is None else hop, channels,
                                              channel_mode, self.k, _freqs(freqs), fs)
+        if lead_in:
+            lib().oracle_stream_set_lead_in(self._h, lead_in)
         self.channels = channels
         self.n = n
 

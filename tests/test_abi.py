@@ -80,3 +80,41 @@ def test_integration_doc_maps_every_export(A):
                             "INTEGRATION.md")).read()
     missing = [n for n in A.header_exports() if n not in doc]
     assert not missing, missing
+
+
+def test_lead_in_field_and_validation(A):
+    """demod_cfg_t.lead_in replaced round 1's `reserved` (same offset): the
+    Opus decoder delay the streaming entry drops; values >= 2^31 are rejected
+    before any device work."""
+    assert A.DemodCfg.lead_in.offset == 8 + 7 * 4 and A.DEMOD_OPUS_LOOKAHEAD == 312
+    cfg = A.make_cfg(lead_in=A.DEMOD_OPUS_LOOKAHEAD)
+    assert cfg.lead_in == 312
+    bad = A.make_cfg()
+    bad.lead_in = 0x80000000
+    with pytest.raises(A.DemodError) as e:
+        A.Demodulator(bad)
+    assert e.value.code == A.DEMOD_BAD_ARG
+
+
+def test_device_tensor_checks(A):
+    """The Python mirror validates tensors before handing raw pointers to the
+    C ABI (a short / strided / wrong-dtype / host tensor would otherwise be an
+    out-of-bounds device access): DemodError(DEMOD_BAD_ARG), no GPU needed."""
+    torch = pytest.importorskip("torch")
+    chk = A._check_dev
+    ok_shape = torch.zeros(4, dtype=torch.int16)
+    for t, dtype, need in [
+        (torch.zeros(4, dtype=torch.int32), "int16", 4),          # dtype
+        (torch.zeros(3, dtype=torch.int16), "int16", 4),          # too short
+        (torch.zeros(8, dtype=torch.int16)[::2], "int16", 4),     # strided
+        (ok_shape, "int16", 4),                                   # host tensor
+        (12345, "int16", 4),                                      # raw address
+        (None, "uint8", 4),                                       # missing
+    ]:
+        with pytest.raises(A.DemodError) as e:
+            chk(t, "x", dtype, need, 0)
+        assert e.value.code == A.DEMOD_BAD_ARG
+    chk(None, "mags", "float32", 10, 0, nullable=True)
+    with pytest.raises(A.DemodError):
+        A.frame_streams_async(torch.zeros(10, dtype=torch.uint8), 2, 5, 1,
+                              torch.zeros(1, dtype=torch.uint8))

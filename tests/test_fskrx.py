@@ -81,10 +81,31 @@ def test_stereo_pcm_to_frames(A, O, fskrx, mode, k):
     assert b"333 samples pending" in r.stderr
 
 
+@pytest.mark.gpu
+def test_batch_many_payloads_and_lead_in(A, O, fskrx):
+    """-b with more than 3 payloads' worth of symbols in one demodulate() call
+    (hop 8: 3 x 32768 + 1000 windows from 0.8 MB of PCM): every payload is
+    framed on its own; and -L drops the stream's lead-in before windowing."""
+    if not _gpu_visible():
+        pytest.skip("no GPU visible")
+    freqs = A.FSK2_FREQS
+    W = 3 * 32768 + 1000
+    n_samp = (W - 1) * 8 + 1024
+    pcm, _ = O.synth_fsk(freqs, 1024, n_samp // 1024 + 2, 5150, 8000, 400)
+    mono = pcm.reshape(-1)[:n_samp + 312]
+    r = _run(fskrx, mono, "-H", "8", "-b", "-L", "312")
+    assert r.returncode == 0, r.stderr.decode()
+    got = _symbols(A, r.stdout, W, 1)
+    ref, _ = O.goertzel(mono[312:], freqs, 1024, 8)
+    assert ref.size == W and np.array_equal(got, ref)
+    assert b"4 ToReceiver frames" in r.stderr
+
+
 def test_network_usage_errors(fskrx):
-    # discovery or -1 without a TCP listener, and a device name over 127 bytes
+    # discovery, -1 or -r without a TCP listener, and a device name over 127 bytes
     assert subprocess.run([fskrx, "-u", "0"], capture_output=True).returncode == 2
     assert subprocess.run([fskrx, "-1"], capture_output=True).returncode == 2
+    assert subprocess.run([fskrx, "-r"], capture_output=True).returncode == 2
     assert subprocess.run([fskrx, "-l", "0", "-N", "x" * 128], capture_output=True).returncode == 2
 
 
@@ -118,7 +139,8 @@ def test_network_receiver_session(A, O, fskrx, channels):
         inter[1::2] = np.random.default_rng(3).integers(-900, 900, mono.size).astype(np.int16)
     else:
         inter = mono
-    p, tport, uport = _start_listener(fskrx, "-c", str(channels), "-m", "left", "-N", "bench-rx")
+    p, tport, uport = _start_listener(fskrx, "-r", "-c", str(channels), "-m", "left", "-N",
+                                      "bench-rx")
     try:
         u = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
         u.settimeout(0.5)
@@ -147,8 +169,9 @@ def test_network_receiver_session(A, O, fskrx, channels):
         raw = inter.astype("<i2").tobytes()
         rng = np.random.default_rng(channels)
         off, wire = 0, b""
-        while off < len(raw):                    # ragged payloads, samples split across frames
-            n = int(rng.integers(1, 4097))
+        fb = 2 * channels
+        while off < len(raw):                    # ragged payloads of whole PCM frames
+            n = fb * int(rng.integers(1, 4096 // fb + 1))
             wire += A.frame_encode(raw[off:off + n])
             off += n
         for i in range(0, len(wire), 1500):      # TCP segments that cut frames
@@ -166,3 +189,51 @@ def test_network_receiver_session(A, O, fskrx, channels):
     got = _symbols(A, out, W, 1)
     ref, _ = O.goertzel(mono, freqs, 1024)
     assert got.size == W and np.array_equal(got, ref)
+
+
+def _hello(A, t):
+    buf = b""
+    while True:
+        buf += t.recv(4096)
+        try:
+            return A.to_transmitter_decode(buf)
+        except A.DemodError as e:
+            assert e.code == A.DEMOD_BUFFER_TOO_SMALL
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("raw,payload", [(False, 4 * 1000), (False, 693), (True, 693),
+                                         (True, 6)])
+def test_network_refuses_non_pcm_audio(A, fskrx, raw, payload):
+    """A reference transmitter sends Opus packets in AudioData
+    (MulticastAudioOutput.kt:124-130); this receiver does not decode Opus, so
+    without -r any AudioData, and with -r a payload that is not whole PCM frames
+    (stereo: 4 B), is refused: ToTransmitter{error{audio_decode_error}}, the
+    connection closed, exit status 4 — never demodulated as noise."""
+    import socket
+    if not _gpu_visible():
+        pytest.skip("no GPU visible")
+    args = ["-c", "2"] + (["-r"] if raw else [])
+    p, tport, _ = _start_listener(fskrx, *args)
+    try:
+        t = socket.create_connection(("127.0.0.1", tport), timeout=30)
+        which, _, _ = _hello(A, t)
+        assert which == A.DEMOD_MSG_RECEIVER_INFORMATION
+        t.sendall(A.frame_encode(bytes(range(256)) * (payload // 256) + bytes(payload % 256)))
+        reply = b""
+        while True:
+            chunk = t.recv(4096)
+            if not chunk:
+                break
+            reply += chunk
+        out, err = p.communicate(timeout=60)
+        t.close()
+    finally:
+        if p.poll() is None:
+            p.kill()
+            p.wait()
+    assert p.returncode == 4, err.decode()
+    which, fields, used = A.to_transmitter_decode(reply)
+    assert which == A.DEMOD_MSG_RECEIVER_ERROR and used == len(reply)
+    assert fields == {"audio_underflow": False, "audio_decode_error": True}
+    assert b"1 refused" in err and out == b""

@@ -1,0 +1,136 @@
+"""Near-tie decisions on every detector.
+
+Windows carry two tones whose powers differ by a designed ratio 1 + eps,
+eps in {0, 1e-7 .. 1e-4}, in both orders (so the higher-index tone is
+sometimes the larger one), with random phases. int16 rounding then spreads
+the realised power ratios over a few 1e-6 around eps: many windows fall
+inside 2^-19 (the band the round-1 packed-key argmax resolved to the lower
+tone whatever the powers said). The decision must be the exact argmax of
+the returned fp32 powers (ties to the lowest tone) on every window, and the
+oracle's wherever its margin is outside the fp32 band (tests/decision.py).
+"""
+import zlib
+
+import numpy as np
+import pytest
+
+from decision import check_decisions
+
+pytestmark = pytest.mark.gpu
+
+GOERTZEL, FFT, FOLDED, RESIDUE = 1, 2, 3, 4
+FSK8_ODD = tuple(46.875 * (32 + 9 * i) for i in range(8))
+NONINT8 = tuple(1234.5 + 1111.1 * i for i in range(8))
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch as t
+    if not t.cuda.is_available():
+        pytest.skip("no GPU visible")
+    return t
+
+
+def near_tie_windows(freqs, W, seed, n=1024, amp=9000.0):
+    """W windows, each two random tones a, b of the plan with random phases;
+    b's amplitude is solved (bisection, double precision, before rounding to
+    int16) so that the two tones' DFT powers at their own frequencies are in
+    ratio P_b / P_a = 1 + eps exactly — including the leakage between them,
+    which matters for off-bin plans."""
+    rng = np.random.default_rng(seed)
+    K = len(freqs)
+    t = np.arange(n)
+    eps_set = np.array([0.0, 1e-7, 3e-7, 1e-6, 2e-6, 5e-6, 1e-5, 1e-4])
+    ab = np.array([rng.choice(K, 2, replace=False) for _ in range(W)])
+    eps = eps_set[np.arange(W) % eps_set.size]
+    ph = rng.uniform(0, 2 * np.pi, (W, 2))
+    w = 2 * np.pi * np.asarray(freqs, np.float64)[ab] / 48000.0          # (W, 2)
+    tones = np.cos(w[:, :, None] * t + ph[:, :, None])                  # (W, 2, n)
+    E = np.exp(-1j * w[:, :, None] * t)                                  # (W, 2, n)
+    c = np.einsum("wjn,wkn->wjk", tones, E)   # c[w, j, k]: tone j's DFT at tone k's frequency
+
+    def ratio(a2):
+        Xa = amp * c[:, 0, 0] + a2 * c[:, 1, 0]
+        Xb = amp * c[:, 0, 1] + a2 * c[:, 1, 1]
+        return np.abs(Xb) ** 2 / np.abs(Xa) ** 2
+
+    lo, hi = np.full(W, 0.5 * amp), np.full(W, 2.0 * amp)
+    for _ in range(60):
+        mid = 0.5 * (lo + hi)
+        up = ratio(mid) < 1.0 + eps
+        lo, hi = np.where(up, mid, lo), np.where(up, hi, mid)
+    a2 = 0.5 * (lo + hi)
+    v = amp * tones[:, 0] + a2[:, None] * tones[:, 1]
+    x = np.clip(np.round(v), -32768, 32767).astype(np.int16)
+    return x, ab
+
+
+@pytest.mark.parametrize("plan,method", [
+    ("FSK8_FREQS", FOLDED),      # fold by 16 (F16), window_sum_decide_split8
+    ("FSK8_FREQS", GOERTZEL),    # plain bank, K = 8, window_sum_decide
+    ("FSK8_ODD", RESIDUE),       # residue kernel, compile-time classes (DCLS)
+    ("ODD5", RESIDUE),           # residue kernel, LDS class file (unbalanced plan)
+    ("ODD16", RESIDUE),          # K = 16: two candidates per lane (V = 32)
+    ("NONINT8", GOERTZEL),       # off-bin tones
+    ("FSK2_FREQS", GOERTZEL),    # K = 2 all-reduce path
+    ("FSK8_FREQS", FFT),         # FFT detector's row pick
+])
+def test_near_ties_follow_exact_argmax(A, O, torch, plan, method):
+    freqs = {"FSK8_FREQS": A.FSK8_FREQS, "FSK8_ODD": FSK8_ODD, "NONINT8": NONINT8,
+             "FSK2_FREQS": A.FSK2_FREQS, "ODD5": FSK8_ODD[:5],
+             "ODD16": tuple(46.875 * (32 + 9 * i) for i in range(16))}[plan]
+    W = 4000
+    x, pairs = near_tie_windows(freqs, W, seed=zlib.crc32(f"{plan}/{method}".encode()))
+    with A.Demodulator(freqs=freqs, method=method) as d:
+        assert d.method == method
+        sym, mag = d.batch(x, mags=True)
+    oracle = O.fft_demod if method == FFT else O.goertzel
+    ref_sym, ref_P = oracle(x, freqs, 1024)
+    in_band = check_decisions(sym, mag, ref_sym, ref_P)
+    # the test must reach the band it is about: realised fp32 power ratios
+    # within 2^-19 of each other, with the larger power on the higher index
+    m = mag.astype(np.float64)
+    top2 = np.sort(m, axis=1)[:, -2:]
+    rel = (top2[:, 1] - top2[:, 0]) / np.maximum(top2[:, 1], 1e-30)
+    hi_wins = pairs.max(axis=1) == sym
+    tight = (rel < 2.0 ** -19) & (rel > 0)
+    assert tight.sum() >= 20, tight.sum()
+    assert (tight & hi_wins).sum() >= 5, (tight & hi_wins).sum()
+    assert in_band > 0
+
+
+@pytest.mark.parametrize("plan,method", [("FSK8_FREQS", FOLDED), ("FSK8_ODD", RESIDUE),
+                                         ("FSK8_FREQS", GOERTZEL)])
+def test_exact_fp32_ties_go_to_lowest_tone(A, torch, plan, method):
+    """Windows with every tone at exactly 0 power (silence, and tones off the
+    plan on another bin) — exact ties in fp32 — decide the lowest tone."""
+    freqs = A.FSK8_FREQS if plan == "FSK8_FREQS" else FSK8_ODD
+    x = np.zeros((4, 1024), np.int16)
+    with A.Demodulator(freqs=freqs, method=method) as d:
+        sym, mag = d.batch(x, mags=True)
+    assert (sym == 0).all() and (mag == 0).all()
+
+
+@pytest.mark.parametrize("sigma", [400, 2000])
+@pytest.mark.parametrize("plan", ["FSK2_FREQS", "FSK8_FREQS"])
+def test_decision_margins_at_bench_levels(A, O, torch, sigma, plan):
+    """The bench signal at sigma 400 (parity level) and 2000 (stress): count
+    the windows whose oracle top-2 margin falls inside the fp32 band, and
+    check every decision (the full-size bench stream uses the same generator)."""
+    freqs = getattr(A, plan)
+    W = 32768
+    cfg = A.make_cfg(freqs=freqs)
+    d_pcm = torch.empty((W, 1024), dtype=torch.int16, device="cuda")
+    d_true = torch.empty(W, dtype=torch.uint8, device="cuda")
+    d_sym = torch.empty(W, dtype=torch.uint8, device="cuda")
+    d_mag = torch.empty((W, len(freqs)), dtype=torch.float32, device="cuda")
+    A.synth_fsk(cfg, A.BENCH_SEED ^ sigma, W, 8000, sigma, d_pcm, d_true)
+    with A.Demodulator(cfg) as d:
+        d.batch_device(d_pcm, W, d_sym, d_mag)
+    ref_sym, ref_P = O.goertzel(d_pcm.cpu().numpy(), freqs, 1024, threads=8)
+    sym, mag = d_sym.cpu().numpy(), d_mag.cpu().numpy()
+    in_band = check_decisions(sym, mag, ref_sym, ref_P)
+    print(f"\n{plan} sigma {sigma}: {in_band} of {W} windows inside the fp32 band, "
+          f"{int((sym != d_true.cpu().numpy()).sum())} transmitted-symbol errors")
+    if sigma == 400:
+        assert in_band == 0 and (sym == d_true.cpu().numpy()).all()

@@ -7,6 +7,8 @@ window, P_ref from the double-precision oracle.
 import numpy as np
 import pytest
 
+from decision import check_decisions
+
 pytestmark = pytest.mark.gpu
 
 MAG_TOL = 1e-5  # relative to the window's max_k P_ref (north_star)
@@ -37,6 +39,7 @@ def run_case(A, O, freqs, n=1024, W=257, hop=None, seed=1, amplitude=8000, sigma
         sym, mag = d.batch(flat, n_windows=Wh, mags=True)
     ref_sym, ref_P = O.goertzel(flat, freqs, n, hop, Wh)
     assert sym.shape == ref_sym.shape
+    check_decisions(sym, mag, ref_sym, ref_P)
     mism = int((sym != ref_sym).sum())
     err = rel_err(mag, ref_P)
     assert mism == 0, f"{mism} symbol mismatches"
@@ -256,6 +259,8 @@ def test_zero_and_extreme_input(A, O, torch, method):
     posed = margin > 4 * MAG_TOL
     assert set(np.flatnonzero(~posed)) <= {0, 1, 2, 3, 5}  # 5: impulse, P = 1 at every tone
     assert (sym[posed] == ref_sym[posed]).all()
+    # and on every window, ties included: the exact argmax of the returned powers
+    check_decisions(sym, mag, ref_sym, ref_P, np.maximum(denom, 1e-30))
 
 
 @pytest.mark.parametrize("method", [GOERTZEL, RESIDUE])
@@ -287,6 +292,7 @@ def test_extreme_input_every_residue_class(A, O, torch, method):
     posed = (Ps[:, -1] - Ps[:, -2]) / denom > 4 * MAG_TOL
     assert posed[[4, 5, 6, 7, 8, 9, 10]].all()
     assert (sym[posed] == ref_sym[posed]).all()
+    check_decisions(sym, mag, ref_sym, ref_P, denom)
 
 
 @pytest.mark.parametrize("freqs,method", [("FSK8_FREQS", FOLDED), ("FSK8_ODD", RESIDUE),
@@ -296,8 +302,7 @@ def test_ties_k8(A, O, torch, freqs, method):
     window: every power 0) goes to the lowest tone. A unit impulse puts
     exactly equal power x^2 on every tone too, but the fp32 powers differ by
     ~1e-6 relative (rounding of the rotation constants, amplified by the
-    recurrence), more than the 2^-19 tie band: an ill-posed decision, so only
-    its magnitudes are checked (within the 1e-5 bar)."""
+    recurrence): the symbol is then the exact argmax of those fp32 powers."""
     f = {"FSK8_FREQS": A.FSK8_FREQS, "FSK8_ODD": FSK8_ODD,
          "NONINT8": tuple(1234.5 + 1111.1 * i for i in range(8))}[freqs]
     n = 1024
@@ -308,9 +313,12 @@ def test_ties_k8(A, O, torch, freqs, method):
         assert d.method == method
         sym, mag = d.batch(x, mags=True)
     assert sym[0] == 0 and sym[5] == 0 and (mag[0] == 0).all() and (mag[5] == 0).all()
-    _, ref_P = O.goertzel(x, f, n)
+    ref_sym, ref_P = O.goertzel(x, f, n)
     for r in range(1, 5):
         assert np.abs(mag[r] / ref_P[r] - 1).max() <= MAG_TOL  # every tone at x^2
+    # the impulse windows are exact mathematical ties: the pick is still the
+    # exact argmax of the returned fp32 powers
+    check_decisions(sym, mag, ref_sym, ref_P)
 
 
 def test_device_pointers_and_async(A, O, torch):
@@ -375,6 +383,49 @@ def test_streaming_demodulate(A, O, torch, channels, mode):
     want = np.concatenate(want)
     assert got.size == want.size == 40
     assert (got == want).all()
+
+
+@pytest.mark.parametrize("channels,lead_in,hop", [(2, 312, 1024), (1, 312, 256), (2, 5000, 1024),
+                                                  (1, 0, 1024)])
+def test_streaming_lead_in(A, O, torch, channels, lead_in, hop):
+    """cfg.lead_in drops the stream's first frames before windowing (the Opus
+    decoder delay, DEMOD_OPUS_LOOKAHEAD = 312, OpusEncoder.kt:65-67): packets
+    shorter and longer than the lead-in, demod_reset re-arms it, and the
+    result equals the oracle's streaming restatement with the same skip."""
+    n = 1024
+    L, truth = O.synth_fsk(A.FSK8_FREQS, n, 30, 313 + channels)
+    R, _ = O.synth_fsk(A.FSK8_FREQS, n, 30, 314 + channels)
+    # the transmitter's symbols, delayed by lead_in samples of decoder output
+    pre = np.random.default_rng(lead_in).integers(-3000, 3000, lead_in).astype(np.int16)
+    mono = np.concatenate([pre, L.reshape(-1)])
+    right = np.concatenate([pre[::-1], R.reshape(-1)])
+    stream = mono if channels == 1 else np.stack([mono, right], axis=1).reshape(-1)
+    sizes = [100, 200, 2880, 1, 7, 2880, 4000]
+    for attempt in range(2):   # the second pass runs after demod_reset
+        ref = O.Stream(A.FSK8_FREQS, n=n, hop=hop, channels=channels, lead_in=lead_in)
+        got, want = [], []
+        if attempt == 0:
+            d = A.Demodulator(A.make_cfg(freqs=A.FSK8_FREQS, hop=hop, channels=channels,
+                                         lead_in=lead_in))
+        else:
+            d.reset()
+        pos, i = 0, 0
+        total = mono.size
+        while pos < total:
+            fr = sizes[i % len(sizes)]
+            i += 1
+            chunk = stream[pos * channels:(pos + fr) * channels]
+            pos += fr
+            assert d.max_symbols(chunk.size // channels) >= 0
+            got.append(d.demodulate(chunk))
+            want.append(ref.push(chunk)[0])
+            assert d.pending() == ref.pending()
+        got, want = np.concatenate(got), np.concatenate(want)
+        assert got.size == want.size == (30 * n - n) // hop + 1
+        assert (got == want).all()
+        if hop == n:
+            assert (got == truth).all()   # aligned with the transmitted symbols
+    d.close()
 
 
 def test_streaming_buffer_too_small_consumes_nothing(A, torch):

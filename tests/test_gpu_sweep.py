@@ -12,6 +12,8 @@ then carry near-equal power); such ties must stay rare.
 import numpy as np
 import pytest
 
+from decision import check_decisions
+
 pytestmark = pytest.mark.gpu
 
 MAG_TOL = 1e-5
@@ -108,6 +110,7 @@ def test_random_case(A, O, torch, i):
     assert posed.mean() >= (0.99 if hop % n == 0 else 0.75), c
     bad = np.flatnonzero(posed & (sym != ref_sym))
     assert bad.size == 0, (bad[:8], c)
+    check_decisions(sym, mag, ref_sym, ref_P, denom)
 
 
 N_STREAM_CASES = 40
@@ -165,6 +168,7 @@ def test_random_stream(A, O, torch, i):
         else np.ones(gs.size, bool)
     bad = np.flatnonzero(posed & (gs != ws))
     assert bad.size == 0, (bad[:8], c)
+    check_decisions(gs, gm, ws, wP, denom)
 
 
 N_STRUCT_CASES = 24
@@ -214,5 +218,6 @@ def test_random_permuted_plans(A, O, torch, i):
     posed = (Ps[:, -1] - Ps[:, -2]) / denom > 4 * MAG_TOL
     bad = np.flatnonzero(posed & (sym != ref_sym))
     assert bad.size == 0, (bad[:8], kind, list(bins))
+    check_decisions(sym, mag, ref_sym, ref_P, denom)
     if hop == 1024:
         assert posed.mean() >= 0.99

@@ -73,7 +73,29 @@ def test_concurrent_handles(A, O, torch):
         except Exception as e:  # surfaced below
             errors.append((i, "exception", repr(e)))
 
+    # the handle-less entry points too: demod_synth_fsk (module sine table,
+    # filled once per device under a lock) and demod_read_ceiling_async, from
+    # several threads at once, each into its own buffers
+    synth_ref = O.synth_fsk(A.FSK8_FREQS, n, 300, 4242, 8000, 400)
+
+    def synth_worker(i):
+        try:
+            cfg = A.make_cfg(freqs=A.FSK8_FREQS)
+            for rep in range(6):
+                d_pcm = torch.empty((300, n), dtype=torch.int16, device="cuda")
+                d_sym = torch.empty(300, dtype=torch.uint8, device="cuda")
+                s = torch.cuda.Stream()
+                A.synth_fsk(cfg, 4242, 300, 8000, 400, d_pcm, d_sym, stream=s.cuda_stream)
+                A.read_ceiling_async(d_pcm, 300 * n * 2 // 8192 * 8192, stream=s.cuda_stream)
+                s.synchronize()
+                if not (np.array_equal(d_pcm.cpu().numpy(), synth_ref[0])
+                        and np.array_equal(d_sym.cpu().numpy(), synth_ref[1])):
+                    errors.append((i, rep, "synth"))
+        except Exception as e:
+            errors.append((i, "synth exception", repr(e)))
+
     threads = [threading.Thread(target=worker, args=(i,)) for i in range(len(jobs))]
+    threads += [threading.Thread(target=synth_worker, args=(100 + i,)) for i in range(4)]
     for t in threads:
         t.start()
     for t in threads:

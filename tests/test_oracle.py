@@ -219,3 +219,23 @@ def test_reference_fft_golden_is_live_reference_output(O):
 def test_oracle_rejects_too_many_tones(O):
     with pytest.raises(ValueError):
         O.goertzel(np.zeros(64, np.int16), [100.0] * 65, 64)
+
+
+def test_stream_lead_in_drops_frames(O):
+    """oracle.Stream(lead_in=L) equals the plain stream over pcm[L:] (the
+    demod_cfg_t.lead_in contract), whatever the packet sizes."""
+    import numpy as np
+    pcm, _ = O.synth_fsk((1500.0, 3000.0), 1024, 12, 99)
+    x = pcm.reshape(-1)
+    for L in (0, 1, 312, 1024, 5000):
+        s = O.Stream((1500.0, 3000.0), lead_in=L)
+        got = np.concatenate([s.push(x[i:i + 2880])[0] for i in range(0, x.size, 2880)])
+        want, _ = O.goertzel(x[L:], (1500.0, 3000.0), 1024)
+        assert np.array_equal(got, want)
+        assert s.pending() == (x.size - L) % 1024
+    st = np.empty(2 * x.size, np.int16)
+    st[0::2], st[1::2] = x, -x
+    s = O.Stream((1500.0, 3000.0), channels=2, channel_mode=1, lead_in=312)
+    got = np.concatenate([s.push(st[i:i + 5760])[0] for i in range(0, st.size, 5760)])
+    want, _ = O.goertzel(-x[312:], (1500.0, 3000.0), 1024)
+    assert np.array_equal(got, want)
