@@ -72,6 +72,7 @@ struct FftParams {
     const float *tw512;      // [512][2]  e^{-2 pi i m / 512}
     const float *tw1024;     // [512][2]  e^{-2 pi i k / 1024}
     const int *bins;         // [k] tone bins round(f n / fs), device
+    int slot[kMaxTones];     // fft_quad_slot(bin) of each tone (quad2 register pick)
     uint8_t *sym;
     float *mag;              // [n_windows][k] or nullptr
     float *spec;             // [n_windows][513] or nullptr
@@ -105,6 +106,7 @@ hipError_t synth_prepare();  // upload the sine table to the current device (onc
 hipError_t launch_synth(const SynthParams &p, hipStream_t s);
 hipError_t launch_read_ceiling(const int16_t *p, long long n_bytes, hipStream_t s);
 hipError_t launch_fft_quad(const FftParams &p, hipStream_t s);  // 16 lanes / window (fft_quad.hip)
+int fft_quad_slot(int bin);  // where fft_quad keeps |X[bin]|^2: 2 (16 j + t) + half, or 512 (bin 256)
 // ip.proto framing of [n_streams][n] symbols, one frame run per stream (frame_gpu.hip)
 long long frame_streams_size(long long n, int bits, long long max_payload, unsigned *per,
                              unsigned *full, int *frames);

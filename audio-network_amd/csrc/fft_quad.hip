@@ -307,6 +307,172 @@ __device__ __forceinline__ void dft(f2 *x)
     }
 }
 
+// ---- fused twiddle butterflies (fft1024_quad2_kernel) ---------------------
+// A twiddled radix-2 butterfly (u, v) = (x + w y, x - w y) in three packed
+// FMAs instead of a complex product (2) and two complex adds (2):
+//   t = fma(y, w.xx, x)                    = (x.x + w.x y.x, x.y + w.x y.y)
+//   u = fma(y.yx, (-w.y, w.y), t)          = x + w y
+//   v = fma(x, 2, -u)                      = x - w y
+// (v is 2x - u: one extra rounding of u, far inside the 1e-5 bar.) The -j w
+// of a radix-4 butterfly's second output pair is the same register read with
+// other op_sel / neg modifiers (-j w = (w.y, -w.x)), so it needs no table.
+// Two independent pairs per asm block, interleaved so no packed result feeds
+// the next instruction (gfx950 packed-fp32 write -> dependent read hazard).
+#define QTB_T(U, Y, W, X) "v_pk_fma_f32 " U ", " Y ", " W ", " X " op_sel_hi:[1,0,1]\n\t"
+#define QTB_U(U, Y, W) "v_pk_fma_f32 " U ", " Y ", " W ", " U " op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_lo:[0,1,0]\n\t"
+#define QTB_TM(U, Y, W, X) "v_pk_fma_f32 " U ", " Y ", " W ", " X " op_sel:[0,1,0] op_sel_hi:[1,1,1]\n\t"
+#define QTB_UM(U, Y, W) "v_pk_fma_f32 " U ", " Y ", " W ", " U " op_sel:[1,0,0] op_sel_hi:[0,0,1] neg_hi:[0,1,0]\n\t"
+#define QTB_V(V, X, TWO, U) "v_pk_fma_f32 " V ", " X ", " TWO ", " U " neg_lo:[0,0,1] neg_hi:[0,0,1]"
+
+// pair 0 with w0, pair 1 with w1 (both SGPR pairs: compile-time constants)
+__device__ __forceinline__ void tbk2(f2 &u0, f2 &v0, f2 x0, f2 y0, f2 w0, f2 &u1, f2 &v1, f2 x1,
+                                     f2 y1, f2 w1)
+{
+    asm(QTB_T("%0", "%5", "%6", "%4") QTB_T("%2", "%8", "%9", "%7")
+        QTB_U("%0", "%5", "%6") QTB_U("%2", "%8", "%9")
+        QTB_V("%1", "%4", "%10", "%0") "\n\t" QTB_V("%3", "%7", "%10", "%2")
+        : "=&v"(u0), "=&v"(v0), "=&v"(u1), "=&v"(v1)
+        : "v"(x0), "v"(y0), "s"(w0), "v"(x1), "v"(y1), "s"(w1), "s"((f2){2.0f, 2.0f}));
+}
+// pair 0 with w, pair 1 with -j w (MJ1) or w (!MJ1); w a VGPR pair (per-lane table)
+template <bool MJ1>
+__device__ __forceinline__ void tbv2(f2 &u0, f2 &v0, f2 x0, f2 y0, f2 &u1, f2 &v1, f2 x1, f2 y1,
+                                     f2 w)
+{
+    if constexpr (MJ1)
+        asm(QTB_T("%0", "%5", "%8", "%4") QTB_TM("%2", "%7", "%8", "%6")
+            QTB_U("%0", "%5", "%8") QTB_UM("%2", "%7", "%8")
+            QTB_V("%1", "%4", "%9", "%0") "\n\t" QTB_V("%3", "%6", "%9", "%2")
+            : "=&v"(u0), "=&v"(v0), "=&v"(u1), "=&v"(v1)
+            : "v"(x0), "v"(y0), "v"(x1), "v"(y1), "v"(w), "s"((f2){2.0f, 2.0f}));
+    else
+        asm(QTB_T("%0", "%5", "%8", "%4") QTB_T("%2", "%7", "%8", "%6")
+            QTB_U("%0", "%5", "%8") QTB_U("%2", "%7", "%8")
+            QTB_V("%1", "%4", "%9", "%0") "\n\t" QTB_V("%3", "%6", "%9", "%2")
+            : "=&v"(u0), "=&v"(v0), "=&v"(u1), "=&v"(v1)
+            : "v"(x0), "v"(y0), "v"(x1), "v"(y1), "v"(w), "s"((f2){2.0f, 2.0f}));
+}
+
+// W32^E trivial (a quarter turn)?
+constexpr bool w32_trivial(int e) { return (((e % 32) + 32) % 32) % 8 == 0; }
+template <int E>
+__device__ __forceinline__ f2 w32c()
+{
+    constexpr int j = ((E % 32) + 32) % 32;
+    return (f2){kW32r[j], kW32i[j]};
+}
+// (u, v) = (x + W32^E y, x - W32^E y) for a quarter-turn E
+template <int E>
+__device__ __forceinline__ void tb_triv(f2 &u, f2 &v, f2 x, f2 y)
+{
+    constexpr int j = ((E % 32) + 32) % 32;
+    static_assert(j % 8 == 0, "quarter turn");
+    if constexpr (j == 0) { u = x + y; v = x - y; }
+    else if constexpr (j == 16) { u = x - y; v = x + y; }
+    else if constexpr (j == 8) { u = add_mj(x, y); v = sub_mj(x, y); }   // w = -j
+    else { u = sub_mj(x, y); v = add_mj(x, y); }                          // w = +j
+}
+// two pairs, W32^E0 and W32^E1, both trivial or both not
+template <int E0, int E1>
+__device__ __forceinline__ void tbk2c(f2 &u0, f2 &v0, f2 x0, f2 y0, f2 &u1, f2 &v1, f2 x1, f2 y1)
+{
+    static_assert(w32_trivial(E0) == w32_trivial(E1), "pair kinds");
+    if constexpr (w32_trivial(E0)) {
+        tb_triv<E0>(u0, v0, x0, y0);
+        tb_triv<E1>(u1, v1, x1, y1);
+    } else {
+        tbk2(u0, v0, x0, y0, w32c<E0>(), u1, v1, x1, y1, w32c<E1>());
+    }
+}
+
+// DFT-4 of (y0, w y1, w^2 y2, w^3 y3) at x[0], x[S], x[2S], x[3S] (natural
+// order out), w = W32^E: four fused butterflies,
+//   a = y0 +- w^2 y2, c = y1 +- w^2 y3, X0/X2 = a0 +- w c0, X1/X3 = a1 +- (-j w) c1.
+template <int E, int S>
+__device__ __forceinline__ void dft4_geo_k(f2 *x)
+{
+    f2 a0, a1, c0, c1;
+    tbk2c<2 * E, 2 * E>(a0, a1, x[0], x[2 * S], c0, c1, x[S], x[3 * S]);
+    f2 X0, X1, X2, X3;
+    tbk2c<E, E + 8>(X0, X2, a0, c0, X1, X3, a1, c1);
+    x[0] = X0;
+    x[S] = X1;
+    x[2 * S] = X2;
+    x[3 * S] = X3;
+}
+// the same with a per-lane w (VGPRs) and its square w2
+template <int S>
+__device__ __forceinline__ void dft4_geo_v(f2 *x, f2 w, f2 w2)
+{
+    f2 a0, a1, c0, c1;
+    tbv2<false>(a0, a1, x[0], x[2 * S], c0, c1, x[S], x[3 * S], w2);
+    f2 X0, X1, X2, X3;
+    tbv2<true>(X0, X2, a0, c0, X1, X3, a1, c1, w);
+    x[0] = X0;
+    x[S] = X1;
+    x[2 * S] = X2;
+    x[3 * S] = X3;
+}
+
+// In-register DFT of x[0], x[S], .., x[(N-1) S] (N = 4, 8, 16, 32), natural
+// order out, every twiddle fused into the butterfly that consumes it.
+// Mixed radix N = N1 x N2 (N2 = 4, or 2 at N = 8): DFT-N1 over i1 for each i2,
+// then per k1 a DFT-N2 over i2 of the twiddled column, which is geometric in
+// w = W_N^{k1} (dft4_geo_k).
+template <int N, int S = 1>
+__device__ __forceinline__ void dftf(f2 *x)
+{
+    if constexpr (N == 4) {
+        dft4_geo_k<0, S>(x);
+    } else if constexpr (N == 8) {
+        dftf<4, 2 * S>(x);       // i2 = 0: X[k1] at slot 2 k1
+        dftf<4, 2 * S>(x + S);   // i2 = 1: X[k1] at slot 2 k1 + 1
+        // per k1: (slot 2k1, slot 2k1+1) -> X[k1], X[k1 + 4], twiddle W8^k1 = W32^{4 k1}
+        f2 u0, v0, u1, v1, u2, v2, u3, v3;
+        tb_triv<0>(u0, v0, x[0], x[S]);
+        tb_triv<8>(u2, v2, x[4 * S], x[5 * S]);
+        tbk2c<4, 12>(u1, v1, x[2 * S], x[3 * S], u3, v3, x[6 * S], x[7 * S]);
+        x[0] = u0; x[S] = u1; x[2 * S] = u2; x[3 * S] = u3;
+        x[4 * S] = v0; x[5 * S] = v1; x[6 * S] = v2; x[7 * S] = v3;
+    } else {
+        constexpr int N1 = N / 4;   // 8 (N = 32) or 4 (N = 16)
+        static_for<0, 4>([&](auto c) {
+            constexpr int i2 = decltype(c)::value;
+            dftf<N1, 4 * S>(x + i2 * S);   // X[k1] of column i2 at slot i2 + 4 k1
+        });
+        static_for<0, N1>([&](auto d) {
+            constexpr int k1 = decltype(d)::value;
+            dft4_geo_k<k1 * (32 / N), S>(x + 4 * k1 * S);   // slot 4 k1 + k2 = X[k1 + N1 k2]
+        });
+        f2 t[N];
+        static_for<0, N>([&](auto e) {
+            constexpr int m = decltype(e)::value;  // m = 4 k1 + k2
+            t[(m / 4) + N1 * (m % 4)] = x[m * S];
+        });
+        static_for<0, N>([&](auto e) {
+            constexpr int m = decltype(e)::value;
+            x[m * S] = t[m];
+        });
+    }
+}
+
+// Real post-pass with the 1/2 of X = (S + W D)/2 folded into two FMAs (T
+// carries W/2): (S.x/2 + T.x, S.x/2 - T.x) and (S.y/2 + T.y, S.y/2 - T.y)
+__device__ __forceinline__ f2 pp_re_h(f2 S, f2 T)
+{
+    f2 r;
+    asm("v_pk_fma_f32 %0, %1, %3, %2 op_sel_hi:[0,1,0] neg_hi:[0,0,1]"
+        : "=v"(r) : "v"(S), "v"(T), "s"((f2){0.5f, 0.5f}));
+    return r;
+}
+__device__ __forceinline__ f2 pp_im_h(f2 S, f2 T)
+{
+    f2 r;
+    asm("v_pk_fma_f32 %0, %1, %3, %2 op_sel:[1,0,1] neg_hi:[0,0,1]"
+        : "=v"(r) : "v"(S), "v"(T), "s"((f2){0.5f, 0.5f}));
+    return r;
+}
+
 }  // namespace quad
 
 // Per-wave LDS: 4 windows x 16 rows x 17 complex (8704 B). The transpose
@@ -546,6 +712,338 @@ void fft1024_quad_kernel(FftParams p)
     }
 }
 
+// fft1024_quad2_kernel: the quad layout with every twiddle fused into the
+// butterfly that consumes it (dftf, dft4_geo_*), the stage-1 twiddle moved
+// behind the transpose and the 1/2 of the real split folded into the
+// post-pass FMAs:
+//   * stage 1: DFT-32 over n1 (compile-time twiddles fused), transposed raw;
+//   * stage 2: lane t' runs, per column col in {t', k1b}, the DFT-16 over rows
+//     t of A_t[col] W512^{t col}. With t = i2 + 4 i1 the twiddle factors as
+//     W512^{i2 col} W128^{i1 col}: the inner DFT-4 over i1 is geometric in
+//     v = W128^col, and W512^{i2 col} moves onto its outputs, where it joins
+//     W16^{i2 k1} into the outer DFT-4's ratio g_k1 = W512^{col + 32 k1}; per
+//     lane and column v, v^2, g_k1, g_k1^2 come from a 2.5 KiB LDS table
+//     (tw2), -j w by operand modifiers;
+//   * post-pass: T = (W/2) D (tw3 holds W1024^kP / 2), (re, im) pairs by FMA
+//     with 1/2 (pp_re_h / pp_im_h).
+// 514 instead of 575 packed instructions per group of 4 windows.
+// PF: 1 = the next group's 32 loads go out during the transpose (32 VGPRs live
+// across stage 2 and the post-pass), 0 = each group loads at the top of its
+// iteration (co-resident waves cover the latency).
+// SPEC: false = symbols (+ tone powers) only: the tone powers are picked
+// from the registers of the lanes that hold them (p.slot, uniform) instead
+// of going through the 2 KiB per-window power slab in LDS; true = the slab,
+// for the full-spectrum store.
+// RS: row stride in windows. 1 = a wave's 4 windows are consecutive (at hop
+// 256 they overlap by 3/4, so each load instruction re-requests lines its
+// other rows requested a few instructions earlier, still in flight); 4 = the
+// 4 waves of a block interleave over 16 consecutive windows (wave v takes
+// v, v + 4, v + 8, v + 12): no overlap inside a wave, and the neighbours'
+// shared lines are requested by the block's other waves instead.
+// ABL (timing ablations for scripts/fft_probe only, results WRONG when set):
+// bit 0 = load the first group only (no global loads in the loop), bit 1 = no
+// LDS transpose (stage 2 reads stage 1's registers).
+// CM: column-major transpose slab ([col][row], 144 B per column: 16 rows +
+// 16 B pad, 2304 B per window): the rows still go out as ds_write2_b64 pairs,
+// but a lane's column comes back as 8 ds_read_b128 (two rows each, half the
+// LDS cycles of ds_read2_b64); the 36-dword column stride puts the 16 lanes of
+// a window on 64 distinct banks and the windows 576 dwords apart, so every
+// b128 lane group is conflict-free.
+constexpr int kCmCol = 18;                 // f2 per column (16 rows + pad)
+constexpr int kCmWin = 16 * kCmCol;        // f2 per window
+constexpr int kCmSlab = 4 * kCmWin;        // f2 per wave (>= 4 x 544 floats of powers / 2)
+// TWP: read all of a group's stage-2 and post-pass twiddles (20 + 16 complex)
+// right behind the transpose reads, as one batch under the same wait, instead
+// of just in time (the compiler sinks each ds_read to its use, which exposes
+// the LDS latency a dozen times per group).
+// FMT (PF = 0 only): typed buffer loads (16_16 SSCALED) convert both int16
+// halves to fp32 in the texture path instead of 64 VALU converts per group.
+template <int WPB = 4, int MINW = 0, int PF = 1, bool SPEC = true, int RS = 1, int ABL = 0,
+          bool CM = false, bool TWP = false, bool FMT = false>
+__global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MINW > 0 ? MINW : 1)))
+void fft1024_quad2_kernel(FftParams p)
+{
+    using namespace quad;
+    __shared__ __attribute__((aligned(16))) f2 slab[WPB][CM ? kCmSlab : kQSlab];
+    __shared__ f2 tw2[2 * 10 * 16];  // [column slot][v, v2, g0, g0^2, .., g3, g3^2][t]
+    __shared__ f2 tw3[16 * 16];      // post-pass W1024^{kP(t, j)} / 2 at [j][t]
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int q = lane >> 4;   // window of the wave
+    const int t = lane & 15;   // row / column-pair index
+    const f2 *t512 = reinterpret_cast<const f2 *>(p.tw512);
+    const f2 *t1024 = reinterpret_cast<const f2 *>(p.tw1024);
+    for (int i = threadIdx.x; i < 2 * 10 * 16; i += 64 * WPB) {
+        const int tt = i & 15, m = (i >> 4) % 10, sl = i / 160;
+        const int col = sl == 0 ? tt : (tt == 0 ? 16 : 32 - tt);
+        int e;  // exponent of W512
+        if (m == 0) e = 4 * col;                          // v = W128^col
+        else if (m == 1) e = 8 * col;                     // v^2
+        else {
+            const int k1 = (m - 2) >> 1;
+            e = (col + 32 * k1) * (((m - 2) & 1) ? 2 : 1);   // g_k1, g_k1^2
+        }
+        tw2[i] = t512[e & 511];
+    }
+    for (int i = threadIdx.x; i < 16 * 16; i += 64 * WPB) {
+        const int tt = i & 15, j = i >> 4;
+        tw3[i] = 0.5f * t1024[(tt == 0 && j >= 8) ? 16 + 32 * (j - 8) : tt + 32 * j];
+    }
+    const int k1b = t == 0 ? 16 : 32 - t;
+    const int myslot = quad_slot(t < p.k ? p.bins[t] : 0);
+    float *pw = reinterpret_cast<float *>(slab[wave]);
+    __syncthreads();
+
+    const long long n_groups = (p.n_windows + 3) >> 2;
+    const long long stride = (long long)gridDim.x * WPB;
+    long long g = tile_block(p.xcd_swizzle) * WPB + wave;
+    static_assert(!FMT || PF == 0, "FMT loads straight into a[]");
+    uint32_t nx[FMT ? 1 : 32];
+    f2 nxf[FMT ? 32 : 1];
+    // first window of group gg and the window of row q (RS above)
+    auto gbase = [&](long long gg) -> long long {
+        return RS == 1 ? 4 * gg : 16 * (gg >> 2) + (gg & 3);
+    };
+    auto load_group = [&](long long gg) {
+        const long long w0 = gbase(gg);
+        const long long left = p.n_windows - w0;  // >= 1
+        const long long wq0 = RS * q;
+        const long long wq = wq0 < left ? wq0 : left - 1;
+        long long bytes = ((left - 1) * p.hop + 1024) * 2;
+        if (bytes > 0x7FFFFFF0LL) bytes = 0x7FFFFFF0LL;
+        __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)(p.pcm + w0 * p.hop), (short)0, (int)bytes, 0x00020000);
+        const int voff = (int)(wq * p.hop * 2) + 4 * t;
+        if constexpr (FMT) {
+            const unsigned long long base = (unsigned long long)(p.pcm + w0 * p.hop);
+            const i4 rf = {(int)(unsigned)base, (int)((base >> 32) & 0xFFFF), (int)bytes, kFmtWord3};
+#pragma unroll
+            for (int n1 = 0; n1 < 32; ++n1)
+                nxf[n1] = raw_buffer_load_format_v2f32(rf, voff + 64 * n1, 0, 2);
+        } else {
+#pragma unroll
+            for (int n1 = 0; n1 < 32; ++n1)
+                nx[n1] = __builtin_amdgcn_raw_buffer_load_b32(rs, voff + 64 * n1, 0, 2);
+        }
+    };
+    static_assert(RS == 1 || (RS == 4 && PF == 0 && WPB % 4 == 0), "RS = 4: no cross-group prefetch");
+    const long long n_groups_rs = RS == 1 ? n_groups : 4 * ((p.n_windows + 15) >> 4);
+    if ((PF || (ABL & 1)) && g < n_groups_rs) load_group(g);
+    for (; g < n_groups_rs; g += stride) {
+        const long long w = gbase(g) + RS * q;
+        if (RS != 1 && gbase(g) >= p.n_windows) continue;  // wave-uniform: a group past the end
+        if (!PF && !(ABL & 1)) load_group(g);
+        f2 a[32];
+#pragma unroll
+        for (int n1 = 0; n1 < 32; ++n1) {
+            if constexpr (FMT) {
+                a[n1] = nxf[n1];
+                continue;
+            }
+            a[n1] = (f2){(float)(int)(short)(nx[FMT ? 0 : n1] & 0xFFFFu),
+                         (float)((int)nx[FMT ? 0 : n1] >> 16)};
+            asm("" : "+v"(a[n1]));  // opaque: keep (float)a + (float)b a packed add
+        }
+
+        // 1. DFT-32 over n1 (fused twiddles), no stage-1 twiddle here
+        dftf<32>(a);
+
+        // 2. transpose in two column rounds; lane (q, t') gets columns
+        //    k1 = t' (round 0) and k1b (round 1) of its window
+        f2 b[32];  // b[n2] = A_n2[t'], b[16 + n2] = A_n2[k1b]
+        f2 *win = slab[wave] + q * (CM ? kCmWin : kQWin);
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            if constexpr ((ABL & 2) != 0) {
+#pragma unroll
+                for (int n2 = 0; n2 < 16; ++n2) b[16 * r + n2] = a[16 * r + n2];
+                continue;
+            }
+            if constexpr (CM) {
+#pragma unroll
+                for (int c = 0; c < 16; ++c) win[c * kCmCol + t] = a[16 * r + c];
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                if (PF && !(ABL & 1) && r == 0) load_group(g + stride < n_groups_rs ? g + stride : g);
+                const int col = r == 0 ? t : k1b - 16;
+                typedef float f4 __attribute__((ext_vector_type(4)));
+                const f4 *cp = reinterpret_cast<const f4 *>(win + col * kCmCol);
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    const f4 v = cp[i];
+                    b[16 * r + 2 * i] = (f2){v.x, v.y};
+                    b[16 * r + 2 * i + 1] = (f2){v.z, v.w};
+                }
+                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                continue;
+            }
+#pragma unroll
+            for (int c = 0; c < 16; ++c) win[t * kQRow + c] = a[16 * r + c];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (PF && !(ABL & 1) && r == 0) load_group(g + stride < n_groups_rs ? g + stride : g);
+            const int col = r == 0 ? t : k1b - 16;
+#pragma unroll
+            for (int n2 = 0; n2 < 16; ++n2) b[16 * r + n2] = win[n2 * kQRow + col];
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+        }
+        // 3. per column: DFT-16 over t of A_t[col] W512^{t col}, twiddles fused
+        f2 twr[TWP ? 36 : 1];  // TWP: [col slot][10] stage-2 twiddles, then the 16 tw3
+        if constexpr (TWP) {
+#pragma unroll
+            for (int m = 0; m < 20; ++m) twr[m] = tw2[(m / 10) * 160 + (m % 10) * 16 + t];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) twr[20 + j] = tw3[16 * j + t];
+#pragma unroll
+            for (int m = 0; m < 36; ++m) asm volatile("" : "+v"(twr[m]));
+        }
+        auto twv = [&](int sl, int m) -> f2 {
+            return TWP ? twr[sl * 10 + m] : tw2[sl * 160 + m * 16 + t];
+        };
+#pragma unroll
+        for (int sl = 0; sl < 2; ++sl) {
+            f2 *bb = b + 16 * sl;
+            const f2 v = twv(sl, 0), v2 = twv(sl, 1);
+            static_for<0, 4>([&](auto c) {
+                constexpr int i2 = decltype(c)::value;
+                dft4_geo_v<4>(bb + i2, v, v2);   // column i2's X[k1] at slot i2 + 4 k1
+            });
+            static_for<0, 4>([&](auto d) {
+                constexpr int k1 = decltype(d)::value;
+                dft4_geo_v<1>(bb + 4 * k1, twv(sl, 2 + 2 * k1), twv(sl, 3 + 2 * k1));
+            });
+            f2 tt[16];
+            static_for<0, 16>([&](auto e) {
+                constexpr int m = decltype(e)::value;  // m = 4 k1 + k2 holds Z[col + 32 (k1 + 4 k2)]
+                tt[(m / 4) + 4 * (m % 4)] = bb[m];
+            });
+            static_for<0, 16>([&](auto e) {
+                constexpr int m = decltype(e)::value;
+                bb[m] = tt[m];
+            });
+        }
+        // b[k2] = Z[t + 32 k2], b[16 + k2] = Z[k1b + 32 k2] (unscaled)
+
+        // 4. real post-pass over 16 mirror pairs, as fft1024_quad_kernel step 3
+        //    with X[kP] = S/2 + (W/2) D and the powers of both mirrors per pair
+        const bool l0 = (t == 0);
+        float *pq = pw + q * kQPow;
+        f2 *const ps = reinterpret_cast<f2 *>(pq) + t;  // slot (j, t) at ps[16 j]
+        // !SPEC: this lane's powers, pv[2 j + half], one 32-register tuple so a
+        // uniform index reads it with v_movrels (no scratch, no select chain)
+        typedef float f32x32 __attribute__((ext_vector_type(32)));
+        f32x32 pv;
+        static_for<0, 8>([&](auto jc) {
+            constexpr int j0 = 2 * decltype(jc)::value, j1 = j0 + 1;
+            f2 P0 = b[j0], Q0 = b[16 + 15 - j0];
+            f2 P1 = b[j1], Q1 = b[16 + 15 - j1];
+            if constexpr (j0 >= 8) {
+                P0 = sel_l0(b[16 + j0 - 8], P0);
+                P1 = sel_l0(b[16 + j1 - 8], P1);
+            }
+            if constexpr (j0 < 8) {
+                Q0 = sel_l0(b[(16 - j0) & 15], Q0);
+                Q1 = sel_l0(b[(16 - j1) & 15], Q1);
+            } else {
+                Q0 = sel_l0(b[16 + 23 - j0], Q0);
+                Q1 = sel_l0(b[16 + 23 - j1], Q1);
+            }
+            f2 pw0, pw1;  // (|X[kP]|^2, |X[512-kP]|^2)
+            const f2 S0 = pp_s(P0, Q0), S1 = pp_s(P1, Q1);
+            const f2 D0 = pp_d(P0, Q0), D1 = pp_d(P1, Q1);
+            f2 T0, T1;
+            cmul2(T0, D0, TWP ? twr[20 + j0] : tw3[16 * j0 + t], T1, D1,
+                  TWP ? twr[20 + j1] : tw3[16 * j1 + t]);
+            const f2 re0 = pp_re_h(S0, T0), re1 = pp_re_h(S1, T1);
+            const f2 im0 = pp_im_h(S0, T0), im1 = pp_im_h(S1, T1);
+            pwr2(pw0, re0, im0, pw1, re1, im1);
+            if constexpr (SPEC) {
+                ps[16 * j0] = pw0;
+                ps[16 * j1] = pw1;
+            } else {
+                pv[2 * j0] = pw0.x;
+                pv[2 * j0 + 1] = pw0.y;
+                pv[2 * j1] = pw1.x;
+                pv[2 * j1 + 1] = pw1.y;
+            }
+        });
+        // Z[256] is its own mirror: |X[256]|^2 = |Z[256]|^2
+        const float p256 = fmaf(b[8].x, b[8].x, b[8].y * b[8].y);
+        const bool live = w < p.n_windows;
+        float pk = -1.f;
+        int arg = t;
+        if constexpr (SPEC) {
+            if (l0) pq[512] = p256;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            // 5. tone pick (as fft1024_quad_kernel step 4)
+            if (t < p.k) pk = pq[myslot];
+            if (live && t < p.k && p.mag) p.mag[w * p.k + t] = pk;
+        } else {
+            // 5. tone pick from registers: tone i's power sits in lane
+            //    (slot >> 1) & 15 of each window row at pv[slot >> 5 | half]
+            //    (uniform index); each lane keeps the best tone it owns (first
+            //    index on ties), then the row argmax below
+            arg = 16;
+#pragma unroll
+            for (int i = 0; i < kMaxTones; ++i) {
+                if (i >= p.k) break;
+                const int f = p.slot[i];
+                const bool own = f == 512 ? l0 : t == ((f >> 1) & 15);
+                const float val = f == 512 ? p256 : pv[((f >> 5) << 1) | (f & 1)];
+                if (own && live && p.mag) p.mag[w * p.k + i] = val;
+                if (own && val > pk) {
+                    pk = val;
+                    arg = i;
+                }
+            }
+        }
+        static_for<0, 4>([&](auto sc) {
+            constexpr int ctrl = 0x120 + (1 << decltype(sc)::value);
+            const float po = __int_as_float(
+                __builtin_amdgcn_update_dpp(0, __float_as_int(pk), ctrl, 0xF, 0xF, false));
+            const int ao = __builtin_amdgcn_update_dpp(0, arg, ctrl, 0xF, 0xF, false);
+            const bool take = (po > pk) | ((po == pk) & (ao < arg));
+            pk = take ? po : pk;
+            arg = take ? ao : arg;
+        });
+        if (live && t == 0) p.sym[w] = (uint8_t)arg;
+        if constexpr (SPEC) {
+            if (p.spec && live) {
+                float *so = p.spec + w * 513;
+                for (int i = t; i < 513; i += 16) so[i] = pq[quad_slot(i)];
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+}
+
+template <int WPB, int MINW, int PF = 1, bool SPEC = true, int RS = 1, int ABL = 0, bool CM = false,
+          bool TWP = false, bool FMT = false>
+hipError_t launch_fft_quad2_t(const FftParams &p, hipStream_t s)
+{
+    int dev = 0, cus = 256, per_cu = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fft1024_quad2_kernel<WPB, MINW, PF, SPEC, RS, ABL, CM, TWP, FMT>,
+                                                     64 * WPB, 0) != hipSuccess ||
+        per_cu < 1)
+        per_cu = 1;
+    const long long groups = (p.n_windows + 3) / 4;
+    long long blocks = (groups + WPB - 1) / WPB;
+    blocks = std::min<long long>(blocks, (long long)cus * per_cu);
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL((fft1024_quad2_kernel<WPB, MINW, PF, SPEC, RS, ABL, CM, TWP, FMT>), dim3((unsigned)blocks), dim3(64 * WPB),
+                       0, s, p);
+    return hipGetLastError();
+}
+
 // Persistent grid: as many blocks as fit the chip, each wave strides over
 // groups of 4 windows (the LDS twiddle tables are built once per block).
 template <int WPB, int MINW, bool SPLIT = false, bool FUSE = false, bool FMT = false>
@@ -571,5 +1069,13 @@ hipError_t launch_fft_quad(const FftParams &p, hipStream_t s)
 {
     return launch_fft_quad_t<4, 0>(p, s);
 }
+
+// probe / A-B entry of the fused-twiddle kernel
+hipError_t launch_fft_quad2(const FftParams &p, hipStream_t s)
+{
+    return launch_fft_quad2_t<4, 0>(p, s);
+}
+
+int fft_quad_slot(int bin) { return quad_slot(bin); }
 
 }  // namespace fskd

@@ -1,0 +1,191 @@
+// fft_probe.hip — interleaved A/B of FFT-detector kernel variants (config 4).
+//
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -Iinclude scripts/fft_probe.hip -o scripts/bin/fft_probe
+//   scripts/bin/fft_probe [hop=256] [rounds=6] [reps=10] [filter]
+//
+// One process, round-robin over variants on the same seeded 2^30-sample
+// stream (cdna_hip_programming.md §5.4 rule 24): min / median kernel time from
+// HIP events. Every variant's symbols and tone powers are compared with the
+// shipped kernel's on all windows, and the full 513-bin spectra on a 4096-window
+// sample (max |dP| relative to the window's peak bin, the 1e-5 bar).
+#include "../audio-network_amd/csrc/fft_quad.hip"
+#include "../audio-network_amd/csrc/synth.hip"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <string>
+#include <vector>
+
+using namespace fskd;
+
+#define CK(x)                                                                   \
+    do {                                                                        \
+        hipError_t e_ = (x);                                                    \
+        if (e_ != hipSuccess) {                                                 \
+            std::fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x,      \
+                         hipGetErrorString(e_));                                \
+            std::exit(1);                                                       \
+        }                                                                       \
+    } while (0)
+
+struct Var {
+    std::string name;
+    std::function<hipError_t(const FftParams &, hipStream_t)> launch;
+    std::vector<float> ms;
+};
+
+int main(int argc, char **argv)
+{
+    const int hop = argc > 1 ? std::atoi(argv[1]) : 256;
+    const int rounds = argc > 2 ? std::atoi(argv[2]) : 6;
+    const int reps = argc > 3 ? std::atoi(argv[3]) : 10;
+    const char *filter = argc > 4 ? argv[4] : nullptr;
+    const long long src_windows = 1LL << 20;
+    const long long n_samples = src_windows * 1024;
+    const long long W = (n_samples - 1024) / hop + 1;
+    const int K = 2;
+    const double freqs[2] = {1500.0, 3000.0};
+
+    int16_t *pcm;
+    CK(hipMalloc(&pcm, n_samples * 2));
+    CK(synth_prepare());
+    SynthParams sp;
+    std::memset(&sp, 0, sizeof sp);
+    sp.seed = 0x2C5DA044;
+    sp.n_windows = src_windows;
+    sp.n = 1024;
+    sp.k = K;
+    sp.amplitude = 8000;
+    sp.sigma = 400;
+    sp.pcm = pcm;
+    for (int t = 0; t < K; ++t)
+        sp.inc[t] = (uint32_t)((unsigned long long)std::llround(freqs[t] / 48000.0 * 4294967296.0));
+    CK(launch_synth(sp, nullptr));
+
+    std::vector<float> t1(1024), t2(1024);
+    for (int m = 0; m < 512; ++m) {
+        t1[2 * m] = (float)std::cos(-2.0 * M_PI * m / 512.0);
+        t1[2 * m + 1] = (float)std::sin(-2.0 * M_PI * m / 512.0);
+        t2[2 * m] = (float)std::cos(-2.0 * M_PI * m / 1024.0);
+        t2[2 * m + 1] = (float)std::sin(-2.0 * M_PI * m / 1024.0);
+    }
+    int bins[2] = {32, 64};
+    float *d_t1, *d_t2;
+    int *d_bins;
+    CK(hipMalloc(&d_t1, 4096));
+    CK(hipMalloc(&d_t2, 4096));
+    CK(hipMalloc(&d_bins, 8));
+    CK(hipMemcpy(d_t1, t1.data(), 4096, hipMemcpyHostToDevice));
+    CK(hipMemcpy(d_t2, t2.data(), 4096, hipMemcpyHostToDevice));
+    CK(hipMemcpy(d_bins, bins, 8, hipMemcpyHostToDevice));
+
+    std::vector<Var> vs;
+    vs.push_back({"quad (shipped r1)", [](const FftParams &p, hipStream_t s) { return launch_fft_quad(p, s); }, {}});
+    vs.push_back({"quad2 fused", [](const FftParams &p, hipStream_t s) { return launch_fft_quad2(p, s); }, {}});
+#define Q2(NAME, WPB, MINW, PF, RS, CM, TWP, FMT) vs.push_back({NAME, [](const FftParams &p, hipStream_t s) { return p.spec ? launch_fft_quad2_t<WPB, MINW, PF, true, RS, 0, CM, TWP, FMT>(p, s) : launch_fft_quad2_t<WPB, MINW, PF, false, RS, 0, CM, TWP, FMT>(p, s); }, {}})
+    Q2("FMT PF0", 4, 0, 0, 1, false, false, true);
+    Q2("FMT PF0 MINW4", 4, 4, 0, 1, false, false, true);
+    vs.push_back({"quad2 PF0 MINW4 REG", [](const FftParams &p, hipStream_t s) { return p.spec ? launch_fft_quad2_t<4, 4, 0, true>(p, s) : launch_fft_quad2_t<4, 4, 0, false>(p, s); }, {}});
+    if (filter) {
+        std::vector<Var> keep;
+        for (size_t i = 0; i < vs.size(); ++i)
+            if (i == 0 || vs[i].name.find(filter) != std::string::npos) keep.push_back(vs[i]);
+        vs.swap(keep);
+    }
+
+    FftParams base;
+    std::memset(&base, 0, sizeof base);
+    base.pcm = pcm;
+    base.n_windows = W;
+    base.hop = hop;
+    base.k = K;
+    base.xcd_swizzle = hop < 1024 ? 1 : 0;
+    base.tw512 = d_t1;
+    base.tw1024 = d_t2;
+    base.bins = d_bins;
+    for (int k = 0; k < K; ++k) base.slot[k] = fft_quad_slot(bins[k]);
+    std::vector<uint8_t *> syms(vs.size());
+    std::vector<float *> mags(vs.size()), specs(vs.size());
+    const long long SW = 4096;
+    for (size_t i = 0; i < vs.size(); ++i) {
+        CK(hipMalloc(&syms[i], W));
+        CK(hipMalloc(&mags[i], W * K * 4));
+        CK(hipMalloc(&specs[i], SW * 513 * 4));
+    }
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    // correctness pass: all windows, symbols + tone powers; spectra on SW windows
+    for (size_t i = 0; i < vs.size(); ++i) {
+        FftParams p = base;
+        p.sym = syms[i];
+        p.mag = mags[i];
+        CK(vs[i].launch(p, nullptr));
+        FftParams ps = base;
+        ps.n_windows = SW;
+        ps.sym = syms[i];
+        ps.spec = specs[i];
+        CK(vs[i].launch(ps, nullptr));
+        CK(vs[i].launch(p, nullptr));   // leave all-window symbols in syms
+    }
+    CK(hipDeviceSynchronize());
+    std::vector<uint8_t> s0(W), si(W);
+    std::vector<float> m0(W * K), mi(W * K), sp0(SW * 513), spi(SW * 513);
+    CK(hipMemcpy(s0.data(), syms[0], W, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(m0.data(), mags[0], W * K * 4, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(sp0.data(), specs[0], SW * 513 * 4, hipMemcpyDeviceToHost));
+    for (size_t i = 1; i < vs.size(); ++i) {
+        CK(hipMemcpy(si.data(), syms[i], W, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(mi.data(), mags[i], W * K * 4, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(spi.data(), specs[i], SW * 513 * 4, hipMemcpyDeviceToHost));
+        long long mism = 0;
+        double merr = 0, serr = 0;
+        for (long long w = 0; w < W; ++w) {
+            mism += s0[w] != si[w];
+            double pk = std::max(m0[w * K], m0[w * K + 1]);
+            for (int k = 0; k < K; ++k)
+                merr = std::max(merr, std::fabs((double)mi[w * K + k] - m0[w * K + k]) / std::max(pk, 1e-30));
+        }
+        for (long long w = 0; w < SW; ++w) {
+            double pk = 0;
+            for (int b = 0; b < 513; ++b) pk = std::max(pk, (double)sp0[w * 513 + b]);
+            for (int b = 0; b < 513; ++b)
+                serr = std::max(serr, std::fabs((double)spi[w * 513 + b] - sp0[w * 513 + b]) / std::max(pk, 1e-30));
+        }
+        std::printf("check %-24s vs shipped: %lld symbol mismatches / %lld, max tone |dP|/peak %.2e, "
+                    "spectrum (%lld windows) %.2e\n", vs[i].name.c_str(), mism, W, merr, SW, serr);
+    }
+    // timing: round-robin, symbols + tone powers (the bench's batch_async shape)
+    for (int r = 0; r < rounds; ++r) {
+        for (size_t i = 0; i < vs.size(); ++i) {
+            FftParams p = base;
+            p.sym = syms[i];
+            p.mag = mags[i];
+            for (int w = 0; w < 3; ++w) CK(vs[i].launch(p, nullptr));
+            for (int k = 0; k < reps; ++k) {
+                CK(hipEventRecord(e0, nullptr));
+                CK(vs[i].launch(p, nullptr));
+                CK(hipEventRecord(e1, nullptr));
+                CK(hipEventSynchronize(e1));
+                float ms = 0;
+                CK(hipEventElapsedTime(&ms, e0, e1));
+                vs[i].ms.push_back(ms);
+            }
+        }
+    }
+    const double fpw = 2.5 * 1024 * 10 + 3 * 513;
+    for (auto &v : vs) {
+        if (v.ms.empty()) continue;
+        std::vector<float> m = v.ms;
+        std::sort(m.begin(), m.end());
+        const double med = m[m.size() / 2];
+        std::printf("%-24s hop %d W %lld: min %.4f ms median %.4f ms  %.1f TF/s (%.1f %% of 157.3)\n",
+                    v.name.c_str(), hop, W, m[0], med, fpw * W / (med * 1e-3) / 1e12,
+                    100.0 * fpw * W / (med * 1e-3) / 1e12 / 157.3);
+    }
+    return 0;
+}
