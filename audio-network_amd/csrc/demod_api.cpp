@@ -30,6 +30,7 @@ struct demod {
     float *d_tw512 = nullptr;   // FFT detector tables
     float *d_tw1024 = nullptr;
     int *d_bins = nullptr;
+    int fft_slot[kMaxTones] = {};  // FFT detector: where each tone bin's power sits (fft_quad_slot)
     float coef[kMaxTones] = {};
     float sgn[kMaxTones] = {};  // plain detector, Reinsch form: sign of cos(w_k)
     bool reinsch = false;       // plain detector: Reinsch-modified recurrence
@@ -210,6 +211,7 @@ static int init_device_state(demod_t *st)
         for (uint32_t k = 0; k < c.k; ++k) {
             long b = std::lround(c.freqs[k] * c.n / c.fs);
             bins[k] = (int)std::min<long>(std::max<long>(b, 0), c.n / 2);
+            st->fft_slot[k] = fft_quad_slot(bins[k]);
         }
         HIP_TRY(hipMalloc(&st->d_tw512, t1.size() * sizeof(float)));
         HIP_TRY(hipMalloc(&st->d_tw1024, t2.size() * sizeof(float)));
@@ -433,6 +435,7 @@ static int enqueue_fft(demod_t *st, const int16_t *d_pcm, size_t n_windows, uint
     p.tw512 = st->d_tw512;
     p.tw1024 = st->d_tw1024;
     p.bins = st->d_bins;
+    for (uint32_t k = 0; k < st->cfg.k; ++k) p.slot[k] = st->fft_slot[k];
     p.sym = d_sym;
     p.mag = d_mag;
     p.spec = d_spec;

@@ -1,25 +1,26 @@
 // fft_quad.hip — the full-spectrum detector laid
-// out as 16 lanes per window, 4 windows per wave. Same contract as
-// fft1024_kernel (fft.hip): per window a 1024-point real FFT, |X[b]|^2 for
-// b = 0..512, symbol = argmax over the tone bins (ties -> lowest k). Oracle:
-// oracle/fsk_oracle.c:oracle_fft_demod.
+// out as 16 lanes per window, 4 windows per wave: per window a 1024-point real
+// FFT, |X[b]|^2 for b = 0..512, symbol = argmax over the tone bins (ties ->
+// lowest k). Oracle: oracle/fsk_oracle.c:oracle_fft_demod.
 //
 // z[n] = x[2n] + i x[2n+1] (n < 512) is a 512-point complex FFT, split 32 x 16:
 //   n = t + 16 n1 (t = lane % 16, n1 < 32),   k = k1 + 32 k2 (k1 < 32, k2 < 16)
 //   Z[k1 + 32 k2] = sum_t W16^{t k2} W512^{t k1} sum_n1 z[t + 16 n1] W32^{n1 k1}
 //   1. lane t loads its 32 dwords z[t + 16 n1] (16 lanes = 64 contiguous bytes
-//      per instruction) and runs a DFT-32 in registers, then multiplies by
-//      W512^{t k1} (block LDS table, broadcast across the 4 windows);
+//      per instruction) and runs a DFT-32 in registers;
 //   2. ONE transpose through LDS: row t -> columns. Lane t' takes the column
-//      pair {k1, 32 - k1} (lane 0: {0, 16}) and runs two DFT-16 in registers;
+//      pair {k1, 32 - k1} (lane 0: {0, 16}) and runs, per column, the DFT-16
+//      of the W512^{t k1}-twiddled column in registers;
 //   3. the real-FFT post-pass pairs Z[k] with conj Z[512 - k]. With the column
 //      pairing above that mirror lives in the same lane, so it needs no
 //      exchange: per pair one twiddle product gives both |X[k]|^2 and
 //      |X[512 - k]|^2.
-// LDS traffic per window: 4 KiB written + 4 KiB read for the transpose, plus
-// 2 KiB of bin powers for the tone pick — against 12 + 12 KiB for the
-// 64-lane radix-8 Stockham layout (fft.hip), whose LDS writes bound it (guide:
-// ds_write aggregates 38-51 TB/s).
+// LDS traffic per window: 4 KiB written + 4 KiB read for the transpose (plus
+// 2 KiB of bin powers when the full spectrum is stored) — against 12 + 12 KiB
+// for a 64-lane radix-8 Stockham layout (scripts/fft_r0.hip), whose LDS writes
+// bound it (guide: ds_write aggregates 38-51 TB/s). Every twiddle product is
+// fused into the butterfly that consumes it (fft1024_quad_kernel below); the
+// round-1 kernel with separate products is scripts/fft_quad_r1b.hip.
 #include <algorithm>
 #include <type_traits>
 
@@ -139,38 +140,6 @@ __device__ __forceinline__ f2 pp_im(f2 S, f2 T)
     return r;
 }
 
-// The real post-pass of two mirror pairs in one block (step 3 of the kernel):
-// S = P + conj Q, D = -i (P - conj Q), T = W D, then
-// pw = (|S + T|^2, |S - T|^2 with the imaginary part of S - T conjugated), i.e.
-// (|X[kP]|^2, |X[512 - kP]|^2). Sixteen packed ops, ordered so that no result
-// feeds the next instruction: one asm block, because the compiler pads every
-// asm boundary whose last write is read next with an s_nop (gfx950 packed-fp32
-// write -> dependent read hazard), and a chain of small blocks is all
-// boundaries.
-__device__ __forceinline__ void post_pair2(f2 &pw0, f2 P0, f2 Q0, f2 W0, f2 &pw1, f2 P1, f2 Q1,
-                                           f2 W1)
-{
-    f2 S0, S1, D0, D1, T0, T1, R0, R1, I0, I1;
-    asm("v_pk_add_f32 %2, %12, %13 neg_hi:[0,1]\n\t"                              // S0
-        "v_pk_add_f32 %3, %15, %16 neg_hi:[0,1]\n\t"                              // S1
-        "v_pk_add_f32 %4, %12, %13 op_sel:[1,1] op_sel_hi:[0,0] neg_hi:[1,0]\n\t" // D0
-        "v_pk_add_f32 %5, %15, %16 op_sel:[1,1] op_sel_hi:[0,0] neg_hi:[1,0]\n\t" // D1
-        "v_pk_mul_f32 %6, %4, %14 op_sel:[1,1] op_sel_hi:[1,0]\n\t"               // t0
-        "v_pk_mul_f32 %7, %5, %17 op_sel:[1,1] op_sel_hi:[1,0]\n\t"               // t1
-        "v_pk_fma_f32 %6, %4, %14, %6 op_sel_hi:[0,1,1] neg_lo:[0,0,1]\n\t"       // T0 = W0 D0
-        "v_pk_fma_f32 %7, %5, %17, %7 op_sel_hi:[0,1,1] neg_lo:[0,0,1]\n\t"       // T1
-        "v_pk_add_f32 %8, %2, %6 op_sel_hi:[0,0] neg_hi:[0,1]\n\t"                // re pair 0
-        "v_pk_add_f32 %9, %3, %7 op_sel_hi:[0,0] neg_hi:[0,1]\n\t"                // re pair 1
-        "v_pk_add_f32 %10, %2, %6 op_sel:[1,1] neg_hi:[0,1]\n\t"                  // im pair 0
-        "v_pk_add_f32 %11, %3, %7 op_sel:[1,1] neg_hi:[0,1]\n\t"                  // im pair 1
-        "v_pk_mul_f32 %4, %10, %10\n\t"                                            // im0^2
-        "v_pk_mul_f32 %5, %11, %11\n\t"                                            // im1^2
-        "v_pk_fma_f32 %0, %8, %8, %4\n\t"                                          // pw0
-        "v_pk_fma_f32 %1, %9, %9, %5"                                                // pw1
-        : "=&v"(pw0), "=&v"(pw1), "=&v"(S0), "=&v"(S1), "=&v"(D0), "=&v"(D1), "=&v"(T0),
-          "=&v"(T1), "=&v"(R0), "=&v"(R1), "=&v"(I0), "=&v"(I1)
-        : "v"(P0), "v"(Q0), "v"(W0), "v"(P1), "v"(Q1), "v"(W1));
-}
 
 // lane % 16 == 0 ? a : b (lanes 0, 16, 32, 48 of the wave)
 __device__ __forceinline__ f2 sel_l0(f2 a, f2 b)
@@ -307,7 +276,7 @@ __device__ __forceinline__ void dft(f2 *x)
     }
 }
 
-// ---- fused twiddle butterflies (fft1024_quad2_kernel) ---------------------
+// ---- fused twiddle butterflies (fft1024_quad_kernel) ----------------------
 // A twiddled radix-2 butterfly (u, v) = (x + w y, x - w y) in three packed
 // FMAs instead of a complex product (2) and two complex adds (2):
 //   t = fma(y, w.xx, x)                    = (x.x + w.x y.x, x.y + w.x y.y)
@@ -501,17 +470,7 @@ constexpr int kQWin = 16 * kQRow;    // complex per window
 constexpr int kQSlab = 4 * kQWin;    // complex per wave
 static_assert(4 * kQPow <= 2 * kQSlab, "bin powers of 4 windows must fit the slab");
 
-// MINW > 0 asks the compiler for MINW waves per SIMD (VGPR budget 512 / MINW).
-// SPLIT: the next group's 32 loads go out in two halves — the 16 dwords the
-// first two DFT-8 columns of stage 1 need (n1 % 4 < 2) during the transpose,
-// the rest after the post-pass — so only 16 prefetch VGPRs are live across
-// the DFT-16 and post-pass.
-// FUSE: step 3 as one asm block per two pairs (post_pair2) instead of the
-// cmul2 / pwr2 pieces: 23 -> 8 hazard nops but 142 -> 160 VGPRs, and the same
-// time (interleaved A/B, profiles/round1/probe_fft_fuse.log), so off.
-// FMT: load z[t + 16 n1] with a typed buffer load (DATA_FORMAT 16_16,
-// NUM_FORMAT SSCALED): the texture path converts both int16 halves to fp32,
-// replacing the 64 VALU converts per group (exact for every int16).
+// Typed (format) buffer loads, for the FMT variant below.
 namespace quad {
 typedef int i4 __attribute__((ext_vector_type(4)));
 __device__ f2 raw_buffer_load_format_v2f32(i4 rsrc, int voffset, int soffset, int aux)
@@ -521,198 +480,7 @@ __device__ f2 raw_buffer_load_format_v2f32(i4 rsrc, int voffset, int soffset, in
 constexpr int kFmtWord3 = 0xFAC | (3 << 12) | (5 << 15);
 }  // namespace quad
 
-template <int WPB = 4, int MINW = 0, bool SPLIT = false, bool FUSE = false, bool FMT = false>
-__global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MINW > 0 ? MINW : 1)))
-void fft1024_quad_kernel(FftParams p)
-{
-    using namespace quad;
-    __shared__ __attribute__((aligned(16))) f2 slab[WPB][kQSlab];
-    __shared__ f2 tw1[31 * 16];  // W512^{t k1} / 2 at [k1 - 1][t]
-    __shared__ f2 tw3[16 * 16];  // post-pass W1024^{kP(t, j)} at [j][t]
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: tile bases stay in SGPRs (no waterfall loop per buffer load)
-    const int q = lane >> 4;   // window of the wave
-    const int t = lane & 15;   // row / column-pair index
-    const f2 *t512 = reinterpret_cast<const f2 *>(p.tw512);
-    const f2 *t1024 = reinterpret_cast<const f2 *>(p.tw1024);
-    // The real split X = (S + W D)/2 needs Z/2: the 1/2 rides on the stage-1
-    // twiddles (and column 0), exact in binary floating point.
-    for (int i = threadIdx.x; i < 31 * 16; i += 64 * WPB)
-        tw1[i] = 0.5f * t512[((i & 15) * ((i >> 4) + 1)) & 511];
-    // post-pass twiddles W1024^kP for bin kP(t, j) (step 3): t + 32 j, and
-    // for t = 0, j >= 8: 16 + 32 (j - 8)
-    for (int i = threadIdx.x; i < 16 * 16; i += 64 * WPB) {
-        const int tt = i & 15, j = i >> 4;
-        tw3[i] = t1024[(tt == 0 && j >= 8) ? 16 + 32 * (j - 8) : tt + 32 * j];
-    }
-    const int k1b = t == 0 ? 16 : 32 - t;
-    const int myslot = quad_slot(t < p.k ? p.bins[t] : 0);
-    float *pw = reinterpret_cast<float *>(slab[wave]);
-    __syncthreads();
-
-    const long long n_groups = (p.n_windows + 3) >> 2;
-    const long long stride = (long long)gridDim.x * WPB;
-    long long g = tile_block(p.xcd_swizzle) * WPB + wave;
-    uint32_t nx[FMT ? 1 : 32];
-    f2 nxf[FMT ? 32 : 1];
-    // One buffer descriptor per group (wave-uniform base = its first window);
-    // the lane offset is the window's start + 4 t bytes, and z[t + 16 n1] is
-    // the immediate offset 64 n1 (< 4 KiB), so the 32 loads need no address
-    // arithmetic. Windows past the end are clamped to the last (never stored).
-    auto load_group = [&](long long gg, int half) {  // half: 0 / 1 of SPLIT, 2 = all
-        const long long w0 = 4 * gg;
-        const long long left = p.n_windows - w0;  // >= 1
-        const int wq = q < left ? q : (int)left - 1;
-        long long bytes = ((left - 1) * p.hop + 1024) * 2;
-        if (bytes > 0x7FFFFFF0LL) bytes = 0x7FFFFFF0LL;
-        __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            (void *)(p.pcm + w0 * p.hop), (short)0, (int)bytes, 0x00020000);
-        const int voff = (int)(wq * p.hop * 2) + 4 * t;
-        if constexpr (FMT) {
-            const unsigned long long base = (unsigned long long)(p.pcm + w0 * p.hop);
-            const i4 rf = {(int)(unsigned)base, (int)((base >> 32) & 0xFFFF), (int)bytes, kFmtWord3};
-#pragma unroll
-            for (int n1 = 0; n1 < 32; ++n1)
-                if (half == 2 || ((n1 & 3) < 2) == (half == 0))
-                    nxf[n1] = raw_buffer_load_format_v2f32(rf, voff + 64 * n1, 0, 2);
-        } else {
-#pragma unroll
-            for (int n1 = 0; n1 < 32; ++n1)
-                if (half == 2 || ((n1 & 3) < 2) == (half == 0))
-                    nx[n1] = __builtin_amdgcn_raw_buffer_load_b32(rs, voff + 64 * n1, 0, 2);
-        }
-    };
-    if (g < n_groups) load_group(g, 2);
-    for (; g < n_groups; g += stride) {
-        const long long w = 4 * g + q;
-        f2 a[32];
-#pragma unroll
-        for (int n1 = 0; n1 < 32; ++n1) {
-            if constexpr (FMT) {
-                a[n1] = nxf[n1];
-                continue;
-            }
-            a[n1] = (f2){(float)(int)(short)(nx[FMT ? 0 : n1] & 0xFFFFu), (float)((int)nx[FMT ? 0 : n1] >> 16)};
-            // opaque: otherwise the compiler rewrites (float)a + (float)b as
-            // (float)(a + b) and the first butterflies become 2 integer ops +
-            // 2 converts each instead of one packed add
-            asm("" : "+v"(a[n1]));
-        }
-
-        // 1. DFT-32 over n1, twiddle W512^{t k1} (and the 1/2 of the real split)
-        dft<32>(a);
-        a[0] *= 0.5f;
-#pragma unroll
-        for (int k1 = 1; k1 < 31; k1 += 2)
-            cmul2(a[k1], a[k1], tw1[16 * (k1 - 1) + t], a[k1 + 1], a[k1 + 1], tw1[16 * k1 + t]);
-        a[31] = cmul(a[31], tw1[16 * 30 + t]);
-
-        // 2. transpose in two column rounds; lane (q, t') gets columns
-        //    k1 = t' (round 0) and k1b (round 1) of its window
-        f2 b[32];  // b[n2] = Y[n2][t'], b[16 + n2] = Y[n2][k1b]
-        f2 *win = slab[wave] + q * kQWin;
-#pragma unroll
-        for (int r = 0; r < 2; ++r) {
-#pragma unroll
-            for (int c = 0; c < 16; ++c) win[t * kQRow + c] = a[16 * r + c];
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            if (r == 0) {
-                // prefetch the next group here, where half of the DFT-32 output
-                // is already in LDS (unconditional, clamped: one basic block)
-                load_group(g + stride < n_groups ? g + stride : g, SPLIT ? 0 : 2);
-            }
-            const int col = r == 0 ? t : k1b - 16;
-#pragma unroll
-            for (int n2 = 0; n2 < 16; ++n2) b[16 * r + n2] = win[n2 * kQRow + col];
-            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-        }
-        dft<16>(b);
-        dft<16>(b + 16);
-        // b[k2] = Z[t + 32 k2], b[16 + k2] = Z[k1b + 32 k2]
-
-        // 3. real post-pass over 16 mirror pairs (P_j, Q_j = Z[512 - kP]):
-        //    t > 0:  P = Za[j], Q = Zb[15 - j], kP = t + 32 j
-        //    t = 0:  j < 8: P = Za[j], Q = Za[(16 - j) % 16], kP = 32 j
-        //            j >= 8: P = Zb[j - 8], Q = Zb[23 - j], kP = 16 + 32 (j - 8)
-        //    X[kP] = (S + W D)/2, X[512 - kP] = conj(S - W D)/2 with
-        //    S = P + conj Q, D = -i (P - conj Q), W = W1024^kP (b holds Z/2,
-        //    so S + W D is X itself).
-        const bool l0 = (t == 0);
-        float *pq = pw + q * kQPow;
-        f2 *const ps = reinterpret_cast<f2 *>(pq) + t;  // slot (j, t) at ps[16 j]
-        // two pairs at a time (j, j + 1), so no packed result feeds the very
-        // next instruction (cmul2 / pwr2)
-        static_for<0, 8>([&](auto jc) {
-            constexpr int j0 = 2 * decltype(jc)::value, j1 = j0 + 1;
-            // lane 0's pairing, selected per lane with v_cndmask on a constant
-            // lane mask (a C++ select of two b[] elements becomes a runtime
-            // index into b, which sends b to scratch)
-            f2 P0 = b[j0], Q0 = b[16 + 15 - j0];
-            f2 P1 = b[j1], Q1 = b[16 + 15 - j1];
-            if constexpr (j0 >= 8) {
-                P0 = sel_l0(b[16 + j0 - 8], P0);
-                P1 = sel_l0(b[16 + j1 - 8], P1);
-            }
-            if constexpr (j0 < 8) {
-                Q0 = sel_l0(b[(16 - j0) & 15], Q0);
-                Q1 = sel_l0(b[(16 - j1) & 15], Q1);
-            } else {
-                Q0 = sel_l0(b[16 + 23 - j0], Q0);
-                Q1 = sel_l0(b[16 + 23 - j1], Q1);
-            }
-            f2 pw0, pw1;  // (|X[kP]|^2, |X[512-kP]|^2)
-            if constexpr (FUSE) {
-                post_pair2(pw0, P0, Q0, tw3[16 * j0 + t], pw1, P1, Q1, tw3[16 * j1 + t]);
-            } else {
-                const f2 S0 = pp_s(P0, Q0), S1 = pp_s(P1, Q1);
-                const f2 D0 = pp_d(P0, Q0), D1 = pp_d(P1, Q1);
-                f2 T0, T1;
-                cmul2(T0, D0, tw3[16 * j0 + t], T1, D1, tw3[16 * j1 + t]);
-                const f2 re0 = pp_re(S0, T0), re1 = pp_re(S1, T1);
-                const f2 im0 = pp_im(S0, T0), im1 = pp_im(S1, T1);
-                pwr2(pw0, re0, im0, pw1, re1, im1);
-            }
-            ps[16 * j0] = pw0;
-            ps[16 * j1] = pw1;
-        });
-        // Z[256] is its own mirror: |X[256]|^2 = |Z[256]|^2 = 4 |b[8]|^2
-        if (l0) pq[512] = 4.f * fmaf(b[8].x, b[8].x, b[8].y * b[8].y);
-        if (SPLIT) load_group(g + stride < n_groups ? g + stride : g, 1);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-
-        // 4. tone pick: lane (q, i < K) reads bin power i, argmax over the
-        //    16-lane row (ties -> lowest i), lane (q, 0) stores the symbol.
-        const bool live = w < p.n_windows;
-        float pk = -1.f;
-        int arg = t;
-        if (t < p.k) pk = pq[myslot];
-        if (live && t < p.k && p.mag) p.mag[w * p.k + t] = pk;
-        // row_ror:1,2,4,8 within the 16-lane row: every lane sees the whole row
-        static_for<0, 4>([&](auto sc) {
-            constexpr int ctrl = 0x120 + (1 << decltype(sc)::value);
-            const float po = __int_as_float(
-                __builtin_amdgcn_update_dpp(0, __float_as_int(pk), ctrl, 0xF, 0xF, false));
-            const int ao = __builtin_amdgcn_update_dpp(0, arg, ctrl, 0xF, 0xF, false);
-            const bool take = (po > pk) | ((po == pk) & (ao < arg));  // branch-free
-            pk = take ? po : pk;
-            arg = take ? ao : arg;
-        });
-        if (live && t == 0) p.sym[w] = (uint8_t)arg;
-        if (p.spec && live) {
-            float *so = p.spec + w * 513;
-            for (int i = t; i < 513; i += 16) so[i] = pq[quad_slot(i)];
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-    }
-}
-
-// fft1024_quad2_kernel: the quad layout with every twiddle fused into the
+// fft1024_quad_kernel (round 2): the quad layout with every twiddle fused into the
 // butterfly that consumes it (dftf, dft4_geo_*), the stage-1 twiddle moved
 // behind the transpose and the 1/2 of the real split folded into the
 // post-pass FMAs:
@@ -729,42 +497,21 @@ void fft1024_quad_kernel(FftParams p)
 // 514 instead of 575 packed instructions per group of 4 windows.
 // PF: 1 = the next group's 32 loads go out during the transpose (32 VGPRs live
 // across stage 2 and the post-pass), 0 = each group loads at the top of its
-// iteration (co-resident waves cover the latency).
+// iteration and the co-resident waves cover the latency (4 waves/SIMD at
+// MINW = 4 without spills: 104-116 VGPRs).
 // SPEC: false = symbols (+ tone powers) only: the tone powers are picked
-// from the registers of the lanes that hold them (p.slot, uniform) instead
-// of going through the 2 KiB per-window power slab in LDS; true = the slab,
-// for the full-spectrum store.
-// RS: row stride in windows. 1 = a wave's 4 windows are consecutive (at hop
-// 256 they overlap by 3/4, so each load instruction re-requests lines its
-// other rows requested a few instructions earlier, still in flight); 4 = the
-// 4 waves of a block interleave over 16 consecutive windows (wave v takes
-// v, v + 4, v + 8, v + 12): no overlap inside a wave, and the neighbours'
-// shared lines are requested by the block's other waves instead.
-// ABL (timing ablations for scripts/fft_probe only, results WRONG when set):
-// bit 0 = load the first group only (no global loads in the loop), bit 1 = no
-// LDS transpose (stage 2 reads stage 1's registers).
-// CM: column-major transpose slab ([col][row], 144 B per column: 16 rows +
-// 16 B pad, 2304 B per window): the rows still go out as ds_write2_b64 pairs,
-// but a lane's column comes back as 8 ds_read_b128 (two rows each, half the
-// LDS cycles of ds_read2_b64); the 36-dword column stride puts the 16 lanes of
-// a window on 64 distinct banks and the windows 576 dwords apart, so every
-// b128 lane group is conflict-free.
-constexpr int kCmCol = 18;                 // f2 per column (16 rows + pad)
-constexpr int kCmWin = 16 * kCmCol;        // f2 per window
-constexpr int kCmSlab = 4 * kCmWin;        // f2 per wave (>= 4 x 544 floats of powers / 2)
-// TWP: read all of a group's stage-2 and post-pass twiddles (20 + 16 complex)
-// right behind the transpose reads, as one batch under the same wait, instead
-// of just in time (the compiler sinks each ds_read to its use, which exposes
-// the LDS latency a dozen times per group).
+// from the registers of the lanes that hold them (p.slot, a wave-uniform
+// index: s_set_gpr_idx) instead of going through the 2 KiB per-window power
+// slab in LDS; true = the slab, for the full-spectrum store.
 // FMT (PF = 0 only): typed buffer loads (16_16 SSCALED) convert both int16
-// halves to fp32 in the texture path instead of 64 VALU converts per group.
-template <int WPB = 4, int MINW = 0, int PF = 1, bool SPEC = true, int RS = 1, int ABL = 0,
-          bool CM = false, bool TWP = false, bool FMT = false>
+// halves to fp32 in the texture path instead of 64 VALU converts per group
+// (measured neutral).
+template <int WPB = 4, int MINW = 4, int PF = 0, bool SPEC = true, bool FMT = false>
 __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MINW > 0 ? MINW : 1)))
-void fft1024_quad2_kernel(FftParams p)
+void fft1024_quad_kernel(FftParams p)
 {
     using namespace quad;
-    __shared__ __attribute__((aligned(16))) f2 slab[WPB][CM ? kCmSlab : kQSlab];
+    __shared__ __attribute__((aligned(16))) f2 slab[WPB][kQSlab];
     __shared__ f2 tw2[2 * 10 * 16];  // [column slot][v, v2, g0, g0^2, .., g3, g3^2][t]
     __shared__ f2 tw3[16 * 16];      // post-pass W1024^{kP(t, j)} / 2 at [j][t]
     const int lane = threadIdx.x & 63;
@@ -800,15 +547,14 @@ void fft1024_quad2_kernel(FftParams p)
     static_assert(!FMT || PF == 0, "FMT loads straight into a[]");
     uint32_t nx[FMT ? 1 : 32];
     f2 nxf[FMT ? 32 : 1];
-    // first window of group gg and the window of row q (RS above)
-    auto gbase = [&](long long gg) -> long long {
-        return RS == 1 ? 4 * gg : 16 * (gg >> 2) + (gg & 3);
-    };
+    // One buffer descriptor per group (wave-uniform base = its first window);
+    // the lane offset is the window's start + 4 t bytes, and z[t + 16 n1] is
+    // the immediate offset 64 n1 (< 4 KiB). Windows past the end are clamped
+    // to the last (never stored).
     auto load_group = [&](long long gg) {
-        const long long w0 = gbase(gg);
+        const long long w0 = 4 * gg;
         const long long left = p.n_windows - w0;  // >= 1
-        const long long wq0 = RS * q;
-        const long long wq = wq0 < left ? wq0 : left - 1;
+        const long long wq = q < left ? q : left - 1;
         long long bytes = ((left - 1) * p.hop + 1024) * 2;
         if (bytes > 0x7FFFFFF0LL) bytes = 0x7FFFFFF0LL;
         __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
@@ -826,13 +572,10 @@ void fft1024_quad2_kernel(FftParams p)
                 nx[n1] = __builtin_amdgcn_raw_buffer_load_b32(rs, voff + 64 * n1, 0, 2);
         }
     };
-    static_assert(RS == 1 || (RS == 4 && PF == 0 && WPB % 4 == 0), "RS = 4: no cross-group prefetch");
-    const long long n_groups_rs = RS == 1 ? n_groups : 4 * ((p.n_windows + 15) >> 4);
-    if ((PF || (ABL & 1)) && g < n_groups_rs) load_group(g);
-    for (; g < n_groups_rs; g += stride) {
-        const long long w = gbase(g) + RS * q;
-        if (RS != 1 && gbase(g) >= p.n_windows) continue;  // wave-uniform: a group past the end
-        if (!PF && !(ABL & 1)) load_group(g);
+    if (PF && g < n_groups) load_group(g);
+    for (; g < n_groups; g += stride) {
+        const long long w = 4 * g + q;
+        if (!PF) load_group(g);
         f2 a[32];
 #pragma unroll
         for (int n1 = 0; n1 < 32; ++n1) {
@@ -851,40 +594,15 @@ void fft1024_quad2_kernel(FftParams p)
         // 2. transpose in two column rounds; lane (q, t') gets columns
         //    k1 = t' (round 0) and k1b (round 1) of its window
         f2 b[32];  // b[n2] = A_n2[t'], b[16 + n2] = A_n2[k1b]
-        f2 *win = slab[wave] + q * (CM ? kCmWin : kQWin);
+        f2 *win = slab[wave] + q * kQWin;
 #pragma unroll
         for (int r = 0; r < 2; ++r) {
-            if constexpr ((ABL & 2) != 0) {
-#pragma unroll
-                for (int n2 = 0; n2 < 16; ++n2) b[16 * r + n2] = a[16 * r + n2];
-                continue;
-            }
-            if constexpr (CM) {
-#pragma unroll
-                for (int c = 0; c < 16; ++c) win[c * kCmCol + t] = a[16 * r + c];
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                if (PF && !(ABL & 1) && r == 0) load_group(g + stride < n_groups_rs ? g + stride : g);
-                const int col = r == 0 ? t : k1b - 16;
-                typedef float f4 __attribute__((ext_vector_type(4)));
-                const f4 *cp = reinterpret_cast<const f4 *>(win + col * kCmCol);
-#pragma unroll
-                for (int i = 0; i < 8; ++i) {
-                    const f4 v = cp[i];
-                    b[16 * r + 2 * i] = (f2){v.x, v.y};
-                    b[16 * r + 2 * i + 1] = (f2){v.z, v.w};
-                }
-                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                continue;
-            }
 #pragma unroll
             for (int c = 0; c < 16; ++c) win[t * kQRow + c] = a[16 * r + c];
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            if (PF && !(ABL & 1) && r == 0) load_group(g + stride < n_groups_rs ? g + stride : g);
+            if (PF && r == 0) load_group(g + stride < n_groups ? g + stride : g);
             const int col = r == 0 ? t : k1b - 16;
 #pragma unroll
             for (int n2 = 0; n2 < 16; ++n2) b[16 * r + n2] = win[n2 * kQRow + col];
@@ -892,18 +610,7 @@ void fft1024_quad2_kernel(FftParams p)
             __builtin_amdgcn_wave_barrier();
         }
         // 3. per column: DFT-16 over t of A_t[col] W512^{t col}, twiddles fused
-        f2 twr[TWP ? 36 : 1];  // TWP: [col slot][10] stage-2 twiddles, then the 16 tw3
-        if constexpr (TWP) {
-#pragma unroll
-            for (int m = 0; m < 20; ++m) twr[m] = tw2[(m / 10) * 160 + (m % 10) * 16 + t];
-#pragma unroll
-            for (int j = 0; j < 16; ++j) twr[20 + j] = tw3[16 * j + t];
-#pragma unroll
-            for (int m = 0; m < 36; ++m) asm volatile("" : "+v"(twr[m]));
-        }
-        auto twv = [&](int sl, int m) -> f2 {
-            return TWP ? twr[sl * 10 + m] : tw2[sl * 160 + m * 16 + t];
-        };
+        auto twv = [&](int sl, int m) -> f2 { return tw2[sl * 160 + m * 16 + t]; };
 #pragma unroll
         for (int sl = 0; sl < 2; ++sl) {
             f2 *bb = b + 16 * sl;
@@ -956,8 +663,7 @@ void fft1024_quad2_kernel(FftParams p)
             const f2 S0 = pp_s(P0, Q0), S1 = pp_s(P1, Q1);
             const f2 D0 = pp_d(P0, Q0), D1 = pp_d(P1, Q1);
             f2 T0, T1;
-            cmul2(T0, D0, TWP ? twr[20 + j0] : tw3[16 * j0 + t], T1, D1,
-                  TWP ? twr[20 + j1] : tw3[16 * j1 + t]);
+            cmul2(T0, D0, tw3[16 * j0 + t], T1, D1, tw3[16 * j1 + t]);
             const f2 re0 = pp_re_h(S0, T0), re1 = pp_re_h(S1, T1);
             const f2 im0 = pp_im_h(S0, T0), im1 = pp_im_h(S1, T1);
             pwr2(pw0, re0, im0, pw1, re1, im1);
@@ -1024,35 +730,15 @@ void fft1024_quad2_kernel(FftParams p)
     }
 }
 
-template <int WPB, int MINW, int PF = 1, bool SPEC = true, int RS = 1, int ABL = 0, bool CM = false,
-          bool TWP = false, bool FMT = false>
-hipError_t launch_fft_quad2_t(const FftParams &p, hipStream_t s)
-{
-    int dev = 0, cus = 256, per_cu = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fft1024_quad2_kernel<WPB, MINW, PF, SPEC, RS, ABL, CM, TWP, FMT>,
-                                                     64 * WPB, 0) != hipSuccess ||
-        per_cu < 1)
-        per_cu = 1;
-    const long long groups = (p.n_windows + 3) / 4;
-    long long blocks = (groups + WPB - 1) / WPB;
-    blocks = std::min<long long>(blocks, (long long)cus * per_cu);
-    if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL((fft1024_quad2_kernel<WPB, MINW, PF, SPEC, RS, ABL, CM, TWP, FMT>), dim3((unsigned)blocks), dim3(64 * WPB),
-                       0, s, p);
-    return hipGetLastError();
-}
-
 // Persistent grid: as many blocks as fit the chip, each wave strides over
 // groups of 4 windows (the LDS twiddle tables are built once per block).
-template <int WPB, int MINW, bool SPLIT = false, bool FUSE = false, bool FMT = false>
+template <int WPB, int MINW, int PF, bool SPEC, bool FMT = false>
 hipError_t launch_fft_quad_t(const FftParams &p, hipStream_t s)
 {
     int dev = 0, cus = 256, per_cu = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fft1024_quad_kernel<WPB, MINW, SPLIT, FUSE, FMT>,
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fft1024_quad_kernel<WPB, MINW, PF, SPEC, FMT>,
                                                      64 * WPB, 0) != hipSuccess ||
         per_cu < 1)
         per_cu = 1;
@@ -1060,20 +746,17 @@ hipError_t launch_fft_quad_t(const FftParams &p, hipStream_t s)
     long long blocks = (groups + WPB - 1) / WPB;
     blocks = std::min<long long>(blocks, (long long)cus * per_cu);
     if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL((fft1024_quad_kernel<WPB, MINW, SPLIT, FUSE, FMT>), dim3((unsigned)blocks), dim3(64 * WPB), 0,
-                       s, p);
+    hipLaunchKernelGGL((fft1024_quad_kernel<WPB, MINW, PF, SPEC, FMT>), dim3((unsigned)blocks), dim3(64 * WPB),
+                       0, s, p);
     return hipGetLastError();
 }
 
+// Shipped: 4-wave blocks, 4 waves/SIMD, loads at the top of each group, the
+// register tone pick unless the full spectrum is asked for
+// (scripts/fft_probe.hip, profiles/round2/fft/).
 hipError_t launch_fft_quad(const FftParams &p, hipStream_t s)
 {
-    return launch_fft_quad_t<4, 0>(p, s);
-}
-
-// probe / A-B entry of the fused-twiddle kernel
-hipError_t launch_fft_quad2(const FftParams &p, hipStream_t s)
-{
-    return launch_fft_quad2_t<4, 0>(p, s);
+    return p.spec ? launch_fft_quad_t<4, 4, 0, true>(p, s) : launch_fft_quad_t<4, 4, 0, false>(p, s);
 }
 
 int fft_quad_slot(int bin) { return quad_slot(bin); }

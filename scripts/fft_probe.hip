@@ -10,6 +10,7 @@
 // sample (max |dP| relative to the window's peak bin, the 1e-5 bar).
 #include "../audio-network_amd/csrc/fft_quad.hip"
 #include "../audio-network_amd/csrc/synth.hip"
+#include "fft_quad_r1b.hip"
 
 #include <algorithm>
 #include <cmath>
@@ -84,12 +85,11 @@ int main(int argc, char **argv)
     CK(hipMemcpy(d_bins, bins, 8, hipMemcpyHostToDevice));
 
     std::vector<Var> vs;
-    vs.push_back({"quad (shipped r1)", [](const FftParams &p, hipStream_t s) { return launch_fft_quad(p, s); }, {}});
-    vs.push_back({"quad2 fused", [](const FftParams &p, hipStream_t s) { return launch_fft_quad2(p, s); }, {}});
-#define Q2(NAME, WPB, MINW, PF, RS, CM, TWP, FMT) vs.push_back({NAME, [](const FftParams &p, hipStream_t s) { return p.spec ? launch_fft_quad2_t<WPB, MINW, PF, true, RS, 0, CM, TWP, FMT>(p, s) : launch_fft_quad2_t<WPB, MINW, PF, false, RS, 0, CM, TWP, FMT>(p, s); }, {}})
-    Q2("FMT PF0", 4, 0, 0, 1, false, false, true);
-    Q2("FMT PF0 MINW4", 4, 4, 0, 1, false, false, true);
-    vs.push_back({"quad2 PF0 MINW4 REG", [](const FftParams &p, hipStream_t s) { return p.spec ? launch_fft_quad2_t<4, 4, 0, true>(p, s) : launch_fft_quad2_t<4, 4, 0, false>(p, s); }, {}});
+    // variant 0 is the reference every other variant is checked against
+    vs.push_back({"quad r1 (round-1 shipped)", [](const FftParams &p, hipStream_t s) { return r1b::launch_fft_quad_r1_t<4, 0>(p, s); }, {}});
+    vs.push_back({"quad shipped (fused, PF0 MINW4)", [](const FftParams &p, hipStream_t s) { return launch_fft_quad(p, s); }, {}});
+    vs.push_back({"fused PF1 MINW0", [](const FftParams &p, hipStream_t s) { return p.spec ? launch_fft_quad_t<4, 0, 1, true>(p, s) : launch_fft_quad_t<4, 0, 1, false>(p, s); }, {}});
+    vs.push_back({"fused FMT PF0 MINW4", [](const FftParams &p, hipStream_t s) { return p.spec ? launch_fft_quad_t<4, 4, 0, true, true>(p, s) : launch_fft_quad_t<4, 4, 0, false, true>(p, s); }, {}});
     if (filter) {
         std::vector<Var> keep;
         for (size_t i = 0; i < vs.size(); ++i)
