@@ -49,3 +49,50 @@ def test_config5_streams_rccl_gather_world1():
     assert ov["frame_kernel_ms"] is not None and ov["gather_ms"] is not None
     ps = line["parity_sample"]
     assert ps["symbol_mismatches"] == 0 and ps["max_rel_mag_err"] <= 1e-5
+
+
+def _torchrun(nproc, port, extra, timeout=400):
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT", "MASTER_ADDR"):
+        env.pop(k, None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "bench.py"),
+           "--gpus", str(nproc), "--dist-backend", "gloo"] + extra
+    r = subprocess.run(cmd, capture_output=True, timeout=timeout, cwd=ROOT, env=env)
+    out = r.stdout.decode()
+    assert r.returncode == 0, (out[-2000:], r.stderr.decode()[-4000:])
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out[-2000:]       # rank 0 prints the one line
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("nproc", [2, 3])
+def test_multi_rank_path_on_one_gpu(nproc):
+    """bench.py's N > 1 path with the real HIP kernels (the CPU gloo test in
+    test_dist.py swaps the kernel for the oracle): nproc ranks share the one
+    GPU, each demodulates its own seeded shard, the gather runs over gloo
+    (RCCL on the 8-GPU node). The max-over-ranks timing, the whole-job value
+    and every rank's symbols come back through rank 0."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU visible")
+    w = 65536
+    line = _torchrun(nproc, 29531 + nproc, ["--steps", "3", "--warmup", "1", "--windows", str(w)])
+    assert line["n_gpus"] == nproc and line["scaling"] == "weak"
+    assert line["symbol_errors"] == 0
+    samples = nproc * w * 1024                # whole-job samples per step
+    assert abs(line["value"] - samples / (line["ms_per_step"] * 1e-3) / 1e6) <= 1e-2 * line["value"]
+    assert "cpu_baseline" not in line or line["cpu_baseline"] is None
+
+
+def test_streams_two_ranks_on_one_gpu():
+    """configs[4] sharded by stream over 2 ranks on one GPU: per-rank device
+    framing, gather of the ToReceiver frames, round trip of all 1024 streams."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU visible")
+    line = _torchrun(2, 29541, ["--config", "streams", "--steps", "2", "--warmup", "1"])
+    assert line["config"]["windows_per_gpu"] == 512 * 2048
+    assert line["symbol_errors"] == 0
+    fr = line["framing"]
+    assert fr["roundtrip_ok"] and fr["frames_bytes"] == 1024 * fr["frame_bytes_per_stream"]
