@@ -503,10 +503,11 @@ constexpr int kFmtWord3 = 0xFAC | (3 << 12) | (5 << 15);
 // from the registers of the lanes that hold them (p.slot, a wave-uniform
 // index: s_set_gpr_idx) instead of going through the 2 KiB per-window power
 // slab in LDS; true = the slab, for the full-spectrum store.
+// AUX: the loads' cache-policy bits (2 = nt, 1 = sc0; launch_fft_quad).
 // FMT (PF = 0 only): typed buffer loads (16_16 SSCALED) convert both int16
 // halves to fp32 in the texture path instead of 64 VALU converts per group
 // (measured neutral).
-template <int WPB = 4, int MINW = 4, int PF = 0, bool SPEC = true, bool FMT = false>
+template <int WPB = 4, int MINW = 4, int PF = 0, bool SPEC = true, bool FMT = false, int AUX = 2>
 __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MINW > 0 ? MINW : 1)))
 void fft1024_quad_kernel(FftParams p)
 {
@@ -565,11 +566,11 @@ void fft1024_quad_kernel(FftParams p)
             const i4 rf = {(int)(unsigned)base, (int)((base >> 32) & 0xFFFF), (int)bytes, kFmtWord3};
 #pragma unroll
             for (int n1 = 0; n1 < 32; ++n1)
-                nxf[n1] = raw_buffer_load_format_v2f32(rf, voff + 64 * n1, 0, 2);
+                nxf[n1] = raw_buffer_load_format_v2f32(rf, voff + 64 * n1, 0, AUX);
         } else {
 #pragma unroll
             for (int n1 = 0; n1 < 32; ++n1)
-                nx[n1] = __builtin_amdgcn_raw_buffer_load_b32(rs, voff + 64 * n1, 0, 2);
+                nx[n1] = __builtin_amdgcn_raw_buffer_load_b32(rs, voff + 64 * n1, 0, AUX);
         }
     };
     if (PF && g < n_groups) load_group(g);
@@ -732,13 +733,13 @@ void fft1024_quad_kernel(FftParams p)
 
 // Persistent grid: as many blocks as fit the chip, each wave strides over
 // groups of 4 windows (the LDS twiddle tables are built once per block).
-template <int WPB, int MINW, int PF, bool SPEC, bool FMT = false>
+template <int WPB, int MINW, int PF, bool SPEC, bool FMT = false, int AUX = 2>
 hipError_t launch_fft_quad_t(const FftParams &p, hipStream_t s)
 {
     int dev = 0, cus = 256, per_cu = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fft1024_quad_kernel<WPB, MINW, PF, SPEC, FMT>,
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fft1024_quad_kernel<WPB, MINW, PF, SPEC, FMT, AUX>,
                                                      64 * WPB, 0) != hipSuccess ||
         per_cu < 1)
         per_cu = 1;
@@ -746,17 +747,25 @@ hipError_t launch_fft_quad_t(const FftParams &p, hipStream_t s)
     long long blocks = (groups + WPB - 1) / WPB;
     blocks = std::min<long long>(blocks, (long long)cus * per_cu);
     if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL((fft1024_quad_kernel<WPB, MINW, PF, SPEC, FMT>), dim3((unsigned)blocks), dim3(64 * WPB),
+    hipLaunchKernelGGL((fft1024_quad_kernel<WPB, MINW, PF, SPEC, FMT, AUX>), dim3((unsigned)blocks), dim3(64 * WPB),
                        0, s, p);
     return hipGetLastError();
 }
 
 // Shipped: 4-wave blocks, 4 waves/SIMD, loads at the top of each group, the
 // register tone pick unless the full spectrum is asked for
-// (scripts/fft_probe.hip, profiles/round2/fft/).
+// (scripts/fft_probe.hip, profiles/round2/fft/). Load policy: windows that
+// overlap (hop < n) are read by up to n / hop groups, so their loads keep the
+// lines in L2 (sc0, AUX 1: FETCH 1.06x the stream at hop 256, -5 %);
+// disjoint windows stream through with nt (AUX 2; nt at hop 256 re-fetches
+// 1.55x the stream).
 hipError_t launch_fft_quad(const FftParams &p, hipStream_t s)
 {
-    return p.spec ? launch_fft_quad_t<4, 4, 0, true>(p, s) : launch_fft_quad_t<4, 4, 0, false>(p, s);
+    if (p.hop < 1024)
+        return p.spec ? launch_fft_quad_t<4, 4, 0, true, false, 1>(p, s)
+                      : launch_fft_quad_t<4, 4, 0, false, false, 1>(p, s);
+    return p.spec ? launch_fft_quad_t<4, 4, 0, true, false, 2>(p, s)
+                  : launch_fft_quad_t<4, 4, 0, false, false, 2>(p, s);
 }
 
 int fft_quad_slot(int bin) { return quad_slot(bin); }

@@ -59,14 +59,14 @@ def load_pkg():
     return mod, dmod
 
 
-def pmc_traffic(config: str, windows: int):
+def pmc_traffic(config: str, windows: int, hop: int = 1024):
     """HBM bytes per launch from profiles/pmc_<config>.json (rocprofv3 PMC)."""
     path = os.path.join(ROOT, "profiles", f"pmc_{config}.json")
     if not os.path.exists(path):
         return None
     try:
         d = json.load(open(path))
-        if int(d.get("windows", -1)) != windows:
+        if int(d.get("windows", -1)) != windows or int(d.get("hop", 1024)) != hop:
             return None
         return float(d["hbm_bytes_per_launch"])
     except Exception:
@@ -446,7 +446,8 @@ def run_config(A, D, torch, dist, args, config, rank, world, local, use_dist, st
              ("fold_tile_kernel<%d,4>" if demod.method == A.METHOD_FOLDED
               else "residue_tile_kernel<%d,4>" if demod.method == A.METHOD_RESIDUE
               else "goertzel_tile_kernel<%d,4>") % K)
-    pmc_name = "fsk8odd" if (config == "fsk8" and plan == "odd") else config
+    pmc_name = ("fsk8odd" if (config == "fsk8" and plan == "odd") else
+                "fft1024" if (config == "fft" and hop == 1024) else config)
     r = {
         "config": config, "freqs": freqs, "K": K, "n": n, "hop": hop, "W": W, "n_eval": n_eval,
         "total_windows": total_windows, "ms_per_step": ms_per_step, "kernel_ms": kernel_ms,
@@ -460,7 +461,7 @@ def run_config(A, D, torch, dist, args, config, rank, world, local, use_dist, st
             "peak": HBM_PEAK_GBPS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 4),
-            "traffic": pmc_traffic(pmc_name, W),
+            "traffic": pmc_traffic(pmc_name, W, hop),
             "alg_bytes_per_launch": alg_bytes,
             # this box's read-only ceiling for the same access pattern
             # (see above) and the kernel's achieved rate as a fraction of it
@@ -507,6 +508,7 @@ def summary(r) -> dict:
         out["roofline"] = r["roofline_valu"]
         out["roofline_hbm_frac"] = round(
             r["W"] * 2048 / (r["kernel_ms"] / 1e3) / 1e9 / HBM_PEAK_GBPS, 4)
+        out["hbm_traffic"] = r["roofline"]["traffic"]
     else:
         out["roofline"] = r["roofline"]
     return out

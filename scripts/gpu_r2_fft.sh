@@ -10,4 +10,6 @@ timeout -k 10 300 python -u -m pytest tests -m gpu -k "fft or FFT or near_ties o
 timeout -k 10 200 scripts/bin/fft_probe 256 5 10 > $O/fft_probe.log 2>&1 && \
 timeout -k 10 100 scripts/bin/fft_probe 1024 4 10 >> $O/fft_probe.log 2>&1 && \
 timeout -k 10 200 python -u bench.py --config fft --steps 20 --warmup 5 --cpu-seconds 5 > $O/bench_fft.log 2>&1 && \
-cd /tmp && timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_fft -o run -- python3 $R/bench.py --config fft --steps 20 --warmup 5 --no-cpu-baseline > $O/prof_fft.log 2>&1
+cd /tmp && timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_fft -o run -- python3 $R/bench.py --config fft --steps 20 --warmup 5 --no-cpu-baseline > $O/prof_fft.log 2>&1 && \
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fft_FETCH_SIZE -o run -- python3 $R/bench.py --config fft --no-cpu-baseline --warmup 2 --steps 5 > $O/pmc_fft_FETCH_SIZE.log 2>&1 && \
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_fft_WRITE_SIZE -o run -- python3 $R/bench.py --config fft --no-cpu-baseline --warmup 2 --steps 5 > $O/pmc_fft_WRITE_SIZE.log 2>&1

@@ -2,9 +2,12 @@
 """Per-launch HBM traffic of the detector kernels from the PMC passes of
 scripts/gpu_pmc_traffic.sh (merged into gpurun_out/): writes
 profiles/pmc_<cfg>.json (read by bench.py for roofline.traffic) and copies the
-counter CSVs to profiles/round1/.
+counter CSVs to profiles/<round>/.
 
-    python scripts/pmc_traffic_json.py
+    python scripts/pmc_traffic_json.py [round2]
+
+Round 2 (scripts/gpu_profile_r2.sh, scripts/gpu_r2_fft.sh) adds the FFT
+detector at hop 256 (configs[3]) and hop 1024.
 
 bytes = KB * 1024; FETCH_SIZE doubled (gfx950 counts half of 16 B/lane
 streaming reads, MI355X_MICROARCH.md §HBM).
@@ -16,12 +19,15 @@ import shutil
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 W = 1 << 20
-CFGS = {"fsk2": (2, "goertzel_tile_kernel"), "fsk8": (8, "fold_tile_kernel"),
-        "fsk8odd": (8, "residue_tile_kernel")}
+CFGS = {"fsk2": (2, "goertzel_tile_kernel", 1024), "fsk8": (8, "fold_tile_kernel", 1024),
+        "fsk8odd": (8, "residue_tile_kernel", 1024), "fft": (2, "fft1024_quad_kernel", 256),
+        "fft1024": (2, "fft1024_quad_kernel", 1024)}
 
 
-def main():
-    for tag, (k, kname) in CFGS.items():
+def main(rnd="round1"):
+    for tag, (k, kname, hop) in CFGS.items():
+        if not os.path.exists(os.path.join(ROOT, "gpurun_out", f"pmc_{tag}_FETCH_SIZE")):
+            continue
         vals, name = {}, None
         for c in ("FETCH_SIZE", "WRITE_SIZE"):
             src = os.path.join(ROOT, "gpurun_out", f"pmc_{tag}_{c}", "run_counter_collection.csv")
@@ -30,27 +36,30 @@ def main():
             name = rows[0]["Kernel_Name"]
             v = [float(r["Counter_Value"]) for r in rows]
             vals[c] = (sum(v) / len(v), len(v))
-            shutil.copy(src, os.path.join(ROOT, "profiles", "round1", f"pmc_{tag}_{c}.csv"))
+            shutil.copy(src, os.path.join(ROOT, "profiles", rnd, f"pmc_{tag}_{c}.csv"))
         rd = vals["FETCH_SIZE"][0] * 1024 * 2
         wr = vals["WRITE_SIZE"][0] * 1024
-        alg = W * 2048 + W * (1 + 4 * k)
+        n_eval = (W * 1024 - 1024) // hop + 1
+        alg = W * 2048 + n_eval * (1 + 4 * k)
         out = {
-            "config": tag, "windows": W, "kernel": name, "launches_sampled": vals["FETCH_SIZE"][1],
+            "config": tag, "windows": W, "hop": hop, "windows_evaluated": n_eval, "kernel": name,
+            "launches_sampled": vals["FETCH_SIZE"][1],
             "FETCH_SIZE_kb_per_launch": vals["FETCH_SIZE"][0],
             "WRITE_SIZE_kb_per_launch": vals["WRITE_SIZE"][0],
             "read_bytes_per_launch": rd, "write_bytes_per_launch": wr,
             "hbm_bytes_per_launch": rd + wr, "alg_bytes_per_launch": alg,
             "traffic_over_alg": (rd + wr) / alg,
             "method": ("rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate runs of "
-                       "bench.py (scripts/gpu_pmc_traffic.sh); bytes = KB*1024, FETCH doubled "
+                       "bench.py (scripts/gpu_pmc_traffic.sh, round 2: gpu_profile_r2.sh / gpu_r2_fft.sh); bytes = KB*1024, FETCH doubled "
                        "per MI355X_MICROARCH.md §HBM (gfx950 counts 1/2 of 16 B/lane streaming "
                        "reads); calibration: the 16 B/lane synth_kernel write of 2 GiB reads "
                        "WRITE_SIZE 2105344 KB = 2.0078 GiB"),
-            "source": f"profiles/round1/pmc_{tag}_FETCH_SIZE.csv, pmc_{tag}_WRITE_SIZE.csv",
+            "source": f"profiles/{rnd}/pmc_{tag}_FETCH_SIZE.csv, pmc_{tag}_WRITE_SIZE.csv",
         }
         json.dump(out, open(os.path.join(ROOT, "profiles", f"pmc_{tag}.json"), "w"), indent=1)
         print(tag, name[:60], out["launches_sampled"], round(out["traffic_over_alg"], 5))
 
 
 if __name__ == "__main__":
-    main()
+    import sys
+    main(*sys.argv[1:])
