@@ -452,15 +452,18 @@ __device__ __forceinline__ f2 pp_im_h(f2 S, f2 T)
 // 32-lane pass of writes or column reads is conflict-free. Reused for the bin
 // powers (4 x 513 floats).
 // Bin powers after step 3, per window (stride kQPow floats): pair j of lane t
-// stores (|X[kP]|^2, |X[512 - kP]|^2) as one f2 at slot 16 j + t; |X[256]|^2
-// sits at float 512. quad_slot(b) is the float index of bin b.
+// stores (|X[kP]|^2, |X[512 - kP]|^2) as one f2 at slot 16 j + t; lane 0's
+// |X[0]|^2, |X[512]|^2 sit at floats 512, 513. quad_slot(b) is the float
+// index of bin b.
 constexpr int kQPow = 544;  // floats per window: 8-byte aligned, odd windows on the other 32 banks
 __host__ __device__ constexpr int quad_slot(int b)
 {
-    if (b == 256) return 512;
     const int u = b & 31, v = b >> 5;
-    if (u == 0) return v < 8 ? 2 * (16 * v) : 2 * (16 * (16 - v)) + 1;  // lane 0: kP = 32 j
-    if (u == 16) return v < 8 ? 2 * (16 * (v + 8)) : 2 * (16 * (23 - v)) + 1;  // lane 0, j >= 8
+    // lane 0: pairs j < 8 hold kP = 16 + 32 j, pair 8 |X[256]|^2 twice,
+    // pairs j > 8 kP = 32 j; |X[0]|^2 and |X[512]|^2 at floats 512, 513
+    if (b == 0 || b == 512) return 512 + (b >> 9);
+    if (u == 0) return v > 8 ? 2 * (16 * v) : v == 8 ? 256 : 2 * (16 * (16 - v)) + 1;
+    if (u == 16) return v < 8 ? 2 * (16 * v) : 2 * (16 * (15 - v)) + 1;
     if (u < 16) return 2 * (16 * v + u);                 // kP = t + 32 j
     return 2 * (16 * (15 - v) + (32 - u)) + 1;           // mirror 512 - kP
 }
@@ -535,7 +538,7 @@ void fft1024_quad_kernel(FftParams p)
     }
     for (int i = threadIdx.x; i < 16 * 16; i += 64 * WPB) {
         const int tt = i & 15, j = i >> 4;
-        tw3[i] = 0.5f * t1024[(tt == 0 && j >= 8) ? 16 + 32 * (j - 8) : tt + 32 * j];
+        tw3[i] = 0.5f * t1024[(tt == 0 && j < 8) ? 16 + 32 * j : tt + 32 * j];
     }
     const int k1b = t == 0 ? 16 : 32 - t;
     const int myslot = quad_slot(t < p.k ? p.bins[t] : 0);
@@ -649,16 +652,16 @@ void fft1024_quad_kernel(FftParams p)
             constexpr int j0 = 2 * decltype(jc)::value, j1 = j0 + 1;
             f2 P0 = b[j0], Q0 = b[16 + 15 - j0];
             f2 P1 = b[j1], Q1 = b[16 + 15 - j1];
-            if constexpr (j0 >= 8) {
-                P0 = sel_l0(b[16 + j0 - 8], P0);
-                P1 = sel_l0(b[16 + j1 - 8], P1);
-            }
+            // lane 0 (columns 0 and 16): pairs j < 8 are column 16's
+            // (Z[16 + 32 j], mirror in the default Q slot), pairs j >= 8
+            // column 0's (Z[32 j] with Z[32 (16 - j)]; j = 8 is Z[256] with
+            // itself): 16 selects instead of 24 for the layout before
             if constexpr (j0 < 8) {
-                Q0 = sel_l0(b[(16 - j0) & 15], Q0);
-                Q1 = sel_l0(b[(16 - j1) & 15], Q1);
+                P0 = sel_l0(b[16 + j0], P0);
+                P1 = sel_l0(b[16 + j1], P1);
             } else {
-                Q0 = sel_l0(b[16 + 23 - j0], Q0);
-                Q1 = sel_l0(b[16 + 23 - j1], Q1);
+                Q0 = sel_l0(b[16 - j0], Q0);
+                Q1 = sel_l0(b[16 - j1], Q1);
             }
             f2 pw0, pw1;  // (|X[kP]|^2, |X[512-kP]|^2)
             const f2 S0 = pp_s(P0, Q0), S1 = pp_s(P1, Q1);
@@ -678,13 +681,18 @@ void fft1024_quad_kernel(FftParams p)
                 pv[2 * j1 + 1] = pw1.y;
             }
         });
-        // Z[256] is its own mirror: |X[256]|^2 = |Z[256]|^2
-        const float p256 = fmaf(b[8].x, b[8].x, b[8].y * b[8].y);
+        // lane 0's X[0] = Re Z[0] + Im Z[0] and X[512] = Re Z[0] - Im Z[0]
+        f2 px;
+        asm("v_pk_add_f32 %0, %1, %1 op_sel:[0,1] op_sel_hi:[0,1] neg_hi:[0,1]" : "=v"(px) : "v"(b[0]));
+        px = px * px;
         const bool live = w < p.n_windows;
         float pk = -1.f;
         int arg = t;
         if constexpr (SPEC) {
-            if (l0) pq[512] = p256;
+            if (l0) {
+                pq[512] = px.x;
+                pq[513] = px.y;
+            }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -701,8 +709,8 @@ void fft1024_quad_kernel(FftParams p)
             for (int i = 0; i < kMaxTones; ++i) {
                 if (i >= p.k) break;
                 const int f = p.slot[i];
-                const bool own = f == 512 ? l0 : t == ((f >> 1) & 15);
-                const float val = f == 512 ? p256 : pv[((f >> 5) << 1) | (f & 1)];
+                const bool own = f >= 512 ? l0 : t == ((f >> 1) & 15);
+                const float val = f >= 512 ? (f == 512 ? px.x : px.y) : pv[((f >> 5) << 1) | (f & 1)];
                 if (own && live && p.mag) p.mag[w * p.k + i] = val;
                 if (own && val > pk) {
                     pk = val;

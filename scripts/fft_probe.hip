@@ -90,9 +90,7 @@ int main(int argc, char **argv)
     vs.push_back({"quad shipped (fused, PF0 MINW4)", [](const FftParams &p, hipStream_t s) { return launch_fft_quad(p, s); }, {}});
     vs.push_back({"aux0 (cached loads)", [](const FftParams &p, hipStream_t s) { return p.spec ? launch_fft_quad_t<4, 4, 0, true, false, 0>(p, s) : launch_fft_quad_t<4, 4, 0, false, false, 0>(p, s); }, {}});
     vs.push_back({"aux2 (nt, round-2 first ship)", [](const FftParams &p, hipStream_t s) { return p.spec ? launch_fft_quad_t<4, 4, 0, true, false, 2>(p, s) : launch_fft_quad_t<4, 4, 0, false, false, 2>(p, s); }, {}});
-    vs.push_back({"aux3 (sc0 nt)", [](const FftParams &p, hipStream_t s) { return p.spec ? launch_fft_quad_t<4, 4, 0, true, false, 3>(p, s) : launch_fft_quad_t<4, 4, 0, false, false, 3>(p, s); }, {}});
     vs.push_back({"fused PF1 MINW0", [](const FftParams &p, hipStream_t s) { return p.spec ? launch_fft_quad_t<4, 0, 1, true>(p, s) : launch_fft_quad_t<4, 0, 1, false>(p, s); }, {}});
-    vs.push_back({"fused FMT PF0 MINW4", [](const FftParams &p, hipStream_t s) { return p.spec ? launch_fft_quad_t<4, 4, 0, true, true>(p, s) : launch_fft_quad_t<4, 4, 0, false, true>(p, s); }, {}});
     if (filter) {
         std::vector<Var> keep;
         for (size_t i = 0; i < vs.size(); ++i)

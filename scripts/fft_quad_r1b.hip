@@ -39,6 +39,17 @@ __device__ __forceinline__ void post_pair2(f2 &pw0, f2 P0, f2 Q0, f2 W0, f2 &pw1
 }
 }  // namespace quad
 namespace r1b {
+// the round-1 lane-0 pairing: pairs j < 8 hold kP = 32 j, j >= 8 kP = 16 + 32 (j - 8),
+// |X[256]|^2 at float 512
+constexpr int quad_slot_r1(int b)
+{
+    if (b == 256) return 512;
+    const int u = b & 31, v = b >> 5;
+    if (u == 0) return v < 8 ? 2 * (16 * v) : 2 * (16 * (16 - v)) + 1;
+    if (u == 16) return v < 8 ? 2 * (16 * (v + 8)) : 2 * (16 * (23 - v)) + 1;
+    if (u < 16) return 2 * (16 * v + u);
+    return 2 * (16 * (15 - v) + (32 - u)) + 1;
+}
 using namespace quad;
 // MINW > 0 asks the compiler for MINW waves per SIMD (VGPR budget 512 / MINW).
 // SPLIT: the next group's 32 loads go out in two halves — the 16 dwords the
@@ -76,7 +87,7 @@ void fft1024_quad_r1_kernel(FftParams p)
         tw3[i] = t1024[(tt == 0 && j >= 8) ? 16 + 32 * (j - 8) : tt + 32 * j];
     }
     const int k1b = t == 0 ? 16 : 32 - t;
-    const int myslot = quad_slot(t < p.k ? p.bins[t] : 0);
+    const int myslot = quad_slot_r1(t < p.k ? p.bins[t] : 0);
     float *pw = reinterpret_cast<float *>(slab[wave]);
     __syncthreads();
 
@@ -235,7 +246,7 @@ void fft1024_quad_r1_kernel(FftParams p)
         if (live && t == 0) p.sym[w] = (uint8_t)arg;
         if (p.spec && live) {
             float *so = p.spec + w * 513;
-            for (int i = t; i < 513; i += 16) so[i] = pq[quad_slot(i)];
+            for (int i = t; i < 513; i += 16) so[i] = pq[quad_slot_r1(i)];
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         __builtin_amdgcn_wave_barrier();
