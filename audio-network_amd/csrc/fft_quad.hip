@@ -25,6 +25,7 @@
 #include <type_traits>
 
 #include "demod_internal.h"
+#include "window_sum.h"
 
 namespace fskd {
 namespace quad {
@@ -687,7 +688,7 @@ void fft1024_quad_kernel(FftParams p)
         px = px * px;
         const bool live = w < p.n_windows;
         float pk = -1.f;
-        int arg = t;
+        int arg = t < p.k ? t : kMaxTones;  // kMaxTones: this lane holds no tone
         if constexpr (SPEC) {
             if (l0) {
                 pq[512] = px.x;
@@ -704,7 +705,7 @@ void fft1024_quad_kernel(FftParams p)
             //    (slot >> 1) & 15 of each window row at pv[slot >> 5 | half]
             //    (uniform index); each lane keeps the best tone it owns (first
             //    index on ties), then the row argmax below
-            arg = 16;
+            arg = kMaxTones;
 #pragma unroll
             for (int i = 0; i < kMaxTones; ++i) {
                 if (i >= p.k) break;
@@ -718,15 +719,9 @@ void fft1024_quad_kernel(FftParams p)
                 }
             }
         }
-        static_for<0, 4>([&](auto sc) {
-            constexpr int ctrl = 0x120 + (1 << decltype(sc)::value);
-            const float po = __int_as_float(
-                __builtin_amdgcn_update_dpp(0, __float_as_int(pk), ctrl, 0xF, 0xF, false));
-            const int ao = __builtin_amdgcn_update_dpp(0, arg, ctrl, 0xF, 0xF, false);
-            const bool take = (po > pk) | ((po == pk) & (ao < arg));
-            pk = take ? po : pk;
-            arg = take ? ao : arg;
-        });
+        // row argmax, ties to the lowest tone: the two DPP max passes of
+        // window_sum.h (powers >= 0, so their bits order as unsigned)
+        arg = (int)ws_argmax<false>(__float_as_uint(pk), arg < kMaxTones, arg);
         if (live && t == 0) p.sym[w] = (uint8_t)arg;
         if constexpr (SPEC) {
             if (p.spec && live) {
