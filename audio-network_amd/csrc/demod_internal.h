@@ -37,6 +37,9 @@ struct GoertzelParams {
     int f16;                 // fold.hip: fold by 16 (K = 8, four tones each on Z0 / Z8)
     int zcls[kMaxTones];     // residue.hip: residue class (0..3) tone k reads
     int xcd_swizzle;         // 1: blocks b, b+8, b+16.. (one XCD) take adjacent tiles
+    // goertzel.hip SLIDE (n = 1024, hop = 64 H < n): a tile is 64 contiguous
+    // segments shared by slide_wt windows (0: off)
+    int slide_wt;
 };
 
 // Output store; NTS = non-temporal (streamed once, never re-read by the kernel).
@@ -101,12 +104,12 @@ hipError_t launch_detector(int detector, const GoertzelParams &p, hipStream_t s)
 // residue.hip: rotation table is [k][g][2] float4 {C1, C2}, {C3, C4}
 const void *residue_kernel_ptr(int k, int log2g, bool dcls = false);
 size_t residue_lds_bytes(int k, int log2g, int qp = 2);
-int tile_grid(long long n_windows, int log2g, int wpb = kWavesPerBlock);
+int tile_grid(long long n_windows, int log2g, int wpb = kWavesPerBlock, int wins_per_tile = 0);
 hipError_t synth_prepare();  // upload the sine table to the current device (once, locked)
 hipError_t launch_synth(const SynthParams &p, hipStream_t s);
 hipError_t launch_read_ceiling(const int16_t *p, long long n_bytes, hipStream_t s);
 hipError_t launch_fft_quad(const FftParams &p, hipStream_t s);  // 16 lanes / window (fft_quad.hip)
-int fft_quad_slot(int bin);  // where fft_quad keeps |X[bin]|^2: 2 (16 j + t) + half, or 512 (bin 256)
+int fft_quad_slot(int bin);  // where fft_quad keeps |X[bin]|^2: 2 (16 j + t) + half, or 512 / 513 (bins 0 / 512)
 // ip.proto framing of [n_streams][n] symbols, one frame run per stream (frame_gpu.hip)
 long long frame_streams_size(long long n, int bits, long long max_payload, unsigned *per,
                              unsigned *full, int *frames);

@@ -64,6 +64,16 @@ __device__ __forceinline__ float group_sum(float v, int log2g)
 //           whole chain after another: issue-stall bound at large K).
 //   WS      window_sum.h epilogue (reduce-scatter, packed-key argmax, one
 //           coalesced magnitude store) at n = 1024.
+//   SLIDE   overlapping windows at n = 1024, hop = 64 H < n: a
+//           window's 16 segments are shared with the windows around it, so a
+//           tile is 64 CONTIGUOUS segments whose recurrence states (s1, s2)
+//           are computed once and kept in LDS; each of the
+//           Wt = (64 - 16) / H + 1 windows u whose segments all lie in the tile
+//           then rotates and sums segments uH .. uH + 15 exactly as the direct
+//           path does (4 windows per pass of the 16-lane epilogue), so its
+//           result is bit-identical to evaluating that window alone. Direct
+//           evaluation recomputes every sample n / hop times and re-reads it
+//           as often.
 //   RS      Reinsch-modified recurrence for tone plans with a tone near 0 or
 //           fs/2, where the fp32 coefficient 2cos(w) cannot resolve w (a tone
 //           at bin 3 of 1024 misses the 1e-5 bar by 4x). With sgn = sign(cos w),
@@ -75,10 +85,11 @@ __device__ __forceinline__ float group_sum(float v, int log2g)
 //           constants: X += (A - sgn B) s1 + sgn B d.
 template <int K, int LOG2G, int PF = 1, bool NT = true, int WPB = kWavesPerBlock,
           bool DIRECT = false, bool NTS = false, bool PK = false, bool SB = false,
-          bool WS = false, bool RS = false>
+          bool WS = false, bool RS = false, bool SLIDE = false>
 __global__ __launch_bounds__(64 * WPB) void goertzel_tile_kernel(GoertzelParams p)
 {
     static_assert(PF == 1 || PF == 2, "prefetch depth");
+    static_assert(!SLIDE || (LOG2G == 4 && !DIRECT && PF == 1), "SLIDE: n = 1024");
     __shared__ __attribute__((aligned(16))) unsigned char lds[DIRECT ? 16 : WPB * kLdsWaveBytes];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: tile bases stay in SGPRs (no waterfall loop per buffer load)
@@ -88,7 +99,7 @@ __global__ __launch_bounds__(64 * WPB) void goertzel_tile_kernel(GoertzelParams 
     const int n = 64 << log2g;
     const int seg = lane & (g - 1);          // segment index inside the window
     const int win_in_tile = lane >> log2g;
-    const long long wins_per_tile = 64 >> log2g;
+    const long long wins_per_tile = SLIDE ? (long long)p.slide_wt : 64 >> log2g;
     const long long n_tiles = (p.n_windows + wins_per_tile - 1) / wins_per_tile;
 
     float4 r[K];
@@ -96,8 +107,10 @@ __global__ __launch_bounds__(64 * WPB) void goertzel_tile_kernel(GoertzelParams 
     for (int k = 0; k < K; ++k) r[k] = p.rot[k * g + seg];
 
     // Byte offset (from the tile's first window) of this lane's 16-byte chunk
-    // i: chunk q = 64 i + lane is chunk (q mod 8G) of tile window q / 8G.
+    // i: chunk q = 64 i + lane is chunk (q mod 8G) of tile window q / 8G
+    // (SLIDE: the tile's samples are contiguous, i.e. the same with hop = n).
     const int cpw_log2 = 3 + log2g;
+    const long long lhop = SLIDE ? (long long)n : p.hop;
     int goff[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -105,7 +118,7 @@ __global__ __launch_bounds__(64 * WPB) void goertzel_tile_kernel(GoertzelParams 
         if (DIRECT)
             goff[i] = (int)(((long long)win_in_tile * p.hop + seg * 64 + 8 * i) * 2);
         else
-            goff[i] = (int)(((long long)(q >> cpw_log2) * p.hop +
+            goff[i] = (int)(((long long)(q >> cpw_log2) * lhop +
                              (long long)(q & ((1 << cpw_log2) - 1)) * 8) * 2);
     }
     // LDS write slot of chunk i: segment 8i + lane/8, chunk lane%8
@@ -244,6 +257,58 @@ __global__ __launch_bounds__(64 * WPB) void goertzel_tile_kernel(GoertzelParams 
         }
         }
 
+        if constexpr (SLIDE) {
+            // segment states -> LDS (the samples are consumed)
+            float2 *lz = reinterpret_cast<float2 *>(wl);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+            for (int k = 0; k < K; ++k) lz[k * 64 + lane] = make_float2(s1[k], s2[k]);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const int H = (int)(p.hop >> 6);
+            const int wt = (int)wins_per_tile;
+            for (int u0 = 0; u0 < wt; u0 += 4) {
+                const int u = u0 + win_in_tile;                 // window of the tile
+                const int sg = (u < wt ? u * H : 0) + seg;      // its segment j = seg
+                const long long w = tt * wins_per_tile + u;
+                const bool live = u < wt && w < p.n_windows;
+                float xr[K], xi[K];
+#pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    const float2 z = lz[k * 64 + sg];   // (s1, s2) of segment j of window u
+                    xr[k] = r[k].x * z.x - r[k].z * z.y;
+                    xi[k] = r[k].y * z.x - r[k].w * z.y;
+                }
+                if constexpr (WS) {
+                    window_sum_decide<K>(xr, xi, lane, w, live, p.sym, p.mag);
+                } else {
+                    float best = -1.f;
+                    int arg = 0;
+                    float P[K];
+#pragma unroll
+                    for (int k = 0; k < K; ++k) {
+                        const float re = group_sum(xr[k], 4), im = group_sum(xi[k], 4);
+                        P[k] = fmaf(re, re, im * im);
+                        if (P[k] > best) { best = P[k]; arg = k; }
+                    }
+                    if (live) {
+                        if (seg == 0) out_store<NTS>(p.sym + w, (uint8_t)arg);
+                        if (p.mag) {
+#pragma unroll
+                            for (int k = 0; k < K; ++k)
+                                if ((k & 15) == seg) out_store<NTS>(p.mag + w * K + k, P[k]);
+                        }
+                    }
+                }
+            }
+            // the next tile's samples overwrite the partials
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            return;
+        }
         const long long w = tt * wins_per_tile + win_in_tile;
         if constexpr (WS && LOG2G == 4) {
             float xr[K], xi[K];
@@ -301,9 +366,16 @@ __global__ __launch_bounds__(64 * WPB) void goertzel_tile_kernel(GoertzelParams 
 // RS (Reinsch form) only for plans with a tone near 0 or fs/2 (the host's
 // kReinschSin test): elsewhere the plain form is within the bar at 2 ops.
 template <int K>
-static const void *kernel_for(int log2g, bool rs)
+static const void *kernel_for(int log2g, bool rs, bool slide)
 {
     constexpr bool PK = K >= 3;
+    if (slide)  // cached loads: neighbouring tiles share their edge segments
+        return rs ? reinterpret_cast<const void *>(
+                        &goertzel_tile_kernel<K, 4, 1, false, kPlainWPB, false, false, PK, false,
+                                              K >= 3, true, true>)
+                  : reinterpret_cast<const void *>(
+                        &goertzel_tile_kernel<K, 4, 1, false, kPlainWPB, false, false, PK, false,
+                                              K >= 3, false, true>);
     if (log2g == 4)
         return rs ? reinterpret_cast<const void *>(
                         &goertzel_tile_kernel<K, 4, 1, true, kPlainWPB, false, false, PK, false,
@@ -318,10 +390,10 @@ static const void *kernel_for(int log2g, bool rs)
                     &goertzel_tile_kernel<K, -1, 1, true, kPlainWPB, false, false, PK>);
 }
 
-static const void *kernel_ptr(int k, int log2g, bool rs)
+static const void *kernel_ptr(int k, int log2g, bool rs, bool slide)
 {
     switch (k) {
-#define FSKD_CASE(K) case K: return kernel_for<K>(log2g, rs);
+#define FSKD_CASE(K) case K: return kernel_for<K>(log2g, rs, slide);
         FSKD_CASE(1) FSKD_CASE(2) FSKD_CASE(3) FSKD_CASE(4)
         FSKD_CASE(5) FSKD_CASE(6) FSKD_CASE(7) FSKD_CASE(8)
         FSKD_CASE(9) FSKD_CASE(10) FSKD_CASE(11) FSKD_CASE(12)
@@ -334,9 +406,9 @@ static const void *kernel_ptr(int k, int log2g, bool rs)
 // One tile per wave (grid = tiles / waves-per-block): measured 317 us vs
 // 363 us for a persistent grid-stride grid on 2^20 windows (profiles/,
 // DESIGN.md §Tuning) — the dispatcher keeps every CU fed to the last tile.
-int tile_grid(long long n_windows, int log2g, int wpb)
+int tile_grid(long long n_windows, int log2g, int wpb, int wins_per_tile_override)
 {
-    const long long wins_per_tile = 64 >> log2g;
+    const long long wins_per_tile = wins_per_tile_override > 0 ? wins_per_tile_override : 64 >> log2g;
     const long long n_tiles = (n_windows + wins_per_tile - 1) / wins_per_tile;
     long long blocks = (n_tiles + wpb - 1) / wpb;
     if (blocks > 0x7FFFFFFFLL) blocks = 0x7FFFFFFFLL;  // kernels grid-stride beyond
@@ -350,13 +422,16 @@ hipError_t launch_detector(int detector, const GoertzelParams &p, hipStream_t s)
 {
     const void *f = detector == kDetFolded    ? fold_kernel_ptr(p.k, p.log2g, p.f16 != 0)
                   : detector == kDetResidue ? residue_kernel_ptr(p.k, p.log2g, p.dcls != 0)
-                                            : kernel_ptr(p.k, p.log2g, p.reinsch != 0);
+                                            : kernel_ptr(p.k, p.log2g, p.reinsch != 0, p.slide_wt > 0);
     if (!f) return hipErrorInvalidValue;
+    if (p.slide_wt > 0 && (detector != kDetGoertzel || p.log2g != 4 || p.hop % 64 ||
+                           (p.slide_wt - 1) * (p.hop / 64) + 16 > 64))
+        return hipErrorInvalidValue;  // a tile must hold every segment of its windows
     const size_t lds = detector == kDetResidue ? residue_lds_bytes(p.k, p.log2g) : 0;
     const int wpb = detector == kDetResidue ? kWavesPerBlock : kPlainWPB;
     void *args[] = {const_cast<GoertzelParams *>(&p)};
-    return hipLaunchKernel(f, dim3(tile_grid(p.n_windows, p.log2g, wpb)), dim3(64 * wpb), args,
-                           lds, s);
+    return hipLaunchKernel(f, dim3(tile_grid(p.n_windows, p.log2g, wpb, p.slide_wt)), dim3(64 * wpb),
+                           args, lds, s);
 }
 
 }  // namespace fskd
