@@ -62,9 +62,14 @@ extern "C" {
 #define DEMOD_CH_DOWNMIX  2   /* x = (L + R) >> 1 (arithmetic shift) */
 
 /* detector selection */
-#define DEMOD_METHOD_AUTO      0 /* FOLDED when eligible and k >= 3, else RESIDUE
-                                    when eligible and k >= 5, else GOERTZEL */
-#define DEMOD_METHOD_GOERTZEL  1 /* per-window Goertzel tone bank over all n samples */
+#define DEMOD_METHOD_AUTO      0 /* GOERTZEL for overlapping windows at n = 1024,
+                                    hop = 64 H <= 256; otherwise FOLDED when eligible
+                                    and k >= 3, else RESIDUE when eligible and
+                                    k >= 5, else GOERTZEL */
+#define DEMOD_METHOD_GOERTZEL  1 /* per-window Goertzel tone bank over all n samples
+                                    (n = 1024, hop = 64 H < n: 64-sample segments
+                                    shared by the windows that contain them, same
+                                    results as evaluating each window alone) */
 #define DEMOD_METHOD_FFT       2 /* full-spectrum n-point real FFT (n = 1024), argmax
                                     over the tone bins round(f*n/fs) */
 #define DEMOD_METHOD_FOLDED    3 /* Goertzel over the window folded to n/8 samples:
