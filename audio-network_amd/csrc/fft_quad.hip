@@ -507,7 +507,7 @@ constexpr int kFmtWord3 = 0xFAC | (3 << 12) | (5 << 15);
 // from the registers of the lanes that hold them (p.slot, a wave-uniform
 // index: s_set_gpr_idx) instead of going through the 2 KiB per-window power
 // slab in LDS; true = the slab, for the full-spectrum store.
-// AUX: the loads' cache-policy bits (2 = nt, 1 = sc0; launch_fft_quad).
+// AUX: the loads' cache-policy bits (2 = nt, 1 = sc0, 0 = plain; launch_fft_quad).
 // FMT (PF = 0 only): typed buffer loads (16_16 SSCALED) convert both int16
 // halves to fp32 in the texture path instead of 64 VALU converts per group
 // (measured neutral).
@@ -759,14 +759,14 @@ hipError_t launch_fft_quad_t(const FftParams &p, hipStream_t s)
 // register tone pick unless the full spectrum is asked for
 // (scripts/fft_probe.hip, profiles/round2/fft/). Load policy: windows that
 // overlap (hop < n) are read by up to n / hop groups, so their loads keep the
-// lines in L2 (sc0, AUX 1: FETCH 1.06x the stream at hop 256, -5 %);
-// disjoint windows stream through with nt (AUX 2; nt at hop 256 re-fetches
-// 1.55x the stream).
+// lines in L2 (plain cached loads, AUX 0: FETCH 1.06x the stream at hop 256,
+// 3-6 % faster; sc0 measured the same or slower); disjoint windows stream
+// through with nt (AUX 2; nt at hop 256 re-fetches 1.55x the stream).
 hipError_t launch_fft_quad(const FftParams &p, hipStream_t s)
 {
     if (p.hop < 1024)
-        return p.spec ? launch_fft_quad_t<4, 4, 0, true, false, 1>(p, s)
-                      : launch_fft_quad_t<4, 4, 0, false, false, 1>(p, s);
+        return p.spec ? launch_fft_quad_t<4, 4, 0, true, false, 0>(p, s)
+                      : launch_fft_quad_t<4, 4, 0, false, false, 0>(p, s);
     return p.spec ? launch_fft_quad_t<4, 4, 0, true, false, 2>(p, s)
                   : launch_fft_quad_t<4, 4, 0, false, false, 2>(p, s);
 }
