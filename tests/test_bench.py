@@ -1,0 +1,81 @@
+"""CPU checks of bench.py's reporting helpers and of the decision checker the
+GPU parity tests rely on (tests/decision.py): no GPU, no compute calls."""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from decision import BAND, check_decisions
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+
+def test_margin_stats_histogram():
+    P = np.array([[1.0, 0.0], [1.0, 1.0 - 1e-7], [1.0, 0.5], [2.0, 2.0 - 4e-5], [3.0, 2.9]])
+    m = bench.margin_stats(P)
+    assert m["windows"] == 5 and sum(m["hist_counts"]) == 5
+    assert m["min_margin"] == pytest.approx(1e-7, rel=1e-6)
+    assert m["below_4e-5"] == 2
+    # bins [0,1e-6) [1e-6,1e-5) [1e-5,1e-4) [1e-4,1e-3) [1e-3,1e-2) [1e-2,1e-1) [1e-1,1]
+    assert m["hist_counts"] == [1, 0, 1, 0, 0, 1, 2]
+    assert bench.margin_stats(np.ones((4, 1))) == {}
+
+
+def test_cpu_share_is_sane():
+    visible, affinity, quota, threads, why = bench.cpu_share()
+    assert 1 <= threads <= affinity <= visible
+    assert quota is None or threads >= 1
+    assert isinstance(why, str) and why
+
+
+def test_pmc_traffic_matches_config_and_hop():
+    d = json.load(open(os.path.join(ROOT, "profiles", "pmc_fsk2.json")))
+    W = int(d["windows"])
+    assert bench.pmc_traffic("fsk2", W) == pytest.approx(d["hbm_bytes_per_launch"])
+    assert bench.pmc_traffic("fsk2", W + 1) is None          # other workload size
+    assert bench.pmc_traffic("fsk2", W, hop=256) is None     # other hop
+    assert bench.pmc_traffic("no_such_config", W) is None
+    f = json.load(open(os.path.join(ROOT, "profiles", "pmc_fft.json")))
+    assert f["hop"] == 256
+    assert bench.pmc_traffic("fft", int(f["windows"]), hop=256) == pytest.approx(f["hbm_bytes_per_launch"])
+    # every traffic file is within a few % of its algorithmic bytes
+    for name in ("fsk2", "fsk8", "fsk8odd", "fft", "fft1024"):
+        t = json.load(open(os.path.join(ROOT, "profiles", f"pmc_{name}.json")))
+        assert 0.99 < t["traffic_over_alg"] < 1.1, name
+
+
+def test_bench_help_lists_the_contract_flags():
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--help"],
+                       capture_output=True, timeout=120, cwd=ROOT)
+    out = r.stdout.decode()
+    assert r.returncode == 0
+    for flag in ("--gpus", "--steps", "--warmup", "--config", "--dist-backend", "--no-extras"):
+        assert flag in out
+
+
+def test_decision_checker_accepts_exact_argmax_and_band_ties():
+    ref_P = np.array([[10.0, 1.0], [1.0, 10.0], [5.0, 5.0 * (1 - BAND / 2)], [0.0, 0.0]])
+    ref_sym = ref_P.argmax(axis=1)
+    mag = ref_P.astype(np.float32).copy()
+    sym = mag.argmax(axis=1)
+    assert check_decisions(sym, mag, ref_sym, ref_P) == 2      # the near tie and the zero window
+    # inside the band the GPU may resolve the near tie the other way
+    mag2 = mag.copy()
+    mag2[2] = [4.9999, 5.0]
+    assert check_decisions(mag2.argmax(axis=1), mag2, ref_sym, ref_P) == 2
+
+
+def test_decision_checker_rejects_wrong_decisions():
+    ref_P = np.array([[10.0, 1.0], [1.0, 10.0]])
+    ref_sym = ref_P.argmax(axis=1)
+    mag = ref_P.astype(np.float32)
+    with pytest.raises(AssertionError):                        # not the argmax of its own powers
+        check_decisions(np.array([1, 1]), mag, ref_sym, ref_P)
+    bad = mag[:, ::-1].copy()
+    with pytest.raises(AssertionError):                        # differs from the oracle outside the band
+        check_decisions(bad.argmax(axis=1), bad, ref_sym, ref_P)
