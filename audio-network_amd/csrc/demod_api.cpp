@@ -195,12 +195,12 @@ static int init_device_state(demod_t *st)
     // Overlapping windows at n = 1024 with hop a multiple of 64 share their
     // 64-sample segments: the plain bank computes each segment once (SLIDE,
     // goertzel.hip). AUTO keeps it over the folded detectors
-    // up to hop 256 (8-FSK: 0.71 vs 0.83 ms at hop 256, 0.59 vs 0.50 at 512).
+    // up to hop 128 (8-FSK: 0.89 vs 1.23 ms at hop 128, 0.71 vs 0.68 at 256).
     const bool slide = lg == 4 && c.hop < c.n && c.hop % 64 == 0;
     st->detector = kDetGoertzel;
     if (c.method == DEMOD_METHOD_FOLDED) st->detector = kDetFolded;
     else if (c.method == DEMOD_METHOD_RESIDUE) st->detector = kDetResidue;
-    else if (c.method == DEMOD_METHOD_AUTO && !(slide && c.hop <= 256)) {
+    else if (c.method == DEMOD_METHOD_AUTO && !(slide && c.hop <= 128)) {
         if (c.k >= 3 && fold_eligible(c)) st->detector = kDetFolded;
         else if (c.k >= 5 && residue_eligible(c)) st->detector = kDetResidue;
     }
@@ -478,7 +478,9 @@ static int enqueue_batch(demod_t *st, const int16_t *d_pcm, size_t n_windows, ui
     p.f16 = st->f16 ? 1 : 0;
     p.perm = st->perm;
     p.slide_wt = st->slide_wt;
-    p.xcd_swizzle = st->slide_wt > 0 ? 1 : 0;  // neighbouring tiles share edge segments in L2
+    // overlapping windows: neighbouring tiles share lines, keep them in one L2
+    p.cached = st->cfg.hop < st->cfg.n ? 1 : 0;
+    p.xcd_swizzle = p.cached;
     HIP_TRY(launch_detector(st->detector, p, s));
     return (int)n_windows;
 }

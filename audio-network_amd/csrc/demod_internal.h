@@ -40,6 +40,9 @@ struct GoertzelParams {
     // goertzel.hip SLIDE (n = 1024, hop = 64 H < n): a tile is 64 contiguous
     // segments shared by slide_wt windows (0: off)
     int slide_wt;
+    // 1: overlapping windows (hop < n) share lines between tiles, so the loads
+    // keep them in L2 (plain policy); 0: each byte is read once (nt)
+    int cached;
 };
 
 // Output store; NTS = non-temporal (streamed once, never re-read by the kernel).
@@ -102,7 +105,7 @@ constexpr int kDetResidue = 4;   // residue.hip: per-residue-class folding (any 
 
 hipError_t launch_detector(int detector, const GoertzelParams &p, hipStream_t s);
 // residue.hip: rotation table is [k][g][2] float4 {C1, C2}, {C3, C4}
-const void *residue_kernel_ptr(int k, int log2g, bool dcls = false);
+const void *residue_kernel_ptr(int k, int log2g, bool dcls = false, bool nt = true);
 size_t residue_lds_bytes(int k, int log2g, int qp = 2);
 int tile_grid(long long n_windows, int log2g, int wpb = kWavesPerBlock, int wins_per_tile = 0);
 hipError_t synth_prepare();  // upload the sine table to the current device (once, locked)

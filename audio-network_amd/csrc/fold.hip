@@ -246,26 +246,33 @@ __global__ __launch_bounds__(64 * WPB) void fold_tile_kernel(GoertzelParams p)
     }
 }
 
-template <int K>
-static const void *fold_kernel_for(int log2g, bool f16)
+template <int K, bool NT>
+static const void *fold_kernel_for_t(int log2g, bool f16)
 {
     if constexpr (K == 8)
         if (log2g == 4 && f16)
             return reinterpret_cast<const void *>(
-                &fold_tile_kernel<8, 4, true, kPlainWPB, false, false, true, false, true, true>);
+                &fold_tile_kernel<8, 4, NT, kPlainWPB, false, false, true, false, true, true>);
     // n = 1024: window_sum.h epilogue (K = 8: 352 -> 347 us, K = 2: 335 -> 329 us)
     // and LDS regrouping of contiguous loads (K = 8: 345.8 -> 339.9 us, K = 2:
     // 338.5 -> 319.9 us; profiles/round1/probe_ldst.log)
     if (log2g == 4)
         return reinterpret_cast<const void *>(
-            &fold_tile_kernel<K, 4, true, kPlainWPB, false, false, true, false, true>);
-    return reinterpret_cast<const void *>(&fold_tile_kernel<K, -1, true, kPlainWPB>);
+            &fold_tile_kernel<K, 4, NT, kPlainWPB, false, false, true, false, true>);
+    return reinterpret_cast<const void *>(&fold_tile_kernel<K, -1, NT, kPlainWPB>);
 }
 
-const void *fold_kernel_ptr(int k, int log2g, bool f16)
+// nt: hop = n (each byte read once); overlapping windows keep their lines in L2
+template <int K>
+static const void *fold_kernel_for(int log2g, bool f16, bool nt)
+{
+    return nt ? fold_kernel_for_t<K, true>(log2g, f16) : fold_kernel_for_t<K, false>(log2g, f16);
+}
+
+const void *fold_kernel_ptr(int k, int log2g, bool f16, bool nt)
 {
     switch (k) {
-#define FSKD_CASE(K) case K: return fold_kernel_for<K>(log2g, f16);
+#define FSKD_CASE(K) case K: return fold_kernel_for<K>(log2g, f16, nt);
         FSKD_CASE(1) FSKD_CASE(2) FSKD_CASE(3) FSKD_CASE(4)
         FSKD_CASE(5) FSKD_CASE(6) FSKD_CASE(7) FSKD_CASE(8)
         FSKD_CASE(9) FSKD_CASE(10) FSKD_CASE(11) FSKD_CASE(12)

@@ -365,8 +365,28 @@ __global__ __launch_bounds__(64 * WPB) void goertzel_tile_kernel(GoertzelParams 
 // profiles/round1/probe_window_sum.log).
 // RS (Reinsch form) only for plans with a tone near 0 or fs/2 (the host's
 // kReinschSin test): elsewhere the plain form is within the bar at 2 ops.
+template <int K, bool NT>
+static const void *kernel_for_t(int log2g, bool rs)
+{
+    constexpr bool PK = K >= 3;
+    if (log2g == 4)
+        return rs ? reinterpret_cast<const void *>(
+                        &goertzel_tile_kernel<K, 4, 1, NT, kPlainWPB, false, false, PK, false,
+                                              K >= 3, true>)
+                  : reinterpret_cast<const void *>(
+                        &goertzel_tile_kernel<K, 4, 1, NT, kPlainWPB, false, false, PK, false,
+                                              K >= 3>);
+    return rs ? reinterpret_cast<const void *>(
+                    &goertzel_tile_kernel<K, -1, 1, NT, kPlainWPB, false, false, PK, false,
+                                          false, true>)
+              : reinterpret_cast<const void *>(
+                    &goertzel_tile_kernel<K, -1, 1, NT, kPlainWPB, false, false, PK>);
+}
+
+// nt: the PCM is read once (hop = n); overlapping windows (hop < n) load with
+// the plain cache policy so neighbouring tiles find their shared lines in L2.
 template <int K>
-static const void *kernel_for(int log2g, bool rs, bool slide)
+static const void *kernel_for(int log2g, bool rs, bool slide, bool nt)
 {
     constexpr bool PK = K >= 3;
     if (slide)  // cached loads: neighbouring tiles share their edge segments
@@ -376,24 +396,13 @@ static const void *kernel_for(int log2g, bool rs, bool slide)
                   : reinterpret_cast<const void *>(
                         &goertzel_tile_kernel<K, 4, 1, false, kPlainWPB, false, false, PK, false,
                                               K >= 3, false, true>);
-    if (log2g == 4)
-        return rs ? reinterpret_cast<const void *>(
-                        &goertzel_tile_kernel<K, 4, 1, true, kPlainWPB, false, false, PK, false,
-                                              K >= 3, true>)
-                  : reinterpret_cast<const void *>(
-                        &goertzel_tile_kernel<K, 4, 1, true, kPlainWPB, false, false, PK, false,
-                                              K >= 3>);
-    return rs ? reinterpret_cast<const void *>(
-                    &goertzel_tile_kernel<K, -1, 1, true, kPlainWPB, false, false, PK, false,
-                                          false, true>)
-              : reinterpret_cast<const void *>(
-                    &goertzel_tile_kernel<K, -1, 1, true, kPlainWPB, false, false, PK>);
+    return nt ? kernel_for_t<K, true>(log2g, rs) : kernel_for_t<K, false>(log2g, rs);
 }
 
-static const void *kernel_ptr(int k, int log2g, bool rs, bool slide)
+static const void *kernel_ptr(int k, int log2g, bool rs, bool slide, bool nt)
 {
     switch (k) {
-#define FSKD_CASE(K) case K: return kernel_for<K>(log2g, rs, slide);
+#define FSKD_CASE(K) case K: return kernel_for<K>(log2g, rs, slide, nt);
         FSKD_CASE(1) FSKD_CASE(2) FSKD_CASE(3) FSKD_CASE(4)
         FSKD_CASE(5) FSKD_CASE(6) FSKD_CASE(7) FSKD_CASE(8)
         FSKD_CASE(9) FSKD_CASE(10) FSKD_CASE(11) FSKD_CASE(12)
@@ -416,13 +425,14 @@ int tile_grid(long long n_windows, int log2g, int wpb, int wins_per_tile_overrid
     return (int)blocks;
 }
 
-const void *fold_kernel_ptr(int k, int log2g, bool f16);
+const void *fold_kernel_ptr(int k, int log2g, bool f16, bool nt);
 
 hipError_t launch_detector(int detector, const GoertzelParams &p, hipStream_t s)
 {
-    const void *f = detector == kDetFolded    ? fold_kernel_ptr(p.k, p.log2g, p.f16 != 0)
-                  : detector == kDetResidue ? residue_kernel_ptr(p.k, p.log2g, p.dcls != 0)
-                                            : kernel_ptr(p.k, p.log2g, p.reinsch != 0, p.slide_wt > 0);
+    const bool nt = p.cached == 0;
+    const void *f = detector == kDetFolded    ? fold_kernel_ptr(p.k, p.log2g, p.f16 != 0, nt)
+                  : detector == kDetResidue ? residue_kernel_ptr(p.k, p.log2g, p.dcls != 0, nt)
+                                            : kernel_ptr(p.k, p.log2g, p.reinsch != 0, p.slide_wt > 0, nt);
     if (!f) return hipErrorInvalidValue;
     if (p.slide_wt > 0 && (detector != kDetGoertzel || p.log2g != 4 || p.hop % 64 ||
                            (p.slide_wt - 1) * (p.hop / 64) + 16 > 64))

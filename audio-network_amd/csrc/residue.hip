@@ -133,7 +133,7 @@ constexpr int kResidueQP = 2;  // shipped: two sample pairs per LDS round
 //         K = 8, e.g. any odd bin spacing).
 template <int K, int LOG2G, int WPB = kWavesPerBlock, bool ASM = true, bool ROTV = false,
           int MINW = (K <= 8 ? 4 : 0), int QP = kResidueQP, bool PF = false, bool WS = true,
-          bool LDST = false, bool DCLS = false>
+          bool LDST = false, bool DCLS = false, bool NT = true>
 __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MINW > 0 ? MINW : 1)))
 void residue_tile_kernel(GoertzelParams p)
 {
@@ -170,7 +170,7 @@ void residue_tile_kernel(GoertzelParams p)
             (void *)(p.pcm + wbase * p.hop), (short)0, (int)bytes, 0x00020000);
 #pragma unroll
         for (int m = 0; m < 8; ++m)
-            v[m] = __builtin_amdgcn_raw_buffer_load_b128(rs, goff[m], 0, 2);
+            v[m] = __builtin_amdgcn_raw_buffer_load_b128(rs, goff[m], 0, NT ? 2 : 0);
     };
 
     const long long stride = (long long)gridDim.x * WPB;
@@ -331,24 +331,35 @@ size_t residue_lds_bytes(int k, int log2g, int qp)
 // DCLS (K = 8, 16 at n = 1024, host-permuted plans with K / 4 tones per
 // class): 356-362 -> 312 us at K = 8 on bins 32 + 9i, the box's read ceiling
 // (profiles/round1/probe_dcls.log).
-template <int K>
-static const void *residue_kernel_for(int log2g, bool dcls)
+template <int K, bool NT>
+static const void *residue_kernel_for_t(int log2g, bool dcls)
 {
     if (log2g == 4) {
         if constexpr (K == 8 || K == 16)
             if (dcls)
                 return reinterpret_cast<const void *>(
                     &residue_tile_kernel<K, 4, kWavesPerBlock, true, false, (K <= 8 ? 4 : 0),
-                                         kResidueQP, false, true, false, true>);
-        return reinterpret_cast<const void *>(&residue_tile_kernel<K, 4>);
+                                         kResidueQP, false, true, false, true, NT>);
+        return reinterpret_cast<const void *>(
+            &residue_tile_kernel<K, 4, kWavesPerBlock, true, false, (K <= 8 ? 4 : 0), kResidueQP,
+                                 false, true, false, false, NT>);
     }
-    return reinterpret_cast<const void *>(&residue_tile_kernel<K, -1>);
+    return reinterpret_cast<const void *>(
+        &residue_tile_kernel<K, -1, kWavesPerBlock, true, false, (K <= 8 ? 4 : 0), kResidueQP, false,
+                             true, false, false, NT>);
 }
 
-const void *residue_kernel_ptr(int k, int log2g, bool dcls)
+// nt: hop = n (each byte read once); overlapping windows keep their lines in L2
+template <int K>
+static const void *residue_kernel_for(int log2g, bool dcls, bool nt)
+{
+    return nt ? residue_kernel_for_t<K, true>(log2g, dcls) : residue_kernel_for_t<K, false>(log2g, dcls);
+}
+
+const void *residue_kernel_ptr(int k, int log2g, bool dcls, bool nt)
 {
     switch (k) {
-#define FSKD_CASE(K) case K: return residue_kernel_for<K>(log2g, dcls);
+#define FSKD_CASE(K) case K: return residue_kernel_for<K>(log2g, dcls, nt);
         FSKD_CASE(1) FSKD_CASE(2) FSKD_CASE(3) FSKD_CASE(4)
         FSKD_CASE(5) FSKD_CASE(6) FSKD_CASE(7) FSKD_CASE(8)
         FSKD_CASE(9) FSKD_CASE(10) FSKD_CASE(11) FSKD_CASE(12)

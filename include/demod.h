@@ -63,7 +63,7 @@ extern "C" {
 
 /* detector selection */
 #define DEMOD_METHOD_AUTO      0 /* GOERTZEL for overlapping windows at n = 1024,
-                                    hop = 64 H <= 256; otherwise FOLDED when eligible
+                                    hop = 64 H <= 128; otherwise FOLDED when eligible
                                     and k >= 3, else RESIDUE when eligible and
                                     k >= 5, else GOERTZEL */
 #define DEMOD_METHOD_GOERTZEL  1 /* per-window Goertzel tone bank over all n samples

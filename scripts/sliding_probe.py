@@ -20,7 +20,7 @@ sys.path.insert(0, ROOT)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--samples-log2", type=int, default=30)
-    ap.add_argument("--hops", default="1024,512,256,128")
+    ap.add_argument("--hops", default="1024,1000,512,256,200,128")
     args = ap.parse_args()
     import numpy as np
     import torch
