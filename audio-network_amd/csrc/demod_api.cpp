@@ -440,7 +440,7 @@ static int enqueue_fft(demod_t *st, const int16_t *d_pcm, size_t n_windows, uint
     p.n_windows = (long long)n_windows;
     p.hop = st->cfg.hop;
     p.k = (int)st->cfg.k;
-    p.xcd_swizzle = st->cfg.hop < st->cfg.n ? 1 : 0;  // overlapping windows: keep neighbours on one L2
+    p.xcd_swizzle = 1;  // neighbouring groups on one L2: shared input lines, whole output lines
     p.tw512 = st->d_tw512;
     p.tw1024 = st->d_tw1024;
     p.bins = st->d_bins;
