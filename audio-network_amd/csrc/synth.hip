@@ -104,12 +104,13 @@ typedef unsigned int u32x4s __attribute__((ext_vector_type(4)));
 // Read-only reference stream for bench.py (demod_read_ceiling_async): each
 // wave reads one contiguous 8 KiB tile with 8 coalesced 16 B/lane
 // non-temporal buffer loads and discards it, i.e. the tile kernels' access
-// pattern with no compute and no stores. Its bandwidth on the box at hand is
-// the practical ceiling the detector kernels are compared with.
-__global__ __launch_bounds__(256) void read_ceiling_kernel(const int16_t *p, long long n_tiles)
+// pattern (2-wave blocks, XCD-swizzled tiles) with no compute and no stores.
+// Its bandwidth on the box at hand is the practical ceiling the detector
+// kernels are compared with.
+__global__ __launch_bounds__(64 * kPlainWPB) void read_ceiling_kernel(const int16_t *p, long long n_tiles)
 {
     const int lane = threadIdx.x & 63;
-    const long long t = (long long)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const long long t = tile_block(1) * kPlainWPB + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (t >= n_tiles) return;
     __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         (void *)(p + t * 4096), (short)0, 8192, 0x00020000);
@@ -126,9 +127,10 @@ hipError_t launch_read_ceiling(const int16_t *p, long long n_bytes, hipStream_t 
 {
     const long long n_tiles = n_bytes / 8192;
     if (n_tiles <= 0) return hipSuccess;
-    const long long blocks = (n_tiles + 3) / 4;
+    const long long blocks = (n_tiles + kPlainWPB - 1) / kPlainWPB;
     if (blocks > 0x7FFFFFFFLL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(read_ceiling_kernel, dim3((unsigned)blocks), dim3(256), 0, s, p, n_tiles);
+    hipLaunchKernelGGL(read_ceiling_kernel, dim3((unsigned)blocks), dim3(64 * kPlainWPB), 0, s, p,
+                       n_tiles);
     return hipGetLastError();
 }
 
