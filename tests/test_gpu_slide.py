@@ -157,3 +157,71 @@ def test_large_stream_hop256(A, O, torch):
     denom = np.maximum(ref_P.max(axis=1), energy / 100)
     assert (np.abs(g_mag.astype(np.float64) - ref_P).max(axis=1) / denom).max() <= MAG_TOL
     check_decisions(g_sym, g_mag, ref_sym, ref_P, denom)
+
+
+def draw(i):
+    rng = np.random.default_rng(0x51DE + i)
+    H = int(rng.integers(1, 16))
+    k = int(rng.integers(1, 17))
+    if rng.random() < 0.5:
+        bins = np.sort(rng.choice(np.arange(2, 510), k, replace=False)).astype(np.float64)
+    else:
+        for _ in range(1000):
+            bins = np.sort(rng.uniform(2.0, 510.0, k))
+            if k == 1 or np.diff(bins).min() >= 2.0:
+                break
+    freqs = tuple(float(b) * 48000.0 / 1024 for b in rng.permutation(bins))
+    W = int(rng.integers(1, 300))
+    amplitude = int(rng.choice([300, 2000, 8000, 20000]))
+    sigma = int(rng.choice([0, 100, 400, 1500]))
+    return H, freqs, W, amplitude, sigma
+
+
+@pytest.mark.parametrize("i", range(40))
+def test_random_sweep(A, O, torch, i):
+    """Seeded random H, K (1..16), integer / off-bin plans, window count and
+    level; windows whose tone powers sit far below their energy (a symbol
+    boundary cancelling every tone) are normalised by energy / 100, as in
+    test_large_stream_hop256."""
+    H, freqs, W, amplitude, sigma = draw(i)
+    n, hop = 1024, 64 * H
+    src = (W - 1) * hop // n + 2
+    pcm, _ = O.synth_fsk(freqs, n, src, 77 + i, amplitude, sigma)
+    flat = pcm.reshape(-1)
+    Wh = min(W, (flat.size - n) // hop + 1)
+    with A.Demodulator(n=n, hop=hop, freqs=freqs, method=GOERTZEL) as d:
+        sym, mag = d.batch(flat, n_windows=Wh, mags=True)
+    ref_sym, ref_P = O.goertzel(flat, freqs, n, hop, Wh)
+    xw = np.lib.stride_tricks.sliding_window_view(flat.astype(np.float64), n)[::hop][:Wh]
+    energy = n * (xw * xw).sum(axis=1) / 2
+    denom = np.maximum(np.maximum(ref_P.max(axis=1), energy / 100), 1e-30)
+    assert (np.abs(mag.astype(np.float64) - ref_P).max(axis=1) / denom).max() <= MAG_TOL
+    check_decisions(sym, mag, ref_sym, ref_P, denom)
+
+
+@pytest.mark.parametrize("hop,channels", [(256, 1), (128, 2), (64, 1), (960, 2)])
+def test_streaming_demodulate(A, O, torch, hop, channels):
+    """demodulate() over ragged packets (carry buffer across calls) with the
+    segment-shared bank: the same symbols as the oracle's stream."""
+    n = 1024
+    L, _ = O.synth_fsk(A.FSK2_FREQS, n, 40, 900 + hop)
+    R, _ = O.synth_fsk(A.FSK2_FREQS, n, 40, 901 + hop)
+    mono = L.reshape(-1)
+    stream = mono if channels == 1 else np.stack([mono, R.reshape(-1)], axis=1).reshape(-1)
+    ref = O.Stream(A.FSK2_FREQS, n=n, hop=hop, channels=channels)
+    sizes = [2880, 100, 1, 4097, 2880, 64, 7000]
+    got, want = [], []
+    with A.Demodulator(A.make_cfg(freqs=A.FSK2_FREQS, hop=hop, channels=channels,
+                                  method=GOERTZEL)) as d:
+        pos, i = 0, 0
+        while pos < mono.size:
+            fr = sizes[i % len(sizes)]
+            i += 1
+            chunk = stream[pos * channels:(pos + fr) * channels]
+            pos += fr
+            got.append(d.demodulate(chunk))
+            want.append(ref.push(chunk)[0])
+            assert d.pending() == ref.pending()
+    got, want = np.concatenate(got), np.concatenate(want)
+    assert got.size == want.size == (40 * n - n) // hop + 1
+    assert (got == want).all()
