@@ -141,6 +141,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "demod_pending": (ctypes.c_int, [_P]),
         "demod_method": (ctypes.c_int, [_P]),
         "demod_max_symbols": (ctypes.c_int, [_P, _SZ]),
+        "demod_batch_launches": (ctypes.c_int, [_P, _SZ, ctypes.c_int]),
         "demodulate": (ctypes.c_int, [_P, _P, _SZ, _P, _SZ]),
         "demodulate_mags": (ctypes.c_int, [_P, _P, _SZ, _P, _P, _SZ]),
         "demod_batch": (ctypes.c_int, [_P, _P, _SZ, _P, _P]),
@@ -317,6 +318,10 @@ class Demodulator:
 
     def max_symbols(self, n_frames: int) -> int:
         return int(self._lib.demod_max_symbols(self._h, n_frames))
+
+    def batch_launches(self, n_windows: int, mags: bool = True) -> int:
+        """Kernel launches one batch of n_windows makes (demod_batch_launches)."""
+        return int(self._lib.demod_batch_launches(self._h, n_windows, 1 if mags else 0))
 
     def demodulate(self, pcm: np.ndarray, mags: bool = False, max_symbols: Optional[int] = None):
         """Streaming demodulate(pcm, n): pcm is int16, interleaved if stereo."""

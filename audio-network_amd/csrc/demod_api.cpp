@@ -423,6 +423,36 @@ static size_t windows_for(const demod_t *st, size_t total)
     return (total - st->cfg.n) / st->cfg.hop + 1;
 }
 
+constexpr size_t kOutChunkBytes = 10u << 20;  // symbol + magnitude bytes per detector launch
+
+// Windows per launch of a Goertzel-family batch (enqueue_batch): outputs
+// beyond ~1 MiB per XCD L2 are written back to HBM while the input still
+// streams in, and the read / write turnarounds cost ~1.3 us per MiB (8-FSK:
+// 336.6 us with magnitudes vs 295.3 without); up to that size they stay dirty
+// in L2 and go out in one burst at the kernel's end (2-FSK's 9 MiB: +1 us).
+// So batches whose outputs exceed kOutChunkBytes run as equal slices of
+// 64-window multiples (8-FSK: 4 launches, 322-325 us;
+// scripts/split_launch_probe.py).
+static size_t launch_slice(const demod_t *st, size_t n_windows, bool mags)
+{
+    if (st->detector == kDetFft || n_windows == 0) return n_windows;
+    const size_t out_per_window = 1 + (mags ? 4 * (size_t)st->cfg.k : 0);
+    const size_t parts = std::min<size_t>(
+        (n_windows * out_per_window + kOutChunkBytes - 1) / kOutChunkBytes, 16);
+    if (parts <= 1) return n_windows;
+    const size_t per = (n_windows + parts - 1) / parts;
+    return (per + 63) / 64 * 64;
+}
+
+int demod_batch_launches(const demod_t *st, size_t n_windows, int with_mags)
+{
+    if (!st) return DEMOD_BAD_ARG;
+    if (n_windows == 0) return 0;
+    const size_t per = launch_slice(st, n_windows, with_mags != 0);
+    const size_t n = (n_windows + per - 1) / per;
+    return n > 0x7FFFFFFF ? 0x7FFFFFFF : (int)n;
+}
+
 int demod_max_symbols(const demod_t *st, size_t n_frames)
 {
     if (!st) return DEMOD_BAD_ARG;
@@ -451,6 +481,7 @@ static int enqueue_fft(demod_t *st, const int16_t *d_pcm, size_t n_windows, uint
     HIP_TRY(launch_fft_quad(p, s));
     return (int)n_windows;
 }
+
 
 // Enqueue the detector kernel on device-resident windows.
 static int enqueue_batch(demod_t *st, const int16_t *d_pcm, size_t n_windows, uint8_t *d_sym,
@@ -485,7 +516,15 @@ static int enqueue_batch(demod_t *st, const int16_t *d_pcm, size_t n_windows, ui
     // same line (2-FSK: 0.325 -> 0.305 ms), and overlapping
     // windows find their shared lines there
     p.xcd_swizzle = 1;
-    HIP_TRY(launch_detector(st->detector, p, s));
+    const size_t per = launch_slice(st, n_windows, d_mag != nullptr);
+    for (size_t w0 = 0; w0 < n_windows; w0 += per) {
+        const size_t cnt = std::min(per, n_windows - w0);
+        p.pcm = d_pcm + w0 * st->cfg.hop;
+        p.n_windows = (long long)cnt;
+        p.sym = d_sym + w0;
+        p.mag = d_mag ? d_mag + w0 * st->cfg.k : nullptr;
+        HIP_TRY(launch_detector(st->detector, p, s));
+    }
     return (int)n_windows;
 }
 

@@ -440,6 +440,9 @@ def run_config(A, D, torch, dist, args, config, rank, world, local, use_dist, st
             framed = {"frames_bytes": len(stream_bytes), "bits_per_symbol": A.bits_per_symbol(K),
                       "roundtrip_ok": bool((back == all_sym.cpu().numpy()).all())}
 
+    # dispatches per step: batches with > ~10 MiB of output run as slices
+    # (demod_batch_launches); kernel_ms brackets the whole batch
+    launches = demod.batch_launches(n_eval, not no_mags)
     alg_bytes = W * 2 * n + n_eval * (1 + (0 if no_mags else 4 * K))
     achieved = alg_bytes / (kernel_ms / 1e3) / 1e9
     kname = ("fft1024_quad_kernel<4>" if demod.method == A.METHOD_FFT else
@@ -468,6 +471,7 @@ def run_config(A, D, torch, dist, args, config, rank, world, local, use_dist, st
             "read_ceiling": round(ceil_gbps, 1) if ceil_gbps else None,
             "frac_of_read_ceiling": round(achieved / ceil_gbps, 4) if ceil_gbps else None,
             "kernel": kname,
+            "launches_per_step": launches,
         },
         "d_pcm": d_pcm, "d_sym": d_sym, "d_mag": d_mag, "cfg": cfg,
     }
@@ -503,7 +507,8 @@ def summary(r) -> dict:
            "kernel_ms": round(r["kernel_ms"], 4),
            "kernel_ms_p10_p50_p90": [round(float(np.percentile(r["kts"], q)), 4) for q in (10, 50, 90)],
            "value": round(r["W"] * 1024 / (r["ms_per_step"] / 1e3) / 1e6, 1), "unit": "Msamples/s",
-           "symbol_errors": r["sym_err"]}
+           "symbol_errors": r["sym_err"],
+           "launches_per_step": r["roofline"]["launches_per_step"]}
     if r["config"] == "fft":
         out["roofline"] = r["roofline_valu"]
         out["roofline_hbm_frac"] = round(

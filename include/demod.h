@@ -121,6 +121,13 @@ int demod_pending(const demod_t *st);
 /* Upper bound on symbols the next demodulate(st, ., n_frames, ...) emits. */
 int demod_max_symbols(const demod_t *st, size_t n_frames);
 
+/* Kernel launches one demod_batch / demod_batch_async of n_windows makes
+ * (with_mags: magnitudes requested). Goertzel-family batches whose symbol +
+ * magnitude output exceeds ~10 MiB run as equal slices, so each launch's
+ * output is written back from L2 in a burst instead of interleaved with the
+ * input stream; profilers see that many dispatches. */
+int demod_batch_launches(const demod_t *st, size_t n_windows, int with_mags);
+
 /*
  * Streaming entry point: demodulate(pcm, n) -> symbols.
  * pcm: host pointer to n_frames frames of `channels` interleaved int16

@@ -25,3 +25,7 @@ for off_mb in (0, 1, 3, 16, 37):
 run(None, "no mags")
 sep = torch.empty((W, 8), dtype=torch.float32, device="cuda")
 run(sep, "mags separate alloc")
+run(d_mag_first := sep, "mags separate alloc (again)")
+for rep in range(3):
+    other = torch.empty((W, 8), dtype=torch.float32, device="cuda")
+    run(other, f"mags fresh alloc {rep}")

@@ -118,3 +118,12 @@ def test_device_tensor_checks(A):
     with pytest.raises(A.DemodError):
         A.frame_streams_async(torch.zeros(10, dtype=torch.uint8), 2, 5, 1,
                               torch.zeros(1, dtype=torch.uint8))
+
+
+def test_batch_launches_matches_the_split_rule(A):
+    """demod_batch_launches without a GPU is only reachable through a handle,
+    which needs a device; the rule itself is checked on the GPU
+    (test_gpu_parity.py::test_batch_launch_slices) - here: the export exists
+    and rejects a NULL handle."""
+    lib = A.load_library()
+    assert lib.demod_batch_launches(None, 10, 1) == A.DEMOD_BAD_ARG

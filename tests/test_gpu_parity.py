@@ -666,3 +666,33 @@ def test_device_framing_matches_host_codec(A, torch, n_streams, n, bits, max_pay
                 back.append(A.unpack_symbols(payload, cnt, bits))
                 got_n += cnt
             assert np.array_equal(np.concatenate(back), sym[s] & mask)
+
+
+def test_batch_launch_slices(A, O, torch):
+    """Batches whose symbol + magnitude output exceeds ~10 MiB run as several
+    launches (demod_batch_launches); the slices must give the same symbols and
+    powers as one launch over the same windows (smaller batches below the
+    threshold), including a window count that is not a multiple of the slice."""
+    n, W = 1024, (1 << 20) + 77
+    f = A.FSK8_FREQS
+    cfg = A.make_cfg(n=n, freqs=f)
+    d_pcm = torch.empty((W, n), dtype=torch.int16, device="cuda")
+    A.synth_fsk(cfg, 99, W, 8000, 400, d_pcm)
+    sym = torch.empty(W, dtype=torch.uint8, device="cuda")
+    mag = torch.empty((W, 8), dtype=torch.float32, device="cuda")
+    with A.Demodulator(cfg) as d:
+        assert d.batch_launches(W, mags=True) == 4
+        assert d.batch_launches(W, mags=False) == 1
+        assert d.batch_launches(1 << 18, mags=True) == 1
+        d.batch_device(d_pcm, W, sym, mag)
+        ref_sym = torch.empty_like(sym)
+        ref_mag = torch.empty_like(mag)
+        step = 1 << 18                       # below the threshold: one launch each
+        for w0 in range(0, W, step):
+            c = min(step, W - w0)
+            d.batch_device(d_pcm[w0:w0 + c], c, ref_sym[w0:w0 + c], ref_mag[w0:w0 + c])
+    torch.cuda.synchronize()
+    assert torch.equal(sym, ref_sym)
+    assert torch.equal(mag.view(torch.int32), ref_mag.view(torch.int32))
+    with A.Demodulator(freqs=A.FSK2_FREQS) as d:
+        assert d.batch_launches(1 << 20, mags=True) == 1    # 9 MiB: stays one launch
