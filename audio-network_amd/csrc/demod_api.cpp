@@ -432,10 +432,13 @@ constexpr size_t kOutChunkBytes = 10u << 20;  // symbol + magnitude bytes per de
 // in L2 and go out in one burst at the kernel's end (2-FSK's 9 MiB: +1 us).
 // So batches whose outputs exceed kOutChunkBytes run as equal slices of
 // 64-window multiples (8-FSK: 4 launches, 322-325 us;
-// scripts/split_launch_probe.py).
+// scripts/split_launch_probe.py). Overlapping windows
+// (hop < n) are bound by the recurrences and L2, not by HBM turnarounds, and
+// only pay the extra launches there (2-FSK hop 128: 0.466 -> 0.494 ms), so
+// they stay one launch, as does the VALU-bound FFT detector.
 static size_t launch_slice(const demod_t *st, size_t n_windows, bool mags)
 {
-    if (st->detector == kDetFft || n_windows == 0) return n_windows;
+    if (st->detector == kDetFft || st->cfg.hop < st->cfg.n || n_windows == 0) return n_windows;
     const size_t out_per_window = 1 + (mags ? 4 * (size_t)st->cfg.k : 0);
     const size_t parts = std::min<size_t>(
         (n_windows * out_per_window + kOutChunkBytes - 1) / kOutChunkBytes, 16);
