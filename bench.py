@@ -43,6 +43,10 @@ HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 VALU_PEAK_TFLOPS = 157.3  # MI355X fp32 vector peak (MI355X_MICROARCH.md)
 METRIC = "PCM Msamples/s demodulated + symbol-error-rate vs reference, 1/2/4/8 MI355X"
 MIN_WARMUP = 64
+# HIP event pairs on every EV_EVERY-th timed step only: a pair on every step
+# adds an ~8 us bubble per 0.3 ms step (scripts/step_gap_probe.py: 310.9 vs
+# 302.8 us per step), which ms_per_step would carry
+EV_EVERY = 4
 MARGIN_BAND = 4e-5  # 4 x the 1e-5 magnitude bar: decisions closer than this are fp32-ill-posed
 
 
@@ -322,8 +326,9 @@ def run_config(A, D, torch, dist, args, config, rank, world, local, use_dist, st
     for _ in range(warm):
         step()
     flush()
-    evs = [mk(3) for _ in range(steps)]
-    gevs = [mk(2) for _ in range(steps)] if use_dist else None
+    timed = [i % EV_EVERY == 0 for i in range(steps)]
+    evs = [mk(3) if timed[i] else None for i in range(steps)]
+    gevs = [mk(2) if timed[i] else None for i in range(steps)] if use_dist else None
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -340,11 +345,13 @@ def run_config(A, D, torch, dist, args, config, rank, world, local, use_dist, st
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    evs = [e for e in evs if e is not None]
     kts = np.array([a.elapsed_time(b) for a, b, _ in evs])
     kernel_ms = float(kts.mean())
     ms_per_step = elapsed / steps * 1e3
     frame_ms = (float(np.mean([b.elapsed_time(c) for _, b, c in evs])) if dev_framing else None)
-    gather_ms = (float(np.mean([a.elapsed_time(b) for a, b in gevs])) if gevs else None)
+    gdone_evs = [e for e in (gevs or []) if e is not None]
+    gather_ms = (float(np.mean([a.elapsed_time(b) for a, b in gdone_evs])) if gdone_evs else None)
     ms_per_step_eager = None
     if use_dist and dev_framing and getattr(args, "graph", False) and args.dist_backend == "nccl":
         # HIP graph of one step: the detector kernel on a
@@ -636,6 +643,7 @@ def main():
             "symbol_errors": r["sym_err"],
             "symbol_error_rate": r["sym_err"] / float(r["total_windows"]),
             "kernel_ms": round(r["kernel_ms"], 4),
+            "kernel_ms_steps": f"HIP events on every {EV_EVERY}th timed step ({len(r['kts'])})",
             "roofline": r["roofline"],
         }
         if "roofline_valu" in r:
