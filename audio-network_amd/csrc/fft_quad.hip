@@ -384,19 +384,71 @@ __device__ __forceinline__ void dft4_geo_v(f2 *x, f2 w, f2 w2)
     x[3 * S] = X3;
 }
 
+// The same two butterfly stages as ONE asm block (12 packed FMAs): every
+// result is read two or more instructions after it is written, so the block
+// needs none of the packed-write s_nops the two separate blocks cost at their
+// seam (the second block's first pairs read the first block's last results).
+// Operands: %0-%3 X0..X3 (out), %4-%7 a0 a1 c0 c1 (scratch), %8-%11 x0..x3,
+// %12 w (second stage; the -j w pair by modifiers), %13 w^2 (first stage),
+// %14 (2, 2).
+#define QF_STAGES(WA, WB, TMB, UMB)                                                        \
+    QTB_T("%4", "%10", WA, "%8") QTB_T("%6", "%11", WA, "%9")                              \
+    QTB_U("%4", "%10", WA) QTB_U("%6", "%11", WA)                                          \
+    QTB_V("%5", "%8", "%14", "%4") "\n\t" QTB_V("%7", "%9", "%14", "%6") "\n\t"         \
+    QTB_T("%0", "%6", WB, "%4") TMB("%1", "%7", WB, "%5")                                   \
+    QTB_U("%0", "%6", WB) UMB("%1", "%7", WB)                                               \
+    QTB_V("%2", "%4", "%14", "%0") "\n\t" QTB_V("%3", "%5", "%14", "%1")
+template <int S>
+__device__ __forceinline__ void dft4_fused_v(f2 *x, f2 w, f2 w2)
+{
+    f2 X0, X1, X2, X3, a0, a1, c0, c1;
+    asm(QF_STAGES("%13", "%12", QTB_TM, QTB_UM)
+        : "=&v"(X0), "=&v"(X1), "=&v"(X2), "=&v"(X3), "=&v"(a0), "=&v"(a1), "=&v"(c0), "=&v"(c1)
+        : "v"(x[0]), "v"(x[S]), "v"(x[2 * S]), "v"(x[3 * S]), "v"(w), "v"(w2),
+          "s"((f2){2.0f, 2.0f}));
+    x[0] = X0;
+    x[S] = X1;
+    x[2 * S] = X2;
+    x[3 * S] = X3;
+}
+
+// dft4_geo_k<E, S> as one block when neither w^2 = W32^{2E} nor w is a
+// quarter turn: first stage both pairs with w^2, second stage w and -j w =
+// W32^{E+8}, all SGPR constants (%12 w, %13 w^2, %15 -j w).
+#define QF_STAGES_K                                                                         \
+    QTB_T("%4", "%10", "%13", "%8") QTB_T("%6", "%11", "%13", "%9")                        \
+    QTB_U("%4", "%10", "%13") QTB_U("%6", "%11", "%13")                                    \
+    QTB_V("%5", "%8", "%14", "%4") "\n\t" QTB_V("%7", "%9", "%14", "%6") "\n\t"         \
+    QTB_T("%0", "%6", "%12", "%4") QTB_T("%1", "%7", "%15", "%5")                           \
+    QTB_U("%0", "%6", "%12") QTB_U("%1", "%7", "%15")                                       \
+    QTB_V("%2", "%4", "%14", "%0") "\n\t" QTB_V("%3", "%5", "%14", "%1")
+template <int E, int S>
+__device__ __forceinline__ void dft4_fused_k(f2 *x)
+{
+    f2 X0, X1, X2, X3, a0, a1, c0, c1;
+    asm(QF_STAGES_K
+        : "=&v"(X0), "=&v"(X1), "=&v"(X2), "=&v"(X3), "=&v"(a0), "=&v"(a1), "=&v"(c0), "=&v"(c1)
+        : "v"(x[0]), "v"(x[S]), "v"(x[2 * S]), "v"(x[3 * S]), "s"(w32c<E>()), "s"(w32c<2 * E>()),
+          "s"((f2){2.0f, 2.0f}), "s"(w32c<E + 8>()));
+    x[0] = X0;
+    x[S] = X1;
+    x[2 * S] = X2;
+    x[3 * S] = X3;
+}
+
 // In-register DFT of x[0], x[S], .., x[(N-1) S] (N = 4, 8, 16, 32), natural
 // order out, every twiddle fused into the butterfly that consumes it.
 // Mixed radix N = N1 x N2 (N2 = 4, or 2 at N = 8): DFT-N1 over i1 for each i2,
 // then per k1 a DFT-N2 over i2 of the twiddled column, which is geometric in
 // w = W_N^{k1} (dft4_geo_k).
-template <int N, int S = 1>
+template <int N, int S = 1, bool F = false>
 __device__ __forceinline__ void dftf(f2 *x)
 {
     if constexpr (N == 4) {
         dft4_geo_k<0, S>(x);
     } else if constexpr (N == 8) {
-        dftf<4, 2 * S>(x);       // i2 = 0: X[k1] at slot 2 k1
-        dftf<4, 2 * S>(x + S);   // i2 = 1: X[k1] at slot 2 k1 + 1
+        dftf<4, 2 * S, F>(x);       // i2 = 0: X[k1] at slot 2 k1
+        dftf<4, 2 * S, F>(x + S);   // i2 = 1: X[k1] at slot 2 k1 + 1
         // per k1: (slot 2k1, slot 2k1+1) -> X[k1], X[k1 + 4], twiddle W8^k1 = W32^{4 k1}
         f2 u0, v0, u1, v1, u2, v2, u3, v3;
         tb_triv<0>(u0, v0, x[0], x[S]);
@@ -408,11 +460,15 @@ __device__ __forceinline__ void dftf(f2 *x)
         constexpr int N1 = N / 4;   // 8 (N = 32) or 4 (N = 16)
         static_for<0, 4>([&](auto c) {
             constexpr int i2 = decltype(c)::value;
-            dftf<N1, 4 * S>(x + i2 * S);   // X[k1] of column i2 at slot i2 + 4 k1
+            dftf<N1, 4 * S, F>(x + i2 * S);   // X[k1] of column i2 at slot i2 + 4 k1
         });
         static_for<0, N1>([&](auto d) {
             constexpr int k1 = decltype(d)::value;
-            dft4_geo_k<k1 * (32 / N), S>(x + 4 * k1 * S);   // slot 4 k1 + k2 = X[k1 + N1 k2]
+            constexpr int E = k1 * (32 / N);
+            if constexpr (F && !w32_trivial(E) && !w32_trivial(2 * E))
+                dft4_fused_k<E, S>(x + 4 * k1 * S);
+            else
+                dft4_geo_k<E, S>(x + 4 * k1 * S);   // slot 4 k1 + k2 = X[k1 + N1 k2]
         });
         f2 t[N];
         static_for<0, N>([&](auto e) {
@@ -441,6 +497,36 @@ __device__ __forceinline__ f2 pp_im_h(f2 S, f2 T)
     asm("v_pk_fma_f32 %0, %1, %3, %2 op_sel:[1,0,1] neg_hi:[0,0,1]"
         : "=v"(r) : "v"(S), "v"(T), "s"((f2){0.5f, 0.5f}));
     return r;
+}
+
+// Two mirror pairs of the real post-pass as one block (16 packed ops):
+// S = P + conj Q, D = -i (P - conj Q), T = D (W / 2), (re, im) of X[kP] and
+// X[512 - kP] side by side, powers (|X[kP]|^2, |X[512 - kP]|^2). Interleaved
+// so every result is read two instructions after it is written.
+// Operands: %0 %1 pw0 pw1 (out), %2-%9 scratch S0 S1 D0 D1 T0 T1 R0 R1,
+// %10 P0, %11 Q0, %12 W0, %13 P1, %14 Q1, %15 W1, %16 (1/2, 1/2).
+__device__ __forceinline__ void postpair2(f2 &pw0, f2 P0, f2 Q0, f2 W0, f2 &pw1, f2 P1, f2 Q1, f2 W1)
+{
+    f2 S0, S1, D0, D1, T0, T1, R0, R1;
+    asm("v_pk_add_f32 %2, %10, %11 neg_hi:[0,1]\n\t"
+        "v_pk_add_f32 %3, %13, %14 neg_hi:[0,1]\n\t"
+        "v_pk_add_f32 %4, %10, %11 op_sel:[1,1] op_sel_hi:[0,0] neg_hi:[1,0]\n\t"
+        "v_pk_add_f32 %5, %13, %14 op_sel:[1,1] op_sel_hi:[0,0] neg_hi:[1,0]\n\t"
+        "v_pk_mul_f32 %6, %4, %12 op_sel:[1,1] op_sel_hi:[1,0]\n\t"
+        "v_pk_mul_f32 %7, %5, %15 op_sel:[1,1] op_sel_hi:[1,0]\n\t"
+        "v_pk_fma_f32 %6, %4, %12, %6 op_sel_hi:[0,1,1] neg_lo:[0,0,1]\n\t"
+        "v_pk_fma_f32 %7, %5, %15, %7 op_sel_hi:[0,1,1] neg_lo:[0,0,1]\n\t"
+        "v_pk_fma_f32 %8, %2, %16, %6 op_sel_hi:[0,1,0] neg_hi:[0,0,1]\n\t"
+        "v_pk_fma_f32 %9, %3, %16, %7 op_sel_hi:[0,1,0] neg_hi:[0,0,1]\n\t"
+        "v_pk_fma_f32 %4, %2, %16, %6 op_sel:[1,0,1] neg_hi:[0,0,1]\n\t"
+        "v_pk_fma_f32 %5, %3, %16, %7 op_sel:[1,0,1] neg_hi:[0,0,1]\n\t"
+        "v_pk_mul_f32 %6, %4, %4\n\t"
+        "v_pk_mul_f32 %7, %5, %5\n\t"
+        "v_pk_fma_f32 %0, %8, %8, %6\n\t"
+        "v_pk_fma_f32 %1, %9, %9, %7"
+        : "=&v"(pw0), "=&v"(pw1), "=&v"(S0), "=&v"(S1), "=&v"(D0), "=&v"(D1), "=&v"(T0), "=&v"(T1),
+          "=&v"(R0), "=&v"(R1)
+        : "v"(P0), "v"(Q0), "v"(W0), "v"(P1), "v"(Q1), "v"(W1), "s"((f2){0.5f, 0.5f}));
 }
 
 }  // namespace quad
@@ -508,10 +594,14 @@ constexpr int kFmtWord3 = 0xFAC | (3 << 12) | (5 << 15);
 // index: s_set_gpr_idx) instead of going through the 2 KiB per-window power
 // slab in LDS; true = the slab, for the full-spectrum store.
 // AUX: the loads' cache-policy bits (2 = nt, 1 = sc0, 0 = plain; launch_fft_quad).
+// FUSED: 1 = each DFT-4's two butterfly stages as one asm block
+// (dft4_fused_v / _k), 2 = also the post-pass pairs (postpair2); the
+// separate blocks cost an s_nop and a scheduling barrier at every seam.
 // FMT (PF = 0 only): typed buffer loads (16_16 SSCALED) convert both int16
 // halves to fp32 in the texture path instead of 64 VALU converts per group
 // (measured neutral).
-template <int WPB = 4, int MINW = 4, int PF = 0, bool SPEC = true, bool FMT = false, int AUX = 2>
+template <int WPB = 4, int MINW = 4, int PF = 0, bool SPEC = true, bool FMT = false, int AUX = 2,
+          int FUSED = 0>
 __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MINW > 0 ? MINW : 1)))
 void fft1024_quad_kernel(FftParams p)
 {
@@ -594,7 +684,7 @@ void fft1024_quad_kernel(FftParams p)
         }
 
         // 1. DFT-32 over n1 (fused twiddles), no stage-1 twiddle here
-        dftf<32>(a);
+        dftf<32, 1, (FUSED >= 1)>(a);
 
         // 2. transpose in two column rounds; lane (q, t') gets columns
         //    k1 = t' (round 0) and k1b (round 1) of its window
@@ -622,11 +712,17 @@ void fft1024_quad_kernel(FftParams p)
             const f2 v = twv(sl, 0), v2 = twv(sl, 1);
             static_for<0, 4>([&](auto c) {
                 constexpr int i2 = decltype(c)::value;
-                dft4_geo_v<4>(bb + i2, v, v2);   // column i2's X[k1] at slot i2 + 4 k1
+                if constexpr (FUSED >= 1)
+                    dft4_fused_v<4>(bb + i2, v, v2);
+                else
+                    dft4_geo_v<4>(bb + i2, v, v2);   // column i2's X[k1] at slot i2 + 4 k1
             });
             static_for<0, 4>([&](auto d) {
                 constexpr int k1 = decltype(d)::value;
-                dft4_geo_v<1>(bb + 4 * k1, twv(sl, 2 + 2 * k1), twv(sl, 3 + 2 * k1));
+                if constexpr (FUSED >= 1)
+                    dft4_fused_v<1>(bb + 4 * k1, twv(sl, 2 + 2 * k1), twv(sl, 3 + 2 * k1));
+                else
+                    dft4_geo_v<1>(bb + 4 * k1, twv(sl, 2 + 2 * k1), twv(sl, 3 + 2 * k1));
             });
             f2 tt[16];
             static_for<0, 16>([&](auto e) {
@@ -665,13 +761,17 @@ void fft1024_quad_kernel(FftParams p)
                 Q1 = sel_l0(b[16 - j1], Q1);
             }
             f2 pw0, pw1;  // (|X[kP]|^2, |X[512-kP]|^2)
-            const f2 S0 = pp_s(P0, Q0), S1 = pp_s(P1, Q1);
-            const f2 D0 = pp_d(P0, Q0), D1 = pp_d(P1, Q1);
-            f2 T0, T1;
-            cmul2(T0, D0, tw3[16 * j0 + t], T1, D1, tw3[16 * j1 + t]);
-            const f2 re0 = pp_re_h(S0, T0), re1 = pp_re_h(S1, T1);
-            const f2 im0 = pp_im_h(S0, T0), im1 = pp_im_h(S1, T1);
-            pwr2(pw0, re0, im0, pw1, re1, im1);
+            if constexpr (FUSED >= 2) {
+                postpair2(pw0, P0, Q0, tw3[16 * j0 + t], pw1, P1, Q1, tw3[16 * j1 + t]);
+            } else {
+                const f2 S0 = pp_s(P0, Q0), S1 = pp_s(P1, Q1);
+                const f2 D0 = pp_d(P0, Q0), D1 = pp_d(P1, Q1);
+                f2 T0, T1;
+                cmul2(T0, D0, tw3[16 * j0 + t], T1, D1, tw3[16 * j1 + t]);
+                const f2 re0 = pp_re_h(S0, T0), re1 = pp_re_h(S1, T1);
+                const f2 im0 = pp_im_h(S0, T0), im1 = pp_im_h(S1, T1);
+                pwr2(pw0, re0, im0, pw1, re1, im1);
+            }
             if constexpr (SPEC) {
                 ps[16 * j0] = pw0;
                 ps[16 * j1] = pw1;
@@ -736,13 +836,13 @@ void fft1024_quad_kernel(FftParams p)
 
 // Persistent grid: as many blocks as fit the chip, each wave strides over
 // groups of 4 windows (the LDS twiddle tables are built once per block).
-template <int WPB, int MINW, int PF, bool SPEC, bool FMT = false, int AUX = 2>
+template <int WPB, int MINW, int PF, bool SPEC, bool FMT = false, int AUX = 2, int FUSED = 0>
 hipError_t launch_fft_quad_t(const FftParams &p, hipStream_t s)
 {
     int dev = 0, cus = 256, per_cu = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fft1024_quad_kernel<WPB, MINW, PF, SPEC, FMT, AUX>,
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fft1024_quad_kernel<WPB, MINW, PF, SPEC, FMT, AUX, FUSED>,
                                                      64 * WPB, 0) != hipSuccess ||
         per_cu < 1)
         per_cu = 1;
@@ -750,7 +850,7 @@ hipError_t launch_fft_quad_t(const FftParams &p, hipStream_t s)
     long long blocks = (groups + WPB - 1) / WPB;
     blocks = std::min<long long>(blocks, (long long)cus * per_cu);
     if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL((fft1024_quad_kernel<WPB, MINW, PF, SPEC, FMT, AUX>), dim3((unsigned)blocks), dim3(64 * WPB),
+    hipLaunchKernelGGL((fft1024_quad_kernel<WPB, MINW, PF, SPEC, FMT, AUX, FUSED>), dim3((unsigned)blocks), dim3(64 * WPB),
                        0, s, p);
     return hipGetLastError();
 }
@@ -762,13 +862,15 @@ hipError_t launch_fft_quad_t(const FftParams &p, hipStream_t s)
 // lines in L2 (plain cached loads, AUX 0: FETCH 1.06x the stream at hop 256,
 // 3-6 % faster; sc0 measured the same or slower); disjoint windows stream
 // through with nt (AUX 2; nt at hop 256 re-fetches 1.55x the stream).
+// FUSED 2: the DFT-4 stages and the post-pass pairs as single asm blocks
+// (-1.5 to -2.6 % at hop 256, -1 % at hop 1024 against separate blocks).
 hipError_t launch_fft_quad(const FftParams &p, hipStream_t s)
 {
     if (p.hop < 1024)
-        return p.spec ? launch_fft_quad_t<4, 4, 0, true, false, 0>(p, s)
-                      : launch_fft_quad_t<4, 4, 0, false, false, 0>(p, s);
-    return p.spec ? launch_fft_quad_t<4, 4, 0, true, false, 2>(p, s)
-                  : launch_fft_quad_t<4, 4, 0, false, false, 2>(p, s);
+        return p.spec ? launch_fft_quad_t<4, 4, 0, true, false, 0, 2>(p, s)
+                      : launch_fft_quad_t<4, 4, 0, false, false, 0, 2>(p, s);
+    return p.spec ? launch_fft_quad_t<4, 4, 0, true, false, 2, 2>(p, s)
+                  : launch_fft_quad_t<4, 4, 0, false, false, 2, 2>(p, s);
 }
 
 int fft_quad_slot(int bin) { return quad_slot(bin); }
