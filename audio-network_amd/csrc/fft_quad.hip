@@ -436,20 +436,90 @@ __device__ __forceinline__ void dft4_fused_k(f2 *x)
     x[3 * S] = X3;
 }
 
+// FUSED 3: the trivial-twiddle pieces of the DFT-32 as single blocks too.
+// x + (-j) y and x - (-j) y as instruction text (add_mj / sub_mj)
+#define QA_MJ(R, X, Y) "v_pk_add_f32 " R ", " X ", " Y " op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]\n\t"
+#define QS_MJ(R, X, Y) "v_pk_add_f32 " R ", " X ", " Y " op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]\n\t"
+#define QADD(R, X, Y) "v_pk_add_f32 " R ", " X ", " Y "\n\t"
+#define QSUB(R, X, Y) "v_pk_add_f32 " R ", " X ", " Y " neg_lo:[0,1] neg_hi:[0,1]\n\t"
+// DFT-4 with no twiddles (dft4_geo_k<0>): 8 packed adds.
+// %0-%3 X0..X3, %4-%7 a0 a1 c0 c1, %8-%11 x0..x3
+template <int S>
+__device__ __forceinline__ void dft4_triv(f2 *x)
+{
+    f2 X0, X1, X2, X3, a0, a1, c0, c1;
+    asm(QADD("%4", "%8", "%10") QSUB("%5", "%8", "%10") QADD("%6", "%9", "%11") QSUB("%7", "%9", "%11")
+        QADD("%0", "%4", "%6") QSUB("%2", "%4", "%6") QA_MJ("%1", "%5", "%7")
+        "v_pk_add_f32 %3, %5, %7 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]"
+        : "=&v"(X0), "=&v"(X1), "=&v"(X2), "=&v"(X3), "=&v"(a0), "=&v"(a1), "=&v"(c0), "=&v"(c1)
+        : "v"(x[0]), "v"(x[S]), "v"(x[2 * S]), "v"(x[3 * S]));
+    x[0] = X0;
+    x[S] = X1;
+    x[2 * S] = X2;
+    x[3 * S] = X3;
+}
+// dft4_geo_k<E> with w^2 = -j (E = 4): first stage add_mj / sub_mj, second
+// stage w = W32^E and -j w = W32^{E+8} (%12, %13 SGPR pairs, %14 (2, 2)).
+template <int E, int S>
+__device__ __forceinline__ void dft4_fused_kq(f2 *x)
+{
+    static_assert(((2 * E) % 32 + 32) % 32 == 8, "w^2 = -j");
+    f2 X0, X1, X2, X3, a0, a1, c0, c1;
+    asm(QA_MJ("%4", "%8", "%10") QA_MJ("%6", "%9", "%11") QS_MJ("%5", "%8", "%10") QS_MJ("%7", "%9", "%11")
+        QTB_T("%0", "%6", "%12", "%4") QTB_T("%1", "%7", "%13", "%5")
+        QTB_U("%0", "%6", "%12") QTB_U("%1", "%7", "%13")
+        QTB_V("%2", "%4", "%14", "%0") "\n\t" QTB_V("%3", "%5", "%14", "%1")
+        : "=&v"(X0), "=&v"(X1), "=&v"(X2), "=&v"(X3), "=&v"(a0), "=&v"(a1), "=&v"(c0), "=&v"(c1)
+        : "v"(x[0]), "v"(x[S]), "v"(x[2 * S]), "v"(x[3 * S]), "s"(w32c<E>()), "s"(w32c<E + 8>()),
+          "s"((f2){2.0f, 2.0f}));
+    x[0] = X0;
+    x[S] = X1;
+    x[2 * S] = X2;
+    x[3 * S] = X3;
+}
+// The DFT-8's last stage (dftf<8>): pairs (slot 2k1, 2k1 + 1) with W8^k1:
+// k1 = 0 trivial, 2 is -j, 1 and 3 general (W32^4, W32^12), interleaved.
+// %0-%7 out slots 0..7 (u0 u1 u2 u3 v0 v1 v2 v3), %8-%15 in, %16 W32^4,
+// %17 W32^12, %18 (2, 2)
+template <int S>
+__device__ __forceinline__ void dft8_last(f2 *x)
+{
+    f2 u0, u1, u2, u3, v0, v1, v2, v3;
+    asm(QTB_T("%1", "%11", "%16", "%10") QTB_T("%3", "%15", "%17", "%14")
+        QADD("%0", "%8", "%9") QSUB("%4", "%8", "%9")
+        QTB_U("%1", "%11", "%16") QTB_U("%3", "%15", "%17")
+        QA_MJ("%2", "%12", "%13") QS_MJ("%6", "%12", "%13")
+        QTB_V("%5", "%10", "%18", "%1") "\n\t" QTB_V("%7", "%14", "%18", "%3")
+        : "=&v"(u0), "=&v"(u1), "=&v"(u2), "=&v"(u3), "=&v"(v0), "=&v"(v1), "=&v"(v2), "=&v"(v3)
+        : "v"(x[0]), "v"(x[S]), "v"(x[2 * S]), "v"(x[3 * S]), "v"(x[4 * S]), "v"(x[5 * S]),
+          "v"(x[6 * S]), "v"(x[7 * S]), "s"(w32c<4>()), "s"(w32c<12>()), "s"((f2){2.0f, 2.0f}));
+    x[0] = u0; x[S] = u1; x[2 * S] = u2; x[3 * S] = u3;
+    x[4 * S] = v0; x[5 * S] = v1; x[6 * S] = v2; x[7 * S] = v3;
+}
+
 // In-register DFT of x[0], x[S], .., x[(N-1) S] (N = 4, 8, 16, 32), natural
 // order out, every twiddle fused into the butterfly that consumes it.
 // Mixed radix N = N1 x N2 (N2 = 4, or 2 at N = 8): DFT-N1 over i1 for each i2,
 // then per k1 a DFT-N2 over i2 of the twiddled column, which is geometric in
 // w = W_N^{k1} (dft4_geo_k).
-template <int N, int S = 1, bool F = false>
+// L (FUSED level): >= 1 both-nontrivial DFT-4s as one block, >= 3 the
+// trivial pieces too.
+template <int N, int S = 1, int L = 0>
 __device__ __forceinline__ void dftf(f2 *x)
 {
     if constexpr (N == 4) {
-        dft4_geo_k<0, S>(x);
+        if constexpr (L >= 3)
+            dft4_triv<S>(x);
+        else
+            dft4_geo_k<0, S>(x);
     } else if constexpr (N == 8) {
-        dftf<4, 2 * S, F>(x);       // i2 = 0: X[k1] at slot 2 k1
-        dftf<4, 2 * S, F>(x + S);   // i2 = 1: X[k1] at slot 2 k1 + 1
+        dftf<4, 2 * S, L>(x);       // i2 = 0: X[k1] at slot 2 k1
+        dftf<4, 2 * S, L>(x + S);   // i2 = 1: X[k1] at slot 2 k1 + 1
         // per k1: (slot 2k1, slot 2k1+1) -> X[k1], X[k1 + 4], twiddle W8^k1 = W32^{4 k1}
+        if constexpr (L >= 3) {
+            dft8_last<S>(x);
+            return;
+        }
         f2 u0, v0, u1, v1, u2, v2, u3, v3;
         tb_triv<0>(u0, v0, x[0], x[S]);
         tb_triv<8>(u2, v2, x[4 * S], x[5 * S]);
@@ -460,13 +530,17 @@ __device__ __forceinline__ void dftf(f2 *x)
         constexpr int N1 = N / 4;   // 8 (N = 32) or 4 (N = 16)
         static_for<0, 4>([&](auto c) {
             constexpr int i2 = decltype(c)::value;
-            dftf<N1, 4 * S, F>(x + i2 * S);   // X[k1] of column i2 at slot i2 + 4 k1
+            dftf<N1, 4 * S, L>(x + i2 * S);   // X[k1] of column i2 at slot i2 + 4 k1
         });
         static_for<0, N1>([&](auto d) {
             constexpr int k1 = decltype(d)::value;
             constexpr int E = k1 * (32 / N);
-            if constexpr (F && !w32_trivial(E) && !w32_trivial(2 * E))
+            if constexpr (L >= 1 && !w32_trivial(E) && !w32_trivial(2 * E))
                 dft4_fused_k<E, S>(x + 4 * k1 * S);
+            else if constexpr (L >= 3 && ((E % 32) + 32) % 32 == 0)
+                dft4_triv<S>(x + 4 * k1 * S);
+            else if constexpr (L >= 3 && !w32_trivial(E) && ((2 * E) % 32 + 32) % 32 == 8)
+                dft4_fused_kq<E, S>(x + 4 * k1 * S);
             else
                 dft4_geo_k<E, S>(x + 4 * k1 * S);   // slot 4 k1 + k2 = X[k1 + N1 k2]
         });
@@ -595,8 +669,10 @@ constexpr int kFmtWord3 = 0xFAC | (3 << 12) | (5 << 15);
 // slab in LDS; true = the slab, for the full-spectrum store.
 // AUX: the loads' cache-policy bits (2 = nt, 1 = sc0, 0 = plain; launch_fft_quad).
 // FUSED: 1 = each DFT-4's two butterfly stages as one asm block
-// (dft4_fused_v / _k), 2 = also the post-pass pairs (postpair2); the
-// separate blocks cost an s_nop and a scheduling barrier at every seam.
+// (dft4_fused_v / _k), 2 = also the post-pass pairs (postpair2), 3 = also
+// the DFT-32's trivial-twiddle DFT-4s and DFT-8 stages (dft4_triv,
+// dft4_fused_kq, dft8_last); the separate blocks cost an s_nop and a
+// scheduling barrier at every seam.
 // FMT (PF = 0 only): typed buffer loads (16_16 SSCALED) convert both int16
 // halves to fp32 in the texture path instead of 64 VALU converts per group
 // (measured neutral).
@@ -684,7 +760,7 @@ void fft1024_quad_kernel(FftParams p)
         }
 
         // 1. DFT-32 over n1 (fused twiddles), no stage-1 twiddle here
-        dftf<32, 1, (FUSED >= 1)>(a);
+        dftf<32, 1, FUSED>(a);
 
         // 2. transpose in two column rounds; lane (q, t') gets columns
         //    k1 = t' (round 0) and k1b (round 1) of its window
@@ -862,15 +938,16 @@ hipError_t launch_fft_quad_t(const FftParams &p, hipStream_t s)
 // lines in L2 (plain cached loads, AUX 0: FETCH 1.06x the stream at hop 256,
 // 3-6 % faster; sc0 measured the same or slower); disjoint windows stream
 // through with nt (AUX 2; nt at hop 256 re-fetches 1.55x the stream).
-// FUSED 2: the DFT-4 stages and the post-pass pairs as single asm blocks
-// (-1.5 to -2.6 % at hop 256, -1 % at hop 1024 against separate blocks).
+// FUSED 3: the DFT-4 stages, the DFT-32's trivial pieces and the post-pass
+// pairs as single asm blocks (-2.5 to -4.5 % at hop 256, -1 to -2 % at hop
+// 1024 against separate blocks; scripts/fft_probe.hip).
 hipError_t launch_fft_quad(const FftParams &p, hipStream_t s)
 {
     if (p.hop < 1024)
-        return p.spec ? launch_fft_quad_t<4, 4, 0, true, false, 0, 2>(p, s)
-                      : launch_fft_quad_t<4, 4, 0, false, false, 0, 2>(p, s);
-    return p.spec ? launch_fft_quad_t<4, 4, 0, true, false, 2, 2>(p, s)
-                  : launch_fft_quad_t<4, 4, 0, false, false, 2, 2>(p, s);
+        return p.spec ? launch_fft_quad_t<4, 4, 0, true, false, 0, 3>(p, s)
+                      : launch_fft_quad_t<4, 4, 0, false, false, 0, 3>(p, s);
+    return p.spec ? launch_fft_quad_t<4, 4, 0, true, false, 2, 3>(p, s)
+                  : launch_fft_quad_t<4, 4, 0, false, false, 2, 3>(p, s);
 }
 
 int fft_quad_slot(int bin) { return quad_slot(bin); }
