@@ -412,6 +412,35 @@ __device__ __forceinline__ void dft4_fused_v(f2 *x, f2 w, f2 w2)
     x[3 * S] = X3;
 }
 
+// Two independent dft4_fused_v, interleaved instruction by instruction
+// (dependent results four instructions apart) and updated in place (the
+// first stage's inputs are dead once it has run): %0-%3 / %4-%7 the two
+// DFT-4s' x0..x3 (in / out), %8-%15 scratch a0 a1 c0 c1 of each, %16 / %17
+// w / w^2 of the first, %18 / %19 of the second, %20 (2, 2).
+template <int S>
+__device__ __forceinline__ void dft4x2_fused_v(f2 *xa, f2 *xb, f2 wa, f2 w2a, f2 wb, f2 w2b)
+{
+    f2 a0, a1, c0, c1, b0, b1, d0, d1;
+    asm(// first stage: a = x0 +- w^2 x2, c = x1 +- w^2 x3 (both DFT-4s)
+        QTB_T("%8", "%2", "%17", "%0") QTB_T("%10", "%3", "%17", "%1")
+        QTB_T("%12", "%6", "%19", "%4") QTB_T("%14", "%7", "%19", "%5")
+        QTB_U("%8", "%2", "%17") QTB_U("%10", "%3", "%17")
+        QTB_U("%12", "%6", "%19") QTB_U("%14", "%7", "%19")
+        QTB_V("%9", "%0", "%20", "%8") "\n\t" QTB_V("%11", "%1", "%20", "%10") "\n\t"
+        QTB_V("%13", "%4", "%20", "%12") "\n\t" QTB_V("%15", "%5", "%20", "%14") "\n\t"
+        // second stage into x: X0/X2 = a0 +- w c0, X1/X3 = a1 +- (-j w) c1
+        QTB_T("%0", "%10", "%16", "%8") QTB_TM("%1", "%11", "%16", "%9")
+        QTB_T("%4", "%14", "%18", "%12") QTB_TM("%5", "%15", "%18", "%13")
+        QTB_U("%0", "%10", "%16") QTB_UM("%1", "%11", "%16")
+        QTB_U("%4", "%14", "%18") QTB_UM("%5", "%15", "%18")
+        QTB_V("%2", "%8", "%20", "%0") "\n\t" QTB_V("%3", "%9", "%20", "%1") "\n\t"
+        QTB_V("%6", "%12", "%20", "%4") "\n\t" QTB_V("%7", "%13", "%20", "%5")
+        : "+v"(xa[0]), "+v"(xa[S]), "+v"(xa[2 * S]), "+v"(xa[3 * S]),
+          "+v"(xb[0]), "+v"(xb[S]), "+v"(xb[2 * S]), "+v"(xb[3 * S]),
+          "=&v"(a0), "=&v"(a1), "=&v"(c0), "=&v"(c1), "=&v"(b0), "=&v"(b1), "=&v"(d0), "=&v"(d1)
+        : "v"(wa), "v"(w2a), "v"(wb), "v"(w2b), "s"((f2){2.0f, 2.0f}));
+}
+
 // dft4_geo_k<E, S> as one block when neither w^2 = W32^{2E} nor w is a
 // quarter turn: first stage both pairs with w^2, second stage w and -j w =
 // W32^{E+8}, all SGPR constants (%12 w, %13 w^2, %15 -j w).
@@ -671,7 +700,8 @@ constexpr int kFmtWord3 = 0xFAC | (3 << 12) | (5 << 15);
 // FUSED: 1 = each DFT-4's two butterfly stages as one asm block
 // (dft4_fused_v / _k), 2 = also the post-pass pairs (postpair2), 3 = also
 // the DFT-32's trivial-twiddle DFT-4s and DFT-8 stages (dft4_triv,
-// dft4_fused_kq, dft8_last); the separate blocks cost an s_nop and a
+// dft4_fused_kq, dft8_last), 4 = stage 2's DFT-4s two per block,
+// interleaved (dft4x2_fused_v); the separate blocks cost an s_nop and a
 // scheduling barrier at every seam.
 // FMT (PF = 0 only): typed buffer loads (16_16 SSCALED) convert both int16
 // halves to fp32 in the texture path instead of 64 VALU converts per group
@@ -786,6 +816,12 @@ void fft1024_quad_kernel(FftParams p)
         for (int sl = 0; sl < 2; ++sl) {
             f2 *bb = b + 16 * sl;
             const f2 v = twv(sl, 0), v2 = twv(sl, 1);
+            if constexpr (FUSED >= 4) {
+                dft4x2_fused_v<4>(bb + 0, bb + 1, v, v2, v, v2);
+                dft4x2_fused_v<4>(bb + 2, bb + 3, v, v2, v, v2);
+                dft4x2_fused_v<1>(bb + 0, bb + 4, twv(sl, 2), twv(sl, 3), twv(sl, 4), twv(sl, 5));
+                dft4x2_fused_v<1>(bb + 8, bb + 12, twv(sl, 6), twv(sl, 7), twv(sl, 8), twv(sl, 9));
+            } else {
             static_for<0, 4>([&](auto c) {
                 constexpr int i2 = decltype(c)::value;
                 if constexpr (FUSED >= 1)
@@ -800,6 +836,7 @@ void fft1024_quad_kernel(FftParams p)
                 else
                     dft4_geo_v<1>(bb + 4 * k1, twv(sl, 2 + 2 * k1), twv(sl, 3 + 2 * k1));
             });
+            }
             f2 tt[16];
             static_for<0, 16>([&](auto e) {
                 constexpr int m = decltype(e)::value;  // m = 4 k1 + k2 holds Z[col + 32 (k1 + 4 k2)]
@@ -938,16 +975,17 @@ hipError_t launch_fft_quad_t(const FftParams &p, hipStream_t s)
 // lines in L2 (plain cached loads, AUX 0: FETCH 1.06x the stream at hop 256,
 // 3-6 % faster; sc0 measured the same or slower); disjoint windows stream
 // through with nt (AUX 2; nt at hop 256 re-fetches 1.55x the stream).
-// FUSED 3: the DFT-4 stages, the DFT-32's trivial pieces and the post-pass
-// pairs as single asm blocks (-2.5 to -4.5 % at hop 256, -1 to -2 % at hop
-// 1024 against separate blocks; scripts/fft_probe.hip).
+// FUSED 4: the DFT-4 stages (stage 2: two interleaved per block), the
+// DFT-32's trivial pieces and the post-pass pairs as single asm blocks
+// (-3 to -4.5 % at hop 256, -2 to -4 % at hop 1024 against separate blocks;
+// scripts/fft_probe.hip, profiles/round2/fft_fused/).
 hipError_t launch_fft_quad(const FftParams &p, hipStream_t s)
 {
     if (p.hop < 1024)
-        return p.spec ? launch_fft_quad_t<4, 4, 0, true, false, 0, 3>(p, s)
-                      : launch_fft_quad_t<4, 4, 0, false, false, 0, 3>(p, s);
-    return p.spec ? launch_fft_quad_t<4, 4, 0, true, false, 2, 3>(p, s)
-                  : launch_fft_quad_t<4, 4, 0, false, false, 2, 3>(p, s);
+        return p.spec ? launch_fft_quad_t<4, 4, 0, true, false, 0, 4>(p, s)
+                      : launch_fft_quad_t<4, 4, 0, false, false, 0, 4>(p, s);
+    return p.spec ? launch_fft_quad_t<4, 4, 0, true, false, 2, 4>(p, s)
+                  : launch_fft_quad_t<4, 4, 0, false, false, 2, 4>(p, s);
 }
 
 int fft_quad_slot(int bin) { return quad_slot(bin); }

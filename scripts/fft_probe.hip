@@ -89,6 +89,7 @@ int main(int argc, char **argv)
     vs.push_back({"quad r1 (round-1 shipped)", [](const FftParams &p, hipStream_t s) { return r1b::launch_fft_quad_r1_t<4, 0>(p, s); }, {}});
     vs.push_back({"separate DFT-4 / post-pass blocks", [](const FftParams &p, hipStream_t s) { return p.hop < 1024 ? (p.spec ? launch_fft_quad_t<4, 4, 0, true, false, 0, 0>(p, s) : launch_fft_quad_t<4, 4, 0, false, false, 0, 0>(p, s)) : (p.spec ? launch_fft_quad_t<4, 4, 0, true, false, 2, 0>(p, s) : launch_fft_quad_t<4, 4, 0, false, false, 2, 0>(p, s)); }, {}});
     vs.push_back({"quad shipped (fused, PF0 MINW4)", [](const FftParams &p, hipStream_t s) { return launch_fft_quad(p, s); }, {}});
+    vs.push_back({"fused level 3", [](const FftParams &p, hipStream_t s) { return p.hop < 1024 ? (p.spec ? launch_fft_quad_t<4, 4, 0, true, false, 0, 3>(p, s) : launch_fft_quad_t<4, 4, 0, false, false, 0, 3>(p, s)) : (p.spec ? launch_fft_quad_t<4, 4, 0, true, false, 2, 3>(p, s) : launch_fft_quad_t<4, 4, 0, false, false, 2, 3>(p, s)); }, {}});
     vs.push_back({"fused level 2 (DFT-4 + post-pass)", [](const FftParams &p, hipStream_t s) { return p.hop < 1024 ? (p.spec ? launch_fft_quad_t<4, 4, 0, true, false, 0, 2>(p, s) : launch_fft_quad_t<4, 4, 0, false, false, 0, 2>(p, s)) : (p.spec ? launch_fft_quad_t<4, 4, 0, true, false, 2, 2>(p, s) : launch_fft_quad_t<4, 4, 0, false, false, 2, 2>(p, s)); }, {}});
     vs.push_back({"fused DFT-4 blocks", [](const FftParams &p, hipStream_t s) { return p.hop < 1024 ? (p.spec ? launch_fft_quad_t<4, 4, 0, true, false, 0, 1>(p, s) : launch_fft_quad_t<4, 4, 0, false, false, 0, 1>(p, s)) : (p.spec ? launch_fft_quad_t<4, 4, 0, true, false, 2, 1>(p, s) : launch_fft_quad_t<4, 4, 0, false, false, 2, 1>(p, s)); }, {}});
     vs.push_back({"aux1 (sc0)", [](const FftParams &p, hipStream_t s) { return p.spec ? launch_fft_quad_t<4, 4, 0, true, false, 1>(p, s) : launch_fft_quad_t<4, 4, 0, false, false, 1>(p, s); }, {}});
