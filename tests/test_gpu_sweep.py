@@ -19,6 +19,9 @@ pytestmark = pytest.mark.gpu
 MAG_TOL = 1e-5
 FS = 48000.0
 N_CASES = 120
+# FSKD_SWEEP_SEED=s draws a different set of cases (default 0: the committed
+# set); a deeper ad-hoc run: FSKD_SWEEP_SEED=1 ... -m gpu tests/test_gpu_sweep.py
+SEED_OFFSET = 1000003 * int(__import__("os").environ.get("FSKD_SWEEP_SEED", "0"))
 
 
 def mag_denom(P, mono, n, hop):
@@ -48,7 +51,7 @@ def draw_case(i, fft_nonint=False):
     """fft_nonint: the FFT detector may get off-bin tones (it picks the nearest
     bin, as oracle.fft_demod does); the streaming oracle is the Goertzel bank,
     so streaming cases keep FFT tones on integer bins."""
-    rng = np.random.default_rng(0x5EED + i)
+    rng = np.random.default_rng(0x5EED + i + SEED_OFFSET)
     method = ["auto", "goertzel", "folded", "residue", "fft"][i % 5]
     n = 1024 if method == "fft" else int(2 ** rng.integers(6, 13))  # 64 .. 4096
     half = n // 2
@@ -123,7 +126,7 @@ def test_random_stream(A, O, torch, i):
     oracle's streaming restatement (oracle.Stream): same symbols, same pending
     count after every call, magnitudes within the bar."""
     c = draw_case(100 + i)
-    rng = np.random.default_rng(0xABC + i)
+    rng = np.random.default_rng(0xABC + i + SEED_OFFSET)
     m = {"auto": A.METHOD_AUTO, "goertzel": A.METHOD_GOERTZEL, "folded": A.METHOD_FOLDED,
          "residue": A.METHOD_RESIDUE, "fft": A.METHOD_FFT}[c["method"]]
     n, hop, freqs = c["n"], c["hop"], c["freqs"]
@@ -181,7 +184,7 @@ def test_random_permuted_plans(A, O, torch, i):
     odd multiples of 8) and the residue kernel's compile-time classes (K = 8
     or 16 with K / 4 tones per class), in random tone order, hop and level;
     magnitudes and symbols in the caller's tone order."""
-    rng = np.random.default_rng(0xC1A55 + i)
+    rng = np.random.default_rng(0xC1A55 + i + SEED_OFFSET)
     kind = ("fold16", "residue8", "residue16")[i % 3]
     if kind == "fold16":
         z0 = rng.choice(np.arange(1, 31) * 16, 4, replace=False)
