@@ -1,0 +1,56 @@
+#!/usr/bin/env python3
+"""Full-spectrum output of the FFT detector (demod_batch_spectrum_async,
+SURVEY §8 f3): kernel time per launch with |X[b]|^2 for all 513 bins stored
+(2052 B per window) against symbols + tone powers only, over one 2^30-sample
+stream at hop 1024 and 256. Median of 20 after 30 warmups; the written
+spectrum rate is n_windows x 2052 B / t.
+
+    python scripts/spectrum_probe.py
+"""
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    import torch
+    import bench
+    A, _ = bench.load_pkg()
+    n, src = 1024, 1 << 20
+    d_pcm = torch.empty((src, n), dtype=torch.int16, device="cuda")
+    A.synth_fsk(A.make_cfg(), 7, src, 8000, 400, d_pcm)
+    s = torch.cuda.current_stream()
+    for hop in (1024, 256):
+        W = (src * n - n) // hop + 1
+        sym = torch.empty(W, dtype=torch.uint8, device="cuda")
+        mag = torch.empty((W, 2), dtype=torch.float32, device="cuda")
+        spec = torch.empty((W, 513), dtype=torch.float32, device="cuda")
+        with A.Demodulator(freqs=A.FSK2_FREQS, hop=hop, method=A.METHOD_FFT) as d:
+            for label, run in (("tones", lambda: d.batch_async(d_pcm, W, sym, mag, stream=s.cuda_stream)),
+                               ("spectrum", lambda: d.batch_spectrum_async(d_pcm, W, sym, mag, spec,
+                                                                           stream=s.cuda_stream))):
+                for _ in range(30):
+                    run()
+                ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                      for _ in range(20)]
+                for a, b in ev:
+                    a.record(s)
+                    run()
+                    b.record(s)
+                torch.cuda.synchronize()
+                ms = float(np.median([a.elapsed_time(b) for a, b in ev]))
+                out = W * (513 * 4 if label == "spectrum" else 9)
+                print(json.dumps({"hop": hop, "windows": W, "output": label, "kernel_ms": round(ms, 4),
+                                  "write_GBps": round(out / (ms / 1e3) / 1e9, 1),
+                                  "read_GBps": round(src * n * 2 / (ms / 1e3) / 1e9, 1)}), flush=True)
+        del spec, mag, sym
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
