@@ -35,6 +35,7 @@ namespace quad {
 // rate as two plain ones, but one wave issues half as many instructions — and
 // this kernel is issue-bound (one wave/SIMD issues a VALU op every 4 cycles).
 typedef float f2 __attribute__((ext_vector_type(2)));
+typedef float f4 __attribute__((ext_vector_type(4)));
 
 // a * w (w in VGPRs): lo = a.x w.x - a.y w.y, hi = a.x w.y + a.y w.x
 __device__ __forceinline__ f2 cmul(f2 a, f2 w)
@@ -707,14 +708,20 @@ constexpr int kFmtWord3 = 0xFAC | (3 << 12) | (5 << 15);
 // halves to fp32 in the texture path instead of 64 VALU converts per group
 // (measured neutral).
 template <int WPB = 4, int MINW = 4, int PF = 0, bool SPEC = true, bool FMT = false, int AUX = 2,
-          int FUSED = 0>
-__global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MINW > 0 ? MINW : 1)))
-void fft1024_quad_kernel(FftParams p)
+          int FUSED = 0, int RD = 0>
+__device__ __attribute__((always_inline)) inline void fft1024_quad_body(const FftParams &p)
 {
     using namespace quad;
     __shared__ __attribute__((aligned(16))) f2 slab[WPB][kQSlab];
-    __shared__ f2 tw2[2 * 10 * 16];  // [column slot][v, v2, g0, g0^2, .., g3, g3^2][t]
-    __shared__ f2 tw3[16 * 16];      // post-pass W1024^{kP(t, j)} / 2 at [j][t]
+    // RD < 2: tw2 [column slot][v, v2, g0, g0^2, .., g3, g3^2][t], tw3 [j][t];
+    // RD 2: lane-major, [slot][t][m] and [t][j] (row padded to 18), so each
+    // pair used together is one 16-byte read; the row strides (20 and 36
+    // dwords) put a ds_read_b128 group's 16 addresses on distinct banks
+    constexpr int kT3 = RD >= 2 ? 18 : 16;
+    __shared__ __attribute__((aligned(16))) f2 tw2[2 * 10 * 16];
+    __shared__ __attribute__((aligned(16))) f2 tw3[16 * kT3];
+    auto tw2_at = [](int sl, int m, int tt) { return RD >= 2 ? sl * 160 + tt * 10 + m : sl * 160 + m * 16 + tt; };
+    auto tw3_at = [](int j, int tt) { return RD >= 2 ? tt * kT3 + j : j * 16 + tt; };
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int q = lane >> 4;   // window of the wave
@@ -731,11 +738,11 @@ void fft1024_quad_kernel(FftParams p)
             const int k1 = (m - 2) >> 1;
             e = (col + 32 * k1) * (((m - 2) & 1) ? 2 : 1);   // g_k1, g_k1^2
         }
-        tw2[i] = t512[e & 511];
+        tw2[tw2_at(sl, m, tt)] = t512[e & 511];
     }
     for (int i = threadIdx.x; i < 16 * 16; i += 64 * WPB) {
         const int tt = i & 15, j = i >> 4;
-        tw3[i] = 0.5f * t1024[(tt == 0 && j < 8) ? 16 + 32 * j : tt + 32 * j];
+        tw3[tw3_at(j, tt)] = 0.5f * t1024[(tt == 0 && j < 8) ? 16 + 32 * j : tt + 32 * j];
     }
     const int k1b = t == 0 ? 16 : 32 - t;
     const int myslot = quad_slot(t < p.k ? p.bins[t] : 0);
@@ -811,16 +818,33 @@ void fft1024_quad_kernel(FftParams p)
             __builtin_amdgcn_wave_barrier();
         }
         // 3. per column: DFT-16 over t of A_t[col] W512^{t col}, twiddles fused
-        auto twv = [&](int sl, int m) -> f2 { return tw2[sl * 160 + m * 16 + t]; };
+        // twp(sl, m): the pair (m, m + 1) of slot sl, m even
+        auto twp = [&](int sl, int m, f2 &lo, f2 &hi) {
+            if constexpr (RD >= 2) {
+                const f4 x = *reinterpret_cast<const f4 *>(&tw2[tw2_at(sl, m, t)]);
+                lo = (f2){x.x, x.y};
+                hi = (f2){x.z, x.w};
+            } else {
+                lo = tw2[tw2_at(sl, m, t)];
+                hi = tw2[tw2_at(sl, m + 1, t)];
+            }
+        };
+        auto twv = [&](int sl, int m) -> f2 { return tw2[tw2_at(sl, m, t)]; };
 #pragma unroll
         for (int sl = 0; sl < 2; ++sl) {
             f2 *bb = b + 16 * sl;
-            const f2 v = twv(sl, 0), v2 = twv(sl, 1);
+            f2 v, v2;
+            twp(sl, 0, v, v2);
             if constexpr (FUSED >= 4) {
                 dft4x2_fused_v<4>(bb + 0, bb + 1, v, v2, v, v2);
                 dft4x2_fused_v<4>(bb + 2, bb + 3, v, v2, v, v2);
-                dft4x2_fused_v<1>(bb + 0, bb + 4, twv(sl, 2), twv(sl, 3), twv(sl, 4), twv(sl, 5));
-                dft4x2_fused_v<1>(bb + 8, bb + 12, twv(sl, 6), twv(sl, 7), twv(sl, 8), twv(sl, 9));
+                f2 g0, g0s, g1, g1s, g2, g2s, g3, g3s;
+                twp(sl, 2, g0, g0s);
+                twp(sl, 4, g1, g1s);
+                twp(sl, 6, g2, g2s);
+                twp(sl, 8, g3, g3s);
+                dft4x2_fused_v<1>(bb + 0, bb + 4, g0, g0s, g1, g1s);
+                dft4x2_fused_v<1>(bb + 8, bb + 12, g2, g2s, g3, g3s);
             } else {
             static_for<0, 4>([&](auto c) {
                 constexpr int i2 = decltype(c)::value;
@@ -874,13 +898,22 @@ void fft1024_quad_kernel(FftParams p)
                 Q1 = sel_l0(b[16 - j1], Q1);
             }
             f2 pw0, pw1;  // (|X[kP]|^2, |X[512-kP]|^2)
+            f2 w0, w1;
+            if constexpr (RD >= 2) {
+                const f4 x = *reinterpret_cast<const f4 *>(&tw3[tw3_at(j0, t)]);
+                w0 = (f2){x.x, x.y};
+                w1 = (f2){x.z, x.w};
+            } else {
+                w0 = tw3[tw3_at(j0, t)];
+                w1 = tw3[tw3_at(j1, t)];
+            }
             if constexpr (FUSED >= 2) {
-                postpair2(pw0, P0, Q0, tw3[16 * j0 + t], pw1, P1, Q1, tw3[16 * j1 + t]);
+                postpair2(pw0, P0, Q0, w0, pw1, P1, Q1, w1);
             } else {
                 const f2 S0 = pp_s(P0, Q0), S1 = pp_s(P1, Q1);
                 const f2 D0 = pp_d(P0, Q0), D1 = pp_d(P1, Q1);
                 f2 T0, T1;
-                cmul2(T0, D0, tw3[16 * j0 + t], T1, D1, tw3[16 * j1 + t]);
+                cmul2(T0, D0, w0, T1, D1, w1);
                 const f2 re0 = pp_re_h(S0, T0), re1 = pp_re_h(S1, T1);
                 const f2 im0 = pp_im_h(S0, T0), im1 = pp_im_h(S1, T1);
                 pwr2(pw0, re0, im0, pw1, re1, im1);
@@ -947,24 +980,53 @@ void fft1024_quad_kernel(FftParams p)
     }
 }
 
+template <int WPB = 4, int MINW = 4, int PF = 0, bool SPEC = true, bool FMT = false, int AUX = 2,
+          int FUSED = 0>
+__global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MINW > 0 ? MINW : 1)))
+void fft1024_quad_kernel(FftParams p)
+{
+    fft1024_quad_body<WPB, MINW, PF, SPEC, FMT, AUX, FUSED, 0>(p);
+}
+
+// (a device-code attribute: the host pass of hipcc does not know the feature)
+#if defined(__HIP_DEVICE_COMPILE__)
+#define FSKD_NO_LDS_PAIRING __attribute__((target("no-load-store-opt")))
+#else
+#define FSKD_NO_LDS_PAIRING
+#endif
+// The same kernel without the backend's LDS-access pairing: the transpose's
+// column reads and the twiddle-table reads stay ds_read_b64 (2 LDS cycles per
+// wave, 256 B/clk) instead of being merged into ds_read2_b64 (8 cycles for
+// twice the bytes, 128 B/clk; MI355X_MICROARCH.md §LDS). RD 2: also the
+// twiddle tables lane-major, one ds_read_b128 (4 cycles) per twiddle pair.
+template <int WPB = 4, int MINW = 4, int PF = 0, bool SPEC = true, bool FMT = false, int AUX = 2,
+          int FUSED = 0, int RD = 1>
+__global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MINW > 0 ? MINW : 1)))
+FSKD_NO_LDS_PAIRING void fft1024_quad_kernel_r64(FftParams p)
+{
+    fft1024_quad_body<WPB, MINW, PF, SPEC, FMT, AUX, FUSED, RD>(p);
+}
+
 // Persistent grid: as many blocks as fit the chip, each wave strides over
 // groups of 4 windows (the LDS twiddle tables are built once per block).
-template <int WPB, int MINW, int PF, bool SPEC, bool FMT = false, int AUX = 2, int FUSED = 0>
+template <int WPB, int MINW, int PF, bool SPEC, bool FMT = false, int AUX = 2, int FUSED = 0, int RD = 0>
 hipError_t launch_fft_quad_t(const FftParams &p, hipStream_t s)
 {
+    void (*kern)(FftParams);
+    if constexpr (RD > 0)
+        kern = fft1024_quad_kernel_r64<WPB, MINW, PF, SPEC, FMT, AUX, FUSED, RD>;
+    else
+        kern = fft1024_quad_kernel<WPB, MINW, PF, SPEC, FMT, AUX, FUSED>;
     int dev = 0, cus = 256, per_cu = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fft1024_quad_kernel<WPB, MINW, PF, SPEC, FMT, AUX, FUSED>,
-                                                     64 * WPB, 0) != hipSuccess ||
-        per_cu < 1)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * WPB, 0) != hipSuccess || per_cu < 1)
         per_cu = 1;
     const long long groups = (p.n_windows + 3) / 4;
     long long blocks = (groups + WPB - 1) / WPB;
     blocks = std::min<long long>(blocks, (long long)cus * per_cu);
     if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL((fft1024_quad_kernel<WPB, MINW, PF, SPEC, FMT, AUX, FUSED>), dim3((unsigned)blocks), dim3(64 * WPB),
-                       0, s, p);
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(64 * WPB), 0, s, p);
     return hipGetLastError();
 }
 

@@ -94,6 +94,8 @@ int main(int argc, char **argv)
     vs.push_back({"fused DFT-4 blocks", [](const FftParams &p, hipStream_t s) { return p.hop < 1024 ? (p.spec ? launch_fft_quad_t<4, 4, 0, true, false, 0, 1>(p, s) : launch_fft_quad_t<4, 4, 0, false, false, 0, 1>(p, s)) : (p.spec ? launch_fft_quad_t<4, 4, 0, true, false, 2, 1>(p, s) : launch_fft_quad_t<4, 4, 0, false, false, 2, 1>(p, s)); }, {}});
     vs.push_back({"aux1 (sc0)", [](const FftParams &p, hipStream_t s) { return p.spec ? launch_fft_quad_t<4, 4, 0, true, false, 1>(p, s) : launch_fft_quad_t<4, 4, 0, false, false, 1>(p, s); }, {}});
     vs.push_back({"aux2 (nt, round-2 first ship)", [](const FftParams &p, hipStream_t s) { return p.spec ? launch_fft_quad_t<4, 4, 0, true, false, 2>(p, s) : launch_fft_quad_t<4, 4, 0, false, false, 2>(p, s); }, {}});
+    vs.push_back({"ds_read_b64 (no read2 pairing)", [](const FftParams &p, hipStream_t s) { return p.hop < 1024 ? (p.spec ? launch_fft_quad_t<4, 4, 0, true, false, 0, 4, 1>(p, s) : launch_fft_quad_t<4, 4, 0, false, false, 0, 4, 1>(p, s)) : (p.spec ? launch_fft_quad_t<4, 4, 0, true, false, 2, 4, 1>(p, s) : launch_fft_quad_t<4, 4, 0, false, false, 2, 4, 1>(p, s)); }, {}});
+    vs.push_back({"ds_read_b64 + b128 tables", [](const FftParams &p, hipStream_t s) { return p.hop < 1024 ? (p.spec ? launch_fft_quad_t<4, 4, 0, true, false, 0, 4, 2>(p, s) : launch_fft_quad_t<4, 4, 0, false, false, 0, 4, 2>(p, s)) : (p.spec ? launch_fft_quad_t<4, 4, 0, true, false, 2, 4, 2>(p, s) : launch_fft_quad_t<4, 4, 0, false, false, 2, 4, 2>(p, s)); }, {}});
     vs.push_back({"fused PF1 MINW0", [](const FftParams &p, hipStream_t s) { return p.spec ? launch_fft_quad_t<4, 0, 1, true>(p, s) : launch_fft_quad_t<4, 0, 1, false>(p, s); }, {}});
     if (filter) {
         std::vector<Var> keep;
