@@ -26,6 +26,10 @@ histogram SURVEY §7 asks for, at sigma 400 and at the sigma 2000 stress level).
 At N = 1 the default run also measures configs[2] (8-FSK) and configs[3]
 (sliding FFT, hop 256) with the same steps/warmup and reports them under
 "fsk8" and "fft_hop256" (no CPU baseline for those).
+
+Defaults: 200 timed steps after 20 warmup steps (the warmup is at least 64
+launches, MIN_WARMUP), so each config keeps the GPU busy for 0.1-0.5 s
+rather than a few ms, long enough for an outside utilisation sampler to see.
 """
 import argparse
 import importlib.util
@@ -529,8 +533,8 @@ def summary(r) -> dict:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", choices=["fsk2", "fsk8", "fft", "streams"], default="fsk2",
                     help="fsk2 = configs[1] (default), fsk8 = configs[2], fft = configs[3]: "
                          "sliding 1024-pt full-spectrum FFT (hop --hop) over the same stream, "
