@@ -27,6 +27,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "liboracle.so")
 REF_NANOPB = os.path.join(HERE, "_ref", "libnanopb_ref.so")
 REF_KISSFFT = os.path.join(HERE, "_ref", "libkissfft_ref.so")
+REF_KISSFFT_CUSTOM = os.path.join(HERE, "_ref", "libkissfft_custom.so")  # CUSTOM_MODES build
 KISSFFT_PRESHIFT = 14  # int16 samples << 14: the Q31 range opus_fft_c is built for
 
 _lib = None
@@ -373,4 +374,34 @@ def ref_fft_static(which: int, x: np.ndarray):
     rc = R.ref_fft_static32(which, x32.ctypes.data, n, re.ctypes.data, im.ctypes.data)
     if rc != n:
         raise ValueError(f"ref_fft_static32: {rc}")
+    return re + 1j * im
+
+
+_ref_kfc = None
+
+
+def ref_kissfft_custom() -> Optional[ctypes.CDLL]:
+    """The same opus_fft_c compiled with CUSTOM_MODES (any nfft it can
+    factor, e.g. the north-star N = 1024), or None."""
+    global _ref_kfc
+    if _ref_kfc is None and os.path.exists(REF_KISSFFT_CUSTOM):
+        R = ctypes.CDLL(REF_KISSFFT_CUSTOM)
+        R.ref_fft_custom32.argtypes = [ctypes.c_int, _P, _P, _P]
+        R.ref_fft_custom32.restype = ctypes.c_int
+        _ref_kfc = R
+    return _ref_kfc
+
+
+def ref_fft_custom(x: np.ndarray):
+    """opus_fft_c of int16 frame x with a state opus_fft_alloc'd for len(x)
+    (kissfft_custom_harness.c); the reference's raw complex output (X / nfft,
+    scaled by 2^KISSFFT_PRESHIFT)."""
+    R = ref_kissfft_custom()
+    x32 = (np.ascontiguousarray(x, np.int16).astype(np.int32) << KISSFFT_PRESHIFT)
+    n = x32.size
+    re = np.empty(n)
+    im = np.empty(n)
+    rc = R.ref_fft_custom32(n, x32.ctypes.data, re.ctypes.data, im.ctypes.data)
+    if rc != n:
+        raise ValueError(f"ref_fft_custom32({n}): {rc}")
     return re + 1j * im

@@ -25,11 +25,20 @@ OPUS     := $(REF)/hardware/lib/libopus/src
 KF_SRCS  := $(OPUS)/celt/kiss_fft.c $(OPUS)/celt/modes.c $(OPUS)/celt/mathops.c \
             oracle/kissfft_ref_harness.c
 
-all: $(OUT)/libnanopb_ref.so $(OUT)/libkissfft_ref.so
+KC_SRCS  := $(OPUS)/celt/kiss_fft.c $(OPUS)/celt/mathops.c oracle/kissfft_custom_harness.c
+
+all: $(OUT)/libnanopb_ref.so $(OUT)/libkissfft_ref.so $(OUT)/libkissfft_custom.so
 
 $(OUT)/libkissfft_ref.so: $(KF_SRCS)
 	@mkdir -p $(OUT)
 	gcc -O2 -fPIC -shared -DHAVE_CONFIG_H -I$(OPUS) -I$(OPUS)/celt $(KF_SRCS) -o $@ \
+	    -Wl,--no-undefined -lm
+
+# the same kiss_fft.c with the libopus configure option CUSTOM_MODES on, so it
+# allocates nfft = 1024 (kissfft_custom_harness.c); config.h otherwise unchanged
+$(OUT)/libkissfft_custom.so: $(KC_SRCS)
+	@mkdir -p $(OUT)
+	gcc -O2 -fPIC -shared -DHAVE_CONFIG_H -DCUSTOM_MODES -I$(OPUS) -I$(OPUS)/celt $(KC_SRCS) -o $@ \
 	    -Wl,--no-undefined -lm
 
 $(OUT)/libnanopb_ref.so: $(SRCS)
@@ -37,6 +46,6 @@ $(OUT)/libnanopb_ref.so: $(SRCS)
 	gcc -O2 -fPIC -shared -I$(NANOPB) -I$(PROTOGEN) $(SRCS) -o $@
 
 clean:
-	rm -f $(OUT)/libnanopb_ref.so $(OUT)/libkissfft_ref.so
+	rm -f $(OUT)/libnanopb_ref.so $(OUT)/libkissfft_ref.so $(OUT)/libkissfft_custom.so
 
 .PHONY: all clean

@@ -11,6 +11,10 @@ seeded int16 frames for each of its four static sizes (480, 240, 120, 60).
 Stored per size N: the input frames x<N> (int16 [F][N]) and the reference's
 raw complex output re<N>, im<N> (float64 [F][N]: X/N in its fixed point,
 inputs pre-shifted by KISSFFT_PRESHIFT). Plain arrays (allow_pickle=False).
+
+N = 1024, the north-star window, comes from the same kiss_fft.c compiled with
+the libopus configure option CUSTOM_MODES (oracle/_ref/libkissfft_custom.so,
+oracle/kissfft_custom_harness.c: opus_fft_alloc(1024) + opus_fft_c).
 """
 import os
 import sys
@@ -56,6 +60,15 @@ def main():
         out[f"re{n}"] = y.real
         out[f"im{n}"] = y.imag
         print(f"kfft[{which}]: nfft {n}, {len(x)} frames")
+    if O.ref_kissfft_custom() is None:
+        sys.exit("oracle/_ref/libkissfft_custom.so missing: run `make -f oracle/ref.mk` first")
+    n = 1024
+    x = frames(n)
+    y = np.stack([O.ref_fft_custom(row) for row in x])
+    out[f"x{n}"] = x
+    out[f"re{n}"] = y.real
+    out[f"im{n}"] = y.imag
+    print(f"custom: nfft {n}, {len(x)} frames")
     np.savez_compressed(os.path.join(HERE, "ref_kissfft.npz"), **out)
 
 

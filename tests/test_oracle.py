@@ -183,12 +183,15 @@ def _ref_powers(g, n):
     return np.abs(Y[:, : n // 2 + 1]) ** 2
 
 
-@pytest.mark.parametrize("n", [480, 240, 120, 60])
+@pytest.mark.parametrize("n", [1024, 480, 240, 120, 60])
 def test_oracle_goertzel_pinned_to_reference_fft(O, n):
     """Oracle Goertzel powers at every bin of the n-point frame equal the
     reference opus_fft_c's |X|^2 (golden outputs) to the reference's Q15
     precision; at n = 480, where the 2-FSK tones are bins 15 and 30, the
-    oracle's symbol is the argmax of the reference spectrum at those bins."""
+    oracle's symbol is the argmax of the reference spectrum at those bins.
+    n = 1024 (the north-star window) is the CUSTOM_MODES build of the same
+    kiss_fft.c; there the oracle's 2-FSK (bins 32, 64) and 8-FSK (bins
+    32 + 8 i) symbols are the argmax of the reference spectrum."""
     g = _ref_kissfft_golden()
     x = g[f"x{n}"]
     Pr = _ref_powers(g, n)
@@ -201,6 +204,17 @@ def test_oracle_goertzel_pinned_to_reference_fft(O, n):
     if n == 480:
         sym, _ = O.goertzel(x[:4], (1500.0, 3000.0), n)
         assert (sym == np.argmax(Pr[:4][:, [15, 30]], axis=1)).all()
+    if n == 1024:
+        sym, _ = O.goertzel(x[:4], (1500.0, 3000.0), n)
+        assert (sym == np.argmax(Pr[:4][:, [32, 64]], axis=1)).all()
+        f8 = tuple(1500.0 + 375.0 * i for i in range(8))
+        sym, _ = O.goertzel(x[4:8], f8, n)
+        assert (sym == np.argmax(Pr[4:8][:, [32 + 8 * i for i in range(8)]], axis=1)).all()
+        # and the FFT oracle's full spectrum against the reference's
+        for i, row in enumerate(x):
+            Pf = O.fft_power(row)
+            energy = n * float((row.astype(np.float64) ** 2).sum())
+            assert np.abs(Pf - Pr[i]).max() <= REF_FFT_TOL * max(energy, 1.0), i
 
 
 def test_reference_fft_golden_is_live_reference_output(O):
@@ -214,6 +228,20 @@ def test_reference_fft_golden_is_live_reference_output(O):
         n = O.ref_kissfft().ref_fft_static_size(which)
         y = np.stack([O.ref_fft_static(which, row) for row in g[f"x{n}"]])
         assert np.array_equal(y.real, g[f"re{n}"]) and np.array_equal(y.imag, g[f"im{n}"])
+
+
+def test_reference_fft1024_golden_is_live_reference_output(O):
+    """The committed N = 1024 outputs are what the reference's kiss_fft.c,
+    compiled with CUSTOM_MODES (oracle/_ref/libkissfft_custom.so), computes;
+    at the static sizes that build agrees with the static states bit for bit."""
+    if O.ref_kissfft_custom() is None:
+        pytest.skip("oracle/_ref/libkissfft_custom.so not built (needs /root/reference)")
+    g = _ref_kissfft_golden()
+    y = np.stack([O.ref_fft_custom(row) for row in g["x1024"]])
+    assert np.array_equal(y.real, g["re1024"]) and np.array_equal(y.imag, g["im1024"])
+    for n in (480, 240):
+        y = np.stack([O.ref_fft_custom(row) for row in g[f"x{n}"][:3]])
+        assert np.array_equal(y.real, g[f"re{n}"][:3]) and np.array_equal(y.imag, g[f"im{n}"][:3])
 
 
 def test_oracle_rejects_too_many_tones(O):
