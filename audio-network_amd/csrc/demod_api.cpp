@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -194,15 +195,21 @@ static int init_device_state(demod_t *st)
     // integer bin (K >= 5: at K = 3, 4 the plain bank measured as fast).
     // Overlapping windows at n = 1024 with hop a multiple of 64 share their
     // 64-sample segments: the plain bank computes each segment once (SLIDE,
-    // goertzel.hip). AUTO keeps it over the folded detectors
-    // up to hop 128 (8-FSK: 0.89 vs 1.23 ms at hop 128, 0.71 vs 0.68 at 256).
-    const bool slide = lg == 4 && c.hop < c.n && c.hop % 64 == 0;
+    // goertzel.hip) and the fold detector runs its folded sums forward from
+    // window to window (fold_slide_kernel, fold.hip). The
+    // residue detector has no segment-shared form, so AUTO keeps the plain
+    // SLIDE over it up to hop 128 (8-FSK: 0.89 vs 1.23 ms at hop 128).
+    // FSKD_NO_SLIDE=1 (measurement switch for probes) runs the direct kernels.
+    const char *no_slide_env = std::getenv("FSKD_NO_SLIDE");
+    const bool slide = lg == 4 && c.hop < c.n && c.hop % 64 == 0 &&
+                       !(no_slide_env && no_slide_env[0] == '1');
     st->detector = kDetGoertzel;
     if (c.method == DEMOD_METHOD_FOLDED) st->detector = kDetFolded;
     else if (c.method == DEMOD_METHOD_RESIDUE) st->detector = kDetResidue;
-    else if (c.method == DEMOD_METHOD_AUTO && !(slide && c.hop <= 128)) {
+    else if (c.method == DEMOD_METHOD_AUTO) {
         if (c.k >= 3 && fold_eligible(c)) st->detector = kDetFolded;
-        else if (c.k >= 5 && residue_eligible(c)) st->detector = kDetResidue;
+        else if (!(slide && c.hop <= 128) && c.k >= 5 && residue_eligible(c))
+            st->detector = kDetResidue;
     }
     if (c.method == DEMOD_METHOD_FFT) {
         st->detector = kDetFft;
@@ -334,6 +341,11 @@ static int init_device_state(demod_t *st)
     st->slide_wt = 0;
     if (slide && st->detector == kDetGoertzel)
         st->slide_wt = (64 - 16) / (int)(c.hop / 64) + 1;  // the last window's 16 segments end in the tile
+    if (slide && st->detector == kDetFolded) {
+        // 4 R windows (R per 16-lane group) whose 16 + (4R - 1) H segments fit the tile
+        const int H = (int)(c.hop / 64);
+        st->slide_wt = 4 * std::max(1, ((kFoldSlideSegs - 16) / H + 1) / 4);
+    }
     return DEMOD_OK;
 }
 

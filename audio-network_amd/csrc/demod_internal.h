@@ -17,6 +17,7 @@ constexpr int kPlainWPB = 2;
 constexpr int kLdsSegStride = 144;    // bytes: 128 B segment + 16 B pad (conflict-free b128 reads)
 constexpr int kLdsWaveBytes = 64 * kLdsSegStride;
 constexpr int kMaxTones = 16;
+constexpr int kFoldSlideSegs = 80;    // fold.hip fold_slide_kernel: segments per tile (10 KiB)
 constexpr int kMaxDevices = 64;       // device ordinals the module tables cover
 
 // Uniform per-launch parameters (kernarg -> SGPRs).

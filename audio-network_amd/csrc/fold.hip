@@ -42,6 +42,78 @@ __device__ __forceinline__ float group_sum_f(float v, int log2g)
     return v;
 }
 
+// The decision of one window at n = 1024 from this lane's folded integer sums
+// acc[0..7] (lane j of the window: positions 8j .. 8j + 7 of the N/8 fold,
+// i.e. the even-segment half of positions 8(j & 7).. for j < 8 and the odd
+// half for j >= 8): the int -> fp32 converts, the K recurrences over the 8
+// folded samples, the rotation into window phase and the window_sum.h
+// epilogue. F16: c16 / r hold this lane's four slots (fold_tile_kernel F16).
+// fold_tile_kernel and fold_slide_kernel both end here, so a window's result
+// does not depend on which of them formed its sums.
+template <int K, bool F16>
+__device__ __forceinline__ void fold_decide(const int (&acc)[8], const float4 *r,
+                                            const float (&c16)[4], int lane, long long w,
+                                            bool live, const GoertzelParams &p)
+{
+    float xf[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) xf[q] = (float)acc[q];
+    if constexpr (F16) {
+        const float sg = (lane & 8) ? -1.f : 1.f;
+        float y[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q)  // lanes < 8: E + O = Z0; lanes >= 8: E - O = Z8
+            y[q] = fmaf(sg, xf[q], dppf_<0x128>(xf[q]));
+        float xr[4], xi[4];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {  // tone pairs in packed fp32 (2 ops per pair-sample)
+            const f32x2f c2 = f32x2f{c16[2 * h], c16[2 * h + 1]};
+            f32x2f a1 = f32x2f{0.f, 0.f}, a2 = f32x2f{0.f, 0.f};
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const f32x2f a = __builtin_elementwise_fma(c2, a1, f32x2f{y[q], y[q]} - a2);
+                a2 = a1;
+                a1 = a;
+            }
+            xr[2 * h] = r[2 * h].x * a1.x - r[2 * h].z * a2.x;
+            xi[2 * h] = r[2 * h].y * a1.x - r[2 * h].w * a2.x;
+            xr[2 * h + 1] = r[2 * h + 1].x * a1.y - r[2 * h + 1].z * a2.y;
+            xi[2 * h + 1] = r[2 * h + 1].y * a1.y - r[2 * h + 1].w * a2.y;
+        }
+        window_sum_decide_split8<true>(xr, xi, lane, w, live, p.sym, p.mag, p.perm);
+    } else {
+        float xr[K], xi[K];
+        constexpr int HP = K / 2;  // packed tone pairs; an odd last tone runs scalar
+#pragma unroll
+        for (int h = 0; h < HP; ++h) {
+            const f32x2f c2 = f32x2f{p.coef[2 * h], p.coef[2 * h + 1]};
+            f32x2f a1 = f32x2f{0.f, 0.f}, a2 = f32x2f{0.f, 0.f};
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const f32x2f a = __builtin_elementwise_fma(c2, a1, f32x2f{xf[q], xf[q]} - a2);
+                a2 = a1;
+                a1 = a;
+            }
+            xr[2 * h] = r[2 * h].x * a1.x - r[2 * h].z * a2.x;
+            xi[2 * h] = r[2 * h].y * a1.x - r[2 * h].w * a2.x;
+            xr[2 * h + 1] = r[2 * h + 1].x * a1.y - r[2 * h + 1].z * a2.y;
+            xi[2 * h + 1] = r[2 * h + 1].y * a1.y - r[2 * h + 1].w * a2.y;
+        }
+        if constexpr (K & 1) {
+            float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const float a = fmaf(p.coef[K - 1], s1, xf[q] - s2);
+                s2 = s1;
+                s1 = a;
+            }
+            xr[K - 1] = r[K - 1].x * s1 - r[K - 1].z * s2;
+            xi[K - 1] = r[K - 1].y * s1 - r[K - 1].w * s2;
+        }
+        window_sum_decide<K>(xr, xi, lane, w, live, p.sym, p.mag);
+    }
+}
+
 //   ROTLDS: keep the per-lane rotation constants in a block LDS table instead
 //           of 4K VGPRs (raises occupancy for large K).
 //   NTS: non-temporal output stores.
@@ -145,33 +217,15 @@ __global__ __launch_bounds__(64 * WPB) void fold_tile_kernel(GoertzelParams p)
                 acc[2 * q + 1] += (int)d4[q] >> 16;
             }
         }
+        if constexpr (F16 || (WS && LOG2G == 4 && !PK && !ROTLDS)) {
+            const long long w = wbase + win_in_tile;
+            fold_decide<K, F16>(acc, r, c16, lane, w, w < p.n_windows, p);
+            continue;
+        }
         float xf[8];
 #pragma unroll
         for (int q = 0; q < 8; ++q) xf[q] = (float)acc[q];
 
-        if constexpr (F16) {
-            const float sg = (lane & 8) ? -1.f : 1.f;
-            float y[8];
-#pragma unroll
-            for (int q = 0; q < 8; ++q)  // lanes < 8: E + O = Z0; lanes >= 8: E - O = Z8
-                y[q] = fmaf(sg, xf[q], dppf_<0x128>(xf[q]));
-            float xr[4], xi[4];
-#pragma unroll
-            for (int s4 = 0; s4 < 4; ++s4) {
-                float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-                for (int q = 0; q < 8; ++q) {
-                    const float a = fmaf(c16[s4], s1, y[q] - s2);
-                    s2 = s1;
-                    s1 = a;
-                }
-                xr[s4] = r[s4].x * s1 - r[s4].z * s2;
-                xi[s4] = r[s4].y * s1 - r[s4].w * s2;
-            }
-            const long long w = wbase + win_in_tile;
-            window_sum_decide_split8<true>(xr, xi, lane, w, w < p.n_windows, p.sym, p.mag, p.perm);
-            continue;
-        }
         if constexpr (WS && LOG2G == 4) {
             float xr[K], xi[K];
             float t1[K], t2[K];
@@ -246,6 +300,125 @@ __global__ __launch_bounds__(64 * WPB) void fold_tile_kernel(GoertzelParams p)
     }
 }
 
+// Overlapping windows (n = 1024, hop = 64 H < n) for fold-eligible plans:
+// the folded sums of a window are sums of its 64-sample segments. With
+// seg_s the segments of the stream and window u starting at segment uH,
+// lane j of the window holds (fold_tile_kernel's LDST layout)
+//     E_u = sum_{m even < 16} seg_{uH + m}   (j < 8)
+//     O_u = sum_{m odd  < 16} seg_{uH + m}   (j >= 8)
+// over positions 8 (j & 7) .. + 7. The window H segments later shares all but
+// H of them: with pp = (parity + H) mod 2, the lane's sums of window u are
+// the previous window's parity-pp sums minus its parity-pp segments m < H and
+// plus its parity-pp segments 16 <= m < 16 + H (for odd H the E and O roles
+// swap between the lane and its partner j ^ 8: one DPP row_ror:8). Integer
+// sums, so every window's sums equal direct folding bit for bit, and the
+// decision is the same fold_decide: the output is bit-identical to
+// fold_tile_kernel on that window alone. Per window a lane reads H segment
+// chunks instead of 8 (hop 256: 32 instead of 64 integer adds) and the tile
+// streams from HBM once, where the direct kernel re-reads every window.
+//   Tile: Wt = 4 R windows (p.slide_wt; host: the largest R whose
+//   16 + (4R - 1) H segments fit kFoldSlideSegs = 80, i.e. 10 KiB), loaded
+//   contiguously (16 B/lane, 10 instructions) into a wave-private LDS slice
+//   (chunk c of segment s at 16 (8 s + c)); each 16-lane group takes R
+//   consecutive windows, running the sums forward from its first. Every
+//   group has R windows, so no pass of the epilogue idles (a 64-segment tile
+//   at hop 256 holds 13 windows: 4 passes for 13).
+template <int K, bool F16>
+__global__ __launch_bounds__(64 * kPlainWPB) void fold_slide_kernel(GoertzelParams p)
+{
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int j = lane & 15;
+    const int par = j >> 3;      // 0: even segments of the window, 1: odd
+    const int chunk = j & 7;     // positions 8 chunk .. + 7 of a segment
+    const int H = (int)(p.hop >> 6);
+    const int wt = p.slide_wt;
+    const int R = wt >> 2;
+    const int u0 = (lane >> 4) * R;
+    const long long n_tiles = (p.n_windows + wt - 1) / wt;
+
+    float4 r[K];
+    float c16[4];
+    if constexpr (F16) {
+        const bool up = (lane & 8) != 0;
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+            c16[s4] = up ? p.coef[4 + s4] : p.coef[s4];
+            r[s4] = p.rot[(s4 + (up ? 4 : 0)) * 16 + j];
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < K; ++k) r[k] = p.rot[k * 16 + j];
+    }
+    constexpr int kChunks = kFoldSlideSegs * 8;  // 16-byte chunks per tile
+    __shared__ __attribute__((aligned(16))) u32x4f lds_s[kPlainWPB * kChunks];
+    u32x4f *wl = lds_s + wave * kChunks;
+
+    const long long stride = (long long)gridDim.x * kPlainWPB;
+    for (long long t = tile_block(p.xcd_swizzle) * kPlainWPB + wave; t < n_tiles; t += stride) {
+        const long long wbase = t * wt;
+        long long bytes = ((p.n_windows - wbase - 1) * p.hop + 1024) * 2;
+        if (bytes > 0x7FFFFFF0LL) bytes = 0x7FFFFFF0LL;
+        __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)(p.pcm + wbase * p.hop), (short)0, (int)bytes, 0x00020000);
+        u32x4f v[kChunks / 64];
+#pragma unroll
+        for (int i = 0; i < kChunks / 64; ++i)  // cached: neighbouring tiles share their edge segments
+            v[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (64 * i + lane) * 16, 0, 0);
+#pragma unroll
+        for (int i = 0; i < kChunks / 64; ++i) wl[64 * i + lane] = v[i];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+        int acc[8];
+        for (int i = 0; i < R; ++i) {
+            const int u = u0 + i;
+            if (i == 0) {
+#pragma unroll
+                for (int q = 0; q < 8; ++q) acc[q] = 0;
+#pragma unroll
+                for (int m2 = 0; m2 < 8; ++m2) {
+                    const u32x4f d = wl[8 * (u * H + 2 * m2 + par) + chunk];
+                    const uint32_t d4[4] = {d.x, d.y, d.z, d.w};
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        acc[2 * q] += (int)(short)(d4[q] & 0xFFFFu);
+                        acc[2 * q + 1] += (int)d4[q] >> 16;
+                    }
+                }
+            } else {
+                if (H & 1) {
+#pragma unroll
+                    for (int q = 0; q < 8; ++q)
+                        acc[q] = __builtin_amdgcn_mov_dpp(acc[q], 0x128, 0xF, 0xF, true);
+                }
+                const int pp = (par + H) & 1;
+                const int base = (u - 1) * H;
+                for (int m2 = 0; 2 * m2 < H; ++m2) {
+                    const int mm = 2 * m2 + pp;
+                    if (mm < H) {
+                        const u32x4f o = wl[8 * (base + mm) + chunk];
+                        const u32x4f nw = wl[8 * (base + 16 + mm) + chunk];
+                        const uint32_t o4[4] = {o.x, o.y, o.z, o.w};
+                        const uint32_t n4[4] = {nw.x, nw.y, nw.z, nw.w};
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            acc[2 * q] += (int)(short)(n4[q] & 0xFFFFu) - (int)(short)(o4[q] & 0xFFFFu);
+                            acc[2 * q + 1] += ((int)n4[q] >> 16) - ((int)o4[q] >> 16);
+                        }
+                    }
+                }
+            }
+            const long long w = wbase + u;
+            fold_decide<K, F16>(acc, r, c16, lane, w, w < p.n_windows, p);
+        }
+        // the next tile's samples overwrite this one's
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
 template <int K, bool NT>
 static const void *fold_kernel_for_t(int log2g, bool f16)
 {
@@ -269,10 +442,19 @@ static const void *fold_kernel_for(int log2g, bool f16, bool nt)
     return nt ? fold_kernel_for_t<K, true>(log2g, f16) : fold_kernel_for_t<K, false>(log2g, f16);
 }
 
-const void *fold_kernel_ptr(int k, int log2g, bool f16, bool nt)
+template <int K>
+static const void *fold_slide_kernel_for(bool f16)
 {
+    if constexpr (K == 8)
+        if (f16) return reinterpret_cast<const void *>(&fold_slide_kernel<8, true>);
+    return reinterpret_cast<const void *>(&fold_slide_kernel<K, false>);
+}
+
+const void *fold_kernel_ptr(int k, int log2g, bool f16, bool nt, bool slide)
+{
+    if (slide && log2g != 4) return nullptr;
     switch (k) {
-#define FSKD_CASE(K) case K: return fold_kernel_for<K>(log2g, f16, nt);
+#define FSKD_CASE(K) case K: return slide ? fold_slide_kernel_for<K>(f16) : fold_kernel_for<K>(log2g, f16, nt);
         FSKD_CASE(1) FSKD_CASE(2) FSKD_CASE(3) FSKD_CASE(4)
         FSKD_CASE(5) FSKD_CASE(6) FSKD_CASE(7) FSKD_CASE(8)
         FSKD_CASE(9) FSKD_CASE(10) FSKD_CASE(11) FSKD_CASE(12)

@@ -425,18 +425,22 @@ int tile_grid(long long n_windows, int log2g, int wpb, int wins_per_tile_overrid
     return (int)blocks;
 }
 
-const void *fold_kernel_ptr(int k, int log2g, bool f16, bool nt);
+const void *fold_kernel_ptr(int k, int log2g, bool f16, bool nt, bool slide);
 
 hipError_t launch_detector(int detector, const GoertzelParams &p, hipStream_t s)
 {
     const bool nt = p.cached == 0;
-    const void *f = detector == kDetFolded    ? fold_kernel_ptr(p.k, p.log2g, p.f16 != 0, nt)
+    const void *f = detector == kDetFolded    ? fold_kernel_ptr(p.k, p.log2g, p.f16 != 0, nt, p.slide_wt > 0)
                   : detector == kDetResidue ? residue_kernel_ptr(p.k, p.log2g, p.dcls != 0, nt)
                                             : kernel_ptr(p.k, p.log2g, p.reinsch != 0, p.slide_wt > 0, nt);
     if (!f) return hipErrorInvalidValue;
-    if (p.slide_wt > 0 && (detector != kDetGoertzel || p.log2g != 4 || p.hop % 64 ||
-                           (p.slide_wt - 1) * (p.hop / 64) + 16 > 64))
-        return hipErrorInvalidValue;  // a tile must hold every segment of its windows
+    // a tile must hold every segment of its windows (fold: 4 R windows in
+    // kFoldSlideSegs segments; plain bank: 64 segments)
+    if (p.slide_wt > 0 && (detector == kDetResidue || p.log2g != 4 || p.hop % 64 || p.hop < 64 ||
+                           (p.slide_wt - 1) * (p.hop / 64) + 16 >
+                               (detector == kDetFolded ? kFoldSlideSegs : 64) ||
+                           (detector == kDetFolded && p.slide_wt % 4)))
+        return hipErrorInvalidValue;
     const size_t lds = detector == kDetResidue ? residue_lds_bytes(p.k, p.log2g) : 0;
     const int wpb = detector == kDetResidue ? kWavesPerBlock : kPlainWPB;
     void *args[] = {const_cast<GoertzelParams *>(&p)};

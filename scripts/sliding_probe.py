@@ -2,9 +2,10 @@
 """Sliding-window (hop < n) throughput of the Goertzel detectors
 over one 2^30-sample int16 stream in HBM: kernel time per launch (HIP events,
 median of 20 after 30 warmup launches), the unique-stream rate (2 GiB / t) and
-the window-bytes rate (n_windows x 2 KiB / t). AUTO takes the segment-shared
-plain bank (SLIDE) at hop = 64 H < n; the folded detector is timed beside it
-for 8-FSK.
+the window-bytes rate (n_windows x 2 KiB / t). At hop = 64 H < n AUTO takes
+the segment-shared plain bank (SLIDE) for 2-FSK and the fold detector's
+segment-shared form for 8-FSK; the other of the two is timed beside each.
+FSKD_NO_SLIDE=1 in the environment times the direct kernels instead.
 
     python scripts/sliding_probe.py [--samples-log2 30]
 """
@@ -34,8 +35,8 @@ def main():
     d_true = torch.empty(src, dtype=torch.uint8, device="cuda")
     A.synth_fsk(cfg0, A.BENCH_SEED, src, 8000, 400, d_pcm, d_true)
     torch.cuda.synchronize()
-    for name, freqs, method in (("fsk2", A.FSK2_FREQS, 0), ("fsk8", A.FSK8_FREQS, 0),
-                                ("fsk8", A.FSK8_FREQS, A.METHOD_FOLDED)):
+    for name, freqs, method in (("fsk2", A.FSK2_FREQS, 0), ("fsk2", A.FSK2_FREQS, A.METHOD_FOLDED),
+                                ("fsk8", A.FSK8_FREQS, 0), ("fsk8", A.FSK8_FREQS, A.METHOD_GOERTZEL)):
         for hop in [int(h) for h in args.hops.split(",")]:
             W = (S - n) // hop + 1
             K = len(freqs)

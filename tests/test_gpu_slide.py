@@ -79,10 +79,12 @@ def test_levels(A, O, torch, amplitude, sigma):
 
 def test_auto_takes_slide_for_overlap(A, torch):
     """AUTO picks the segment-shared plain bank for overlapping windows at
-    hop 64 H (any K; for fold-eligible plans up to hop 128, where it beats
-    the fold); folded / residue stay available explicitly, hop = n keeps the
-    fold."""
+    hop 64 H unless the plan folds (K >= 3 on multiples of 8 bins: the fold
+    detector's own segment-shared form, tests/test_gpu_fold_slide.py);
+    folded / residue stay available explicitly, hop = n keeps the fold."""
     with A.Demodulator(freqs=A.FSK8_FREQS, hop=128) as d:
+        assert d.method == 3
+    with A.Demodulator(freqs=FSK8_ODD, hop=128) as d:
         assert d.method == GOERTZEL
     with A.Demodulator(freqs=A.FSK8_FREQS, hop=256) as d:
         assert d.method == 3
