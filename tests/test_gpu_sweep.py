@@ -224,3 +224,67 @@ def test_random_permuted_plans(A, O, torch, i):
     check_decisions(sym, mag, ref_sym, ref_P, denom)
     if hop == 1024:
         assert posed.mean() >= 0.99
+
+
+N_SLIDE_CASES = 40
+
+
+@pytest.mark.parametrize("i", range(N_SLIDE_CASES))
+def test_random_segment_shared(A, O, torch, i):
+    """The segment-shared paths at n = 1024, hop = 64 H < n:
+    the plain SLIDE (any plan) and the fold detector's running sums (plans on
+    multiples of 8 bins, incl. fold-by-16 plans), drawn with random H, K,
+    tone order, batch size and level; against the oracle with the same bar,
+    and bit-identical to the direct kernels (FSKD_NO_SLIDE=1)."""
+    import os
+    rng = np.random.default_rng(0x511DE + i + SEED_OFFSET)
+    n = 1024
+    kind = ("fold", "fold16", "plain")[i % 3]
+    if kind == "fold16":
+        z0 = rng.choice(np.arange(1, 31) * 16, 4, replace=False)
+        z8 = rng.choice(np.arange(0, 31) * 16 + 8, 4, replace=False)
+        bins = rng.permutation(np.concatenate([z0, z8])).astype(np.float64)
+        method = A.METHOD_FOLDED
+    elif kind == "fold":
+        k = int(rng.integers(1, 17))
+        bins = rng.choice(np.arange(8, 505, 8), k, replace=False).astype(np.float64)
+        method = A.METHOD_FOLDED
+    else:
+        k = int(rng.integers(1, 17))
+        if rng.random() < 0.5:
+            bins = rng.choice(np.arange(2, 510), k, replace=False).astype(np.float64)
+        else:
+            bins = rng.uniform(2.0, 510.0, k)
+        method = A.METHOD_GOERTZEL
+    freqs = tuple(float(b) * FS / n for b in bins)
+    hop = 64 * int(rng.integers(1, 16))
+    W = int(rng.integers(1, 700))
+    amplitude = int(rng.choice([300, 2000, 8000, 32767]))
+    sigma = int(rng.choice([0, 100, 400, 1500]))
+    src = (W - 1) * hop // n + 2
+    pcm, _ = O.synth_fsk(freqs, n, src, 77 + i, amplitude, sigma)
+    flat = pcm.reshape(-1)
+    Wh = min(W, (flat.size - n) // hop + 1)
+    out = []
+    for direct in (False, True):
+        old = os.environ.get("FSKD_NO_SLIDE")
+        if direct:
+            os.environ["FSKD_NO_SLIDE"] = "1"
+        try:
+            with A.Demodulator(n=n, hop=hop, freqs=freqs, method=method) as d:
+                assert d.method == method
+                out.append(d.batch(flat, n_windows=Wh, mags=True))
+        finally:
+            if direct:
+                if old is None:
+                    del os.environ["FSKD_NO_SLIDE"]
+                else:
+                    os.environ["FSKD_NO_SLIDE"] = old
+    (sym, mag), (sym_d, mag_d) = out
+    assert np.array_equal(sym, sym_d), (kind, hop, W)
+    assert np.array_equal(mag.view(np.uint32), mag_d.view(np.uint32)), (kind, hop, W)
+    ref_sym, ref_P = O.goertzel(flat, freqs, n, hop, Wh)
+    denom = mag_denom(ref_P, flat, n, hop)
+    err = (np.abs(mag.astype(np.float64) - ref_P).max(axis=1) / denom).max()
+    assert err <= MAG_TOL, (err, kind, hop, W)
+    check_decisions(sym, mag, ref_sym, ref_P, denom)
