@@ -22,6 +22,7 @@
 // fused into the butterfly that consumes it (fft1024_quad_kernel below); the
 // round-1 kernel with separate products is scripts/fft_quad_r1b.hip.
 #include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 
 #include "demod_internal.h"
@@ -707,10 +708,18 @@ constexpr int kFmtWord3 = 0xFAC | (3 << 12) | (5 << 15);
 // FMT (PF = 0 only): typed buffer loads (16_16 SSCALED) convert both int16
 // halves to fp32 in the texture path instead of 64 VALU converts per group
 // (measured neutral).
+// SPL (with SPEC): 1 = the bin powers go to the slab as the output's own
+// layout (4 windows x 513 floats, contiguous, bin b of window q at float
+// 513 q + b; each lane's pair j lands at its bins by immediate offsets), and
+// the group's live windows leave as one contiguous run of 16-byte stores
+// (9 ds_read_b128 + 9 dwordx4 stores per lane, 1 KiB per wave instruction);
+// 2 = the same with non-temporal stores (the spectrum is written once);
+// 0 = the quad_slot layout, 33 scattered dword stores per lane.
 template <int WPB = 4, int MINW = 4, int PF = 0, bool SPEC = true, bool FMT = false, int AUX = 2,
-          int FUSED = 0, int RD = 0>
+          int FUSED = 0, int RD = 0, int SPL = 0>
 __device__ __attribute__((always_inline)) inline void fft1024_quad_body(const FftParams &p)
 {
+    static_assert(!SPL || SPEC, "SPL: the linear power slab of the spectrum store");
     using namespace quad;
     __shared__ __attribute__((aligned(16))) f2 slab[WPB][kQSlab];
     // RD < 2: tw2 [column slot][v, v2, g0, g0^2, .., g3, g3^2][t], tw3 [j][t];
@@ -745,8 +754,15 @@ __device__ __attribute__((always_inline)) inline void fft1024_quad_body(const Ff
         tw3[tw3_at(j, tt)] = 0.5f * t1024[(tt == 0 && j < 8) ? 16 + 32 * j : tt + 32 * j];
     }
     const int k1b = t == 0 ? 16 : 32 - t;
-    const int myslot = quad_slot(t < p.k ? p.bins[t] : 0);
+    const int mybin = t < p.k ? p.bins[t] : 0;
+    const int myslot = SPL ? q * 513 + mybin : quad_slot(mybin);
     float *pw = reinterpret_cast<float *>(slab[wave]);
+    // SPL: float index of (|X[kP]|^2, |X[512 - kP]|^2) of pair j, as
+    // row base + 32 j and mirror base + 32 (15 - j): lane t has kP = t + 32 j;
+    // lane 0 has kP = 16 + 32 j for j < 8 (like t = 16) and 32 j for j >= 8
+    const int te_lo = t == 0 ? 16 : t;
+    const int spl_a_lo = q * 513 + te_lo, spl_m_lo = q * 513 + 32 - te_lo;
+    const int spl_a_hi = q * 513 + t, spl_m_hi = q * 513 + 32 - t;
     __syncthreads();
 
     const long long n_groups = (p.n_windows + 3) >> 2;
@@ -918,7 +934,13 @@ __device__ __attribute__((always_inline)) inline void fft1024_quad_body(const Ff
                 const f2 im0 = pp_im_h(S0, T0), im1 = pp_im_h(S1, T1);
                 pwr2(pw0, re0, im0, pw1, re1, im1);
             }
-            if constexpr (SPEC) {
+            if constexpr (SPEC && SPL) {
+                const int a = j0 < 8 ? spl_a_lo : spl_a_hi, m = j0 < 8 ? spl_m_lo : spl_m_hi;
+                pw[a + 32 * j0] = pw0.x;
+                pw[m + 32 * (15 - j0)] = pw0.y;
+                pw[a + 32 * j1] = pw1.x;
+                pw[m + 32 * (15 - j1)] = pw1.y;
+            } else if constexpr (SPEC) {
                 ps[16 * j0] = pw0;
                 ps[16 * j1] = pw1;
             } else {
@@ -937,14 +959,19 @@ __device__ __attribute__((always_inline)) inline void fft1024_quad_body(const Ff
         int arg = t < p.k ? t : kMaxTones;  // kMaxTones: this lane holds no tone
         if constexpr (SPEC) {
             if (l0) {
-                pq[512] = px.x;
-                pq[513] = px.y;
+                if constexpr (SPL) {
+                    pw[q * 513] = px.x;
+                    pw[q * 513 + 512] = px.y;
+                } else {
+                    pq[512] = px.x;
+                    pq[513] = px.y;
+                }
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             // 5. tone pick (as fft1024_quad_kernel step 4)
-            if (t < p.k) pk = pq[myslot];
+            if (t < p.k) pk = SPL ? pw[myslot] : pq[myslot];
             if (live && t < p.k && p.mag) p.mag[w * p.k + t] = pk;
         } else {
             // 5. tone pick from registers: tone i's power sits in lane
@@ -969,7 +996,28 @@ __device__ __attribute__((always_inline)) inline void fft1024_quad_body(const Ff
         // window_sum.h (powers >= 0, so their bits order as unsigned)
         arg = (int)ws_argmax<false>(__float_as_uint(pk), arg < kMaxTones, arg);
         if (live && t == 0) p.sym[w] = (uint8_t)arg;
-        if constexpr (SPEC) {
+        if constexpr (SPEC && SPL) {
+            if (p.spec) {
+                // the group's live windows: floats [0, L) of the slab = the
+                // output run from window 4 g (16-byte aligned: 4 g x 513 x 4 B)
+                const long long wg = 4 * g;
+                const int L = 513 * (int)(p.n_windows - wg < 4 ? p.n_windows - wg : 4);
+                float *dst = p.spec + wg * 513;
+                const f4 *src4 = reinterpret_cast<const f4 *>(pw);
+#pragma unroll
+                for (int i = 0; i < 9; ++i) {
+                    const int f = 64 * i + lane;
+                    if (4 * f + 4 <= L) {
+                        if constexpr (SPL == 2)
+                            __builtin_nontemporal_store(src4[f], reinterpret_cast<f4 *>(dst + 4 * f));
+                        else
+                            *reinterpret_cast<f4 *>(dst + 4 * f) = src4[f];
+                    } else if (4 * f < L) {
+                        for (int e = 4 * f; e < L; ++e) dst[e] = pw[e];
+                    }
+                }
+            }
+        } else if constexpr (SPEC) {
             if (p.spec && live) {
                 float *so = p.spec + w * 513;
                 for (int i = t; i < 513; i += 16) so[i] = pq[quad_slot(i)];
@@ -981,11 +1029,11 @@ __device__ __attribute__((always_inline)) inline void fft1024_quad_body(const Ff
 }
 
 template <int WPB = 4, int MINW = 4, int PF = 0, bool SPEC = true, bool FMT = false, int AUX = 2,
-          int FUSED = 0>
+          int FUSED = 0, int SPL = 0>
 __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MINW > 0 ? MINW : 1)))
 void fft1024_quad_kernel(FftParams p)
 {
-    fft1024_quad_body<WPB, MINW, PF, SPEC, FMT, AUX, FUSED, 0>(p);
+    fft1024_quad_body<WPB, MINW, PF, SPEC, FMT, AUX, FUSED, 0, SPL>(p);
 }
 
 // (a device-code attribute: the host pass of hipcc does not know the feature)
@@ -1009,14 +1057,16 @@ FSKD_NO_LDS_PAIRING void fft1024_quad_kernel_r64(FftParams p)
 
 // Persistent grid: as many blocks as fit the chip, each wave strides over
 // groups of 4 windows (the LDS twiddle tables are built once per block).
-template <int WPB, int MINW, int PF, bool SPEC, bool FMT = false, int AUX = 2, int FUSED = 0, int RD = 0>
+template <int WPB, int MINW, int PF, bool SPEC, bool FMT = false, int AUX = 2, int FUSED = 0, int RD = 0,
+          int SPL = 0>
 hipError_t launch_fft_quad_t(const FftParams &p, hipStream_t s)
 {
     void (*kern)(FftParams);
+    static_assert(!(RD > 0 && SPL > 0), "SPL: fft1024_quad_kernel only");
     if constexpr (RD > 0)
         kern = fft1024_quad_kernel_r64<WPB, MINW, PF, SPEC, FMT, AUX, FUSED, RD>;
     else
-        kern = fft1024_quad_kernel<WPB, MINW, PF, SPEC, FMT, AUX, FUSED>;
+        kern = fft1024_quad_kernel<WPB, MINW, PF, SPEC, FMT, AUX, FUSED, SPL>;
     int dev = 0, cus = 256, per_cu = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
@@ -1041,12 +1091,22 @@ hipError_t launch_fft_quad_t(const FftParams &p, hipStream_t s)
 // DFT-32's trivial pieces and the post-pass pairs as single asm blocks
 // (-3 to -4.5 % at hop 256, -2 to -4 % at hop 1024 against separate blocks;
 // scripts/fft_probe.hip, profiles/round2/fft_fused/).
+// The full-spectrum store (p.spec) goes through the linear slab with
+// non-temporal 16-byte stores (SPL 2) when the output is 16-byte aligned,
+// else through the quad_slot slab. Hop 256, 4.19 M windows, 8.6 GB of
+// spectrum: quad_slot slab 4.00-4.12 ms, linear slab 2.85-2.89 ms, + nt
+// 2.73 ms; a write-only fill of the same buffer 1.45 ms, the detector
+// without the spectrum 1.71-1.80 ms (scripts/spectrum_probe.py,
+// profiles/round2/spec_lin/).
 hipError_t launch_fft_quad(const FftParams &p, hipStream_t s)
 {
+    const bool lin = p.spec && ((uintptr_t)p.spec & 15) == 0;
     if (p.hop < 1024)
-        return p.spec ? launch_fft_quad_t<4, 4, 0, true, false, 0, 4>(p, s)
+        return lin ? launch_fft_quad_t<4, 4, 0, true, false, 0, 4, 0, 2>(p, s)
+             : p.spec ? launch_fft_quad_t<4, 4, 0, true, false, 0, 4>(p, s)
                       : launch_fft_quad_t<4, 4, 0, false, false, 0, 4>(p, s);
-    return p.spec ? launch_fft_quad_t<4, 4, 0, true, false, 2, 4>(p, s)
+    return lin ? launch_fft_quad_t<4, 4, 0, true, false, 2, 4, 0, 2>(p, s)
+         : p.spec ? launch_fft_quad_t<4, 4, 0, true, false, 2, 4>(p, s)
                   : launch_fft_quad_t<4, 4, 0, false, false, 2, 4>(p, s);
 }
 

@@ -750,3 +750,41 @@ def test_tone_bank_vs_reference_kissfft(A, method, plan, torch):
     err = np.abs(mag.astype(np.float64) - Pr[:, bins]).max(axis=1) / energy
     assert err.max() <= REF_FFT_TOL, err
     assert (sym[rows] == np.argmax(Pr[rows][:, bins], axis=1)).all()
+
+
+@pytest.mark.parametrize("W", [1, 3, 4, 5, 7, 257, 4097])
+@pytest.mark.parametrize("hop", [1024, 256])
+def test_fft_spectrum_store_paths_agree(A, O, torch, W, hop):
+    """The full-spectrum store has two paths: a 16-byte-aligned output goes
+    through the linear power slab and leaves as 16-byte stores of the group's
+    contiguous run (partial last group: scalar tail), any other alignment
+    through the quad_slot slab with dword stores. Both carry the same powers:
+    equal bits, and equal to the oracle's spectrum on a sample."""
+    n = 1024
+    src = (W - 1) * hop // n + 2
+    pcm, _ = O.synth_fsk(A.FSK8_FREQS, n, src, 31 + W, 8000, 400)
+    flat = pcm.reshape(-1)
+    Wh = min(W, (flat.size - n) // hop + 1)
+    d_pcm = torch.from_numpy(flat.copy()).cuda()
+    with A.Demodulator(freqs=A.FSK8_FREQS, hop=hop, method=FFT) as d:
+        outs = []
+        for off in (0, 1):   # off 1: the spectrum 4 bytes past a 16-byte boundary
+            buf = torch.full((Wh * 513 + 8,), -1.0, dtype=torch.float32, device="cuda")
+            spec = buf[off:off + Wh * 513]
+            d_sym = torch.empty(Wh, dtype=torch.uint8, device="cuda")
+            d_mag = torch.empty((Wh, 8), dtype=torch.float32, device="cuda")
+            d.batch_spectrum_async(d_pcm, Wh, d_sym, d_mag, spec)
+            torch.cuda.synchronize()
+            b = buf.cpu().numpy()
+            assert (b[:off] == -1.0).all() and (b[off + Wh * 513:] == -1.0).all()
+            outs.append((d_sym.cpu().numpy(), d_mag.cpu().numpy(), spec.cpu().numpy()))
+    (s0, m0, p0), (s1, m1, p1) = outs
+    assert np.array_equal(s0, s1) and np.array_equal(m0.view(np.uint32), m1.view(np.uint32))
+    assert np.array_equal(p0.view(np.uint32), p1.view(np.uint32))
+    spec = p0.reshape(Wh, 513)
+    idx = np.unique(np.concatenate([np.arange(min(Wh, 8)), np.arange(max(0, Wh - 8), Wh)]))
+    full = np.stack([O.fft_power(flat[i * hop:i * hop + n]) for i in idx])
+    assert _spec_err(spec[idx], full) <= MAG_TOL
+    ref_sym, ref_P = O.fft_demod(flat, A.FSK8_FREQS, n, hop)
+    assert (s0 == ref_sym[:Wh]).all()
+    assert rel_err(m0, ref_P[:Wh]) <= MAG_TOL
