@@ -25,7 +25,8 @@ histogram SURVEY §7 asks for, at sigma 400 and at the sigma 2000 stress level).
 
 At N = 1 the default run also measures configs[2] (8-FSK) and configs[3]
 (sliding FFT, hop 256) with the same steps/warmup and reports them under
-"fsk8" and "fft_hop256" (no CPU baseline for those).
+"fsk8" and "fft_hop256", plus configs[3] with the full 513-bin spectrum
+stored as "fft_hop256_spectrum" (no CPU baseline for those).
 
 Defaults: 200 timed steps after 20 warmup steps (the warmup is at least 64
 launches, MIN_WARMUP), so each config keeps the GPU busy for 0.1-0.5 s
@@ -219,7 +220,7 @@ def free_port() -> int:
 
 
 def run_config(A, D, torch, dist, args, config, rank, world, local, use_dist, steps, warmup,
-               plan="survey", method_name="auto", hop_fft=256, no_mags=False):
+               plan="survey", method_name="auto", hop_fft=256, no_mags=False, spectrum=False):
     """Allocate, synthesise, warm up and time one workload; returns a dict."""
     freqs = A.FSK8_FREQS if config == "fsk8" else A.FSK2_FREQS
     if config == "fsk8" and plan == "odd":
@@ -248,6 +249,9 @@ def run_config(A, D, torch, dist, args, config, rank, world, local, use_dist, st
     d_true = torch.empty(W, dtype=torch.uint8, device=dev)
     d_sym = torch.empty(n_eval, dtype=torch.uint8, device=dev)
     d_mag = None if no_mags else torch.empty((n_eval, K), dtype=torch.float32, device=dev)
+    # config 4 with the full |X[b]|^2 spectrum stored (513 floats per window)
+    d_spec = (torch.empty((n_eval, 513), dtype=torch.float32, device=dev)
+              if (spectrum and config == "fft") else None)
     A.synth_fsk(cfg, A.BENCH_SEED, W, 8000, 400, d_pcm, d_true, w0=w0)
     torch.cuda.synchronize()
     demod = A.Demodulator(cfg)
@@ -293,7 +297,11 @@ def run_config(A, D, torch, dist, args, config, rank, world, local, use_dist, st
             comp.wait_event(gdone[slot])
         if ev is not None:
             ev[0].record(comp)
-        demod.batch_async(d_pcm, n_eval, slots[slot], d_mag, stream=comp.cuda_stream)
+        if d_spec is not None:
+            demod.batch_spectrum_async(d_pcm, n_eval, slots[slot], d_mag, d_spec,
+                                       stream=comp.cuda_stream)
+        else:
+            demod.batch_async(d_pcm, n_eval, slots[slot], d_mag, stream=comp.cuda_stream)
         if ev is not None:
             ev[1].record(comp)
         if dev_framing:
@@ -454,7 +462,8 @@ def run_config(A, D, torch, dist, args, config, rank, world, local, use_dist, st
     # dispatches per step: batches with > ~10 MiB of output run as slices
     # (demod_batch_launches); kernel_ms brackets the whole batch
     launches = demod.batch_launches(n_eval, not no_mags)
-    alg_bytes = W * 2 * n + n_eval * (1 + (0 if no_mags else 4 * K))
+    alg_bytes = W * 2 * n + n_eval * (1 + (0 if no_mags else 4 * K) +
+                                      (513 * 4 if d_spec is not None else 0))
     achieved = alg_bytes / (kernel_ms / 1e3) / 1e9
     kname = ("fft1024_quad_kernel<4>" if demod.method == A.METHOD_FFT else
              ("fold_tile_kernel<%d,4>" if demod.method == A.METHOD_FOLDED
@@ -485,6 +494,7 @@ def run_config(A, D, torch, dist, args, config, rank, world, local, use_dist, st
             "launches_per_step": launches,
         },
         "d_pcm": d_pcm, "d_sym": d_sym, "d_mag": d_mag, "cfg": cfg,
+        "spectrum": d_spec is not None,
     }
     if dev_framing or use_dist:
         # per-step cost above the detector kernel: the frame
@@ -513,7 +523,9 @@ def run_config(A, D, torch, dist, args, config, rank, world, local, use_dist, st
 def summary(r) -> dict:
     """The extra-config entry of the bench line."""
     out = {"workload": (f"configs[2]: 8-FSK Goertzel, {r['W']} x 1024 windows" if r["config"] == "fsk8"
-                        else f"configs[3]: sliding 1024-pt FFT, hop {r['hop']}, {r['n_eval']} windows"),
+                        else f"configs[3]: sliding 1024-pt FFT, hop {r['hop']}, {r['n_eval']} windows"
+                        + (", full |X[b]|^2 spectrum stored (513 floats per window)"
+                           if r.get("spectrum") else "")),
            "detector": r["detector"], "ms_per_step": round(r["ms_per_step"], 4),
            "kernel_ms": round(r["kernel_ms"], 4),
            "kernel_ms_p10_p50_p90": [round(float(np.percentile(r["kts"], q)), 4) for q in (10, 50, 90)],
@@ -522,9 +534,13 @@ def summary(r) -> dict:
            "launches_per_step": r["roofline"]["launches_per_step"]}
     if r["config"] == "fft":
         out["roofline"] = r["roofline_valu"]
+        # HBM: the unique input stream plus the outputs (with the spectrum:
+        # 2052 B per window written, the larger stream)
         out["roofline_hbm_frac"] = round(
-            r["W"] * 2048 / (r["kernel_ms"] / 1e3) / 1e9 / HBM_PEAK_GBPS, 4)
-        out["hbm_traffic"] = r["roofline"]["traffic"]
+            r["roofline"]["alg_bytes_per_launch"] / (r["kernel_ms"] / 1e3) / 1e9 / HBM_PEAK_GBPS, 4)
+        out["hbm_alg_bytes_per_launch"] = r["roofline"]["alg_bytes_per_launch"]
+        if not r.get("spectrum"):
+            out["hbm_traffic"] = r["roofline"]["traffic"]
     else:
         out["roofline"] = r["roofline"]
     return out
@@ -543,6 +559,8 @@ def main():
     ap.add_argument("--hop", type=int, default=256, help="window advance for --config fft")
     ap.add_argument("--windows", type=int, default=1 << 20, help="windows per GPU (fsk2/fsk8)")
     ap.add_argument("--no-mags", action="store_true", help="symbols only")
+    ap.add_argument("--spectrum", action="store_true",
+                    help="--config fft: also store the full |X[b]|^2 spectrum (513 floats per window)")
     ap.add_argument("--method", choices=["auto", "goertzel", "folded", "residue"], default="auto")
     ap.add_argument("--plan", choices=["survey", "odd"], default="survey",
                     help="fsk8 tone plan: survey = SURVEY §8 (1500 + 375 i Hz, multiples of 8 "
@@ -586,7 +604,7 @@ def main():
     A, D = load_pkg()
     r = run_config(A, D, torch, dist, args, args.config, rank, world, local, use_dist,
                    args.steps, args.warmup, plan=args.plan, method_name=args.method,
-                   hop_fft=args.hop, no_mags=args.no_mags)
+                   hop_fft=args.hop, no_mags=args.no_mags, spectrum=args.spectrum)
 
     extras = {}
     if (world == 1 and args.config == "fsk2" and not args.no_extras and not args.force_dist
@@ -594,9 +612,10 @@ def main():
         # configs[2] and configs[3], same steps / warmup, in their own buffers
         # (the main run's stay alive for the CPU baseline's parity sample)
         main_keep = {k: r[k] for k in ("d_pcm", "d_sym", "d_mag")}
-        for key, cfgname in (("fsk8", "fsk8"), ("fft_hop256", "fft")):
+        for key, cfgname, spec in (("fsk8", "fsk8", False), ("fft_hop256", "fft", False),
+                                   ("fft_hop256_spectrum", "fft", True)):
             rr = run_config(A, D, torch, dist, args, cfgname, rank, world, local, False,
-                            args.steps, args.warmup, hop_fft=256)
+                            args.steps, args.warmup, hop_fft=256, spectrum=spec)
             extras[key] = summary(rr)
             del rr
             torch.cuda.empty_cache()
