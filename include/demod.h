@@ -62,10 +62,10 @@ extern "C" {
 #define DEMOD_CH_DOWNMIX  2   /* x = (L + R) >> 1 (arithmetic shift) */
 
 /* detector selection */
-#define DEMOD_METHOD_AUTO      0 /* GOERTZEL for overlapping windows at n = 1024,
-                                    hop = 64 H <= 128; otherwise FOLDED when eligible
-                                    and k >= 3, else RESIDUE when eligible and
-                                    k >= 5, else GOERTZEL */
+#define DEMOD_METHOD_AUTO      0 /* FOLDED when eligible and k >= 3; else RESIDUE
+                                    when eligible and k >= 5 (except overlapping
+                                    windows at n = 1024, hop = 64 H <= 128, which
+                                    take GOERTZEL); else GOERTZEL */
 #define DEMOD_METHOD_GOERTZEL  1 /* per-window Goertzel tone bank over all n samples
                                     (n = 1024, hop = 64 H < n: 64-sample segments
                                     shared by the windows that contain them, same
@@ -74,7 +74,10 @@ extern "C" {
                                     over the tone bins round(f*n/fs) */
 #define DEMOD_METHOD_FOLDED    3 /* Goertzel over the window folded to n/8 samples:
                                     exact when every tone is on a multiple of 8
-                                    bins (f*n/fs integer, divisible by 8) */
+                                    bins (f*n/fs integer, divisible by 8); at
+                                    n = 1024, hop = 64 H < n the folded sums are
+                                    carried from window to window (same results
+                                    as evaluating each window alone) */
 #define DEMOD_METHOD_RESIDUE   4 /* Goertzel over the window folded to n/8 samples per
                                     residue class of the bin mod 8: exact when every
                                     tone is on an integer bin (f*n/fs integer) */
@@ -165,7 +168,9 @@ int demod_batch_async(demod_t *st, const int16_t *d_pcm, size_t n_windows,
 /*
  * Full-spectrum variant of demod_batch_async for DEMOD_METHOD_FFT handles:
  * additionally writes |X[b]|^2, b = 0..n/2, to d_spectrum[W][n/2 + 1]
- * (nullable). Other handles return DEMOD_UNIMPLEMENTED.
+ * (nullable). Other handles return DEMOD_UNIMPLEMENTED. Any float alignment
+ * is accepted; a 16-byte-aligned d_spectrum takes the faster store path
+ * (whole 16-byte stores of each 4-window group's rows).
  */
 int demod_batch_spectrum_async(demod_t *st, const int16_t *d_pcm, size_t n_windows,
                                uint8_t *d_symbols, float *d_mags, float *d_spectrum,
