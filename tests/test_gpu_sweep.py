@@ -68,6 +68,13 @@ def draw_case(i, fft_nonint=False):
             b = np.sort(rng.uniform(2.0, half - 2.0, k))
             if k == 1 or np.diff(b).min() >= 2.0:
                 break
+        else:
+            # no draw kept the tones 2 bins apart (many tones in a short
+            # window): spread them evenly instead, with a random sub-bin offset,
+            # so the plan stays resolvable (tones a fraction of a bin apart
+            # make most decisions ties, which the case is not testing)
+            step = (half - 4.0) / k
+            b = 2.0 + step * (np.arange(k) + 0.5) + rng.uniform(-0.25, 0.25) * min(step - 2.0, 1.0)
     else:
         b = np.sort(rng.choice(slots, k, replace=False)).astype(np.float64)
     freqs = tuple(float(x) * FS / n for x in rng.permutation(b))
@@ -109,8 +116,12 @@ def test_random_case(A, O, torch, i):
     # windows inside one symbol have one clear winner; windows straddling two
     # symbols (hop not a multiple of n) split the power between two tones, and
     # evenly (a structural tie) wherever a window starts half a symbol in:
-    # every 8th window at n = 1024, hop = 384
-    assert posed.mean() >= (0.99 if hop % n == 0 else 0.75), c
+    # every 8th window at n = 1024, hop = 384, every other one at hop = n / 2.
+    # The posed fraction is taken over the other windows (the structural ties
+    # are still held to the decision rule by check_decisions below).
+    half_in = (np.arange(Wh) * hop) % n == n // 2
+    if (~half_in).any():
+        assert posed[~half_in].mean() >= (0.99 if hop % n == 0 else 0.75), c
     bad = np.flatnonzero(posed & (sym != ref_sym))
     assert bad.size == 0, (bad[:8], c)
     check_decisions(sym, mag, ref_sym, ref_P, denom)
