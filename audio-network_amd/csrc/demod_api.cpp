@@ -198,7 +198,8 @@ static int init_device_state(demod_t *st)
     // goertzel.hip) and the fold detector runs its folded sums forward from
     // window to window (fold_slide_kernel, fold.hip). The
     // residue detector has no segment-shared form, so AUTO keeps the plain
-    // SLIDE over it up to hop 128 (8-FSK: 0.89 vs 1.23 ms at hop 128).
+    // SLIDE over it up to hop 384 (8-FSK on bins 32 + 9 i: 0.70 vs 0.90 ms at
+    // hop 256, 0.63 vs 0.64 at 384, 0.58 vs 0.52 at 512).
     // FSKD_NO_SLIDE=1 (measurement switch for probes) runs the direct kernels.
     const char *no_slide_env = std::getenv("FSKD_NO_SLIDE");
     const bool slide = lg == 4 && c.hop < c.n && c.hop % 64 == 0 &&
@@ -208,7 +209,7 @@ static int init_device_state(demod_t *st)
     else if (c.method == DEMOD_METHOD_RESIDUE) st->detector = kDetResidue;
     else if (c.method == DEMOD_METHOD_AUTO) {
         if (c.k >= 3 && fold_eligible(c)) st->detector = kDetFolded;
-        else if (!(slide && c.hop <= 128) && c.k >= 5 && residue_eligible(c))
+        else if (!(slide && c.hop <= 384) && c.k >= 5 && residue_eligible(c))
             st->detector = kDetResidue;
     }
     if (c.method == DEMOD_METHOD_FFT) {

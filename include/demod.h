@@ -64,7 +64,7 @@ extern "C" {
 /* detector selection */
 #define DEMOD_METHOD_AUTO      0 /* FOLDED when eligible and k >= 3; else RESIDUE
                                     when eligible and k >= 5 (except overlapping
-                                    windows at n = 1024, hop = 64 H <= 128, which
+                                    windows at n = 1024, hop = 64 H <= 384, which
                                     take GOERTZEL); else GOERTZEL */
 #define DEMOD_METHOD_GOERTZEL  1 /* per-window Goertzel tone bank over all n samples
                                     (n = 1024, hop = 64 H < n: 64-sample segments

@@ -22,6 +22,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--samples-log2", type=int, default=30)
     ap.add_argument("--hops", default="1024,1000,512,256,200,128")
+    ap.add_argument("--plans", default="fsk2,fsk8", help="comma list of fsk2, fsk8, fsk8odd")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -35,8 +36,11 @@ def main():
     d_true = torch.empty(src, dtype=torch.uint8, device="cuda")
     A.synth_fsk(cfg0, A.BENCH_SEED, src, 8000, 400, d_pcm, d_true)
     torch.cuda.synchronize()
-    for name, freqs, method in (("fsk2", A.FSK2_FREQS, 0), ("fsk2", A.FSK2_FREQS, A.METHOD_FOLDED),
-                                ("fsk8", A.FSK8_FREQS, 0), ("fsk8", A.FSK8_FREQS, A.METHOD_GOERTZEL)):
+    odd = tuple(46.875 * (32 + 9 * i) for i in range(8))   # integer bins, every residue class
+    cases = {"fsk2": (("fsk2", A.FSK2_FREQS, 0), ("fsk2", A.FSK2_FREQS, A.METHOD_FOLDED)),
+             "fsk8": (("fsk8", A.FSK8_FREQS, 0), ("fsk8", A.FSK8_FREQS, A.METHOD_GOERTZEL)),
+             "fsk8odd": (("fsk8odd", odd, A.METHOD_GOERTZEL), ("fsk8odd", odd, A.METHOD_RESIDUE))}
+    for name, freqs, method in [c for key in args.plans.split(",") for c in cases[key]]:
         for hop in [int(h) for h in args.hops.split(",")]:
             W = (S - n) // hop + 1
             K = len(freqs)

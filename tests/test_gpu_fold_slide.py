@@ -128,7 +128,7 @@ def test_extreme_samples(A, torch):
 def test_auto_takes_fold_slide(A, torch):
     """AUTO: fold-eligible plans with K >= 3 take the fold detector at every
     hop (its segment-shared form at hop = 64 H); other integer-bin plans keep
-    the plain SLIDE up to hop 128."""
+    the plain SLIDE up to hop 384."""
     for hop in (64, 128, 256, 512, 1024, 200):
         with A.Demodulator(freqs=A.FSK8_FREQS, hop=hop) as d:
             assert d.method == FOLDED, hop

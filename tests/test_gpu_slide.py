@@ -84,8 +84,11 @@ def test_auto_takes_slide_for_overlap(A, torch):
     folded / residue stay available explicitly, hop = n keeps the fold."""
     with A.Demodulator(freqs=A.FSK8_FREQS, hop=128) as d:
         assert d.method == 3
-    with A.Demodulator(freqs=FSK8_ODD, hop=128) as d:
-        assert d.method == GOERTZEL
+    for hop in (128, 256, 384):     # residue plans: SLIDE up to hop 384
+        with A.Demodulator(freqs=FSK8_ODD, hop=hop) as d:
+            assert d.method == GOERTZEL, hop
+    with A.Demodulator(freqs=FSK8_ODD, hop=512) as d:
+        assert d.method == 4
     with A.Demodulator(freqs=A.FSK8_FREQS, hop=256) as d:
         assert d.method == 3
     with A.Demodulator(freqs=A.FSK2_FREQS, hop=512) as d:
