@@ -169,6 +169,12 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "demod_to_transmitter_decode": (ctypes.c_int, [_P, _SZ, ctypes.POINTER(DemodReceiverInfo),
                                                        ctypes.POINTER(DemodReceiverError),
                                                        ctypes.POINTER(_SZ)]),
+        "demod_streams_create": (_P, [ctypes.POINTER(DemodCfg), _SZ, ctypes.POINTER(ctypes.c_int)]),
+        "demod_streams_destroy": (None, [_P]),
+        "demod_streams_reset": (ctypes.c_int, [_P, _SZ]),
+        "demod_streams_pending": (ctypes.c_int, [_P, _SZ]),
+        "demod_streams_max_symbols": (ctypes.c_longlong, [_P, _P]),
+        "demod_streams_push": (ctypes.c_int, [_P, _P, _P, _P, _P, _SZ, _P]),
         "demod_synth_fsk": (ctypes.c_int, [ctypes.POINTER(DemodCfg), ctypes.c_uint64,
                                            ctypes.c_uint64, _SZ, ctypes.c_int, ctypes.c_int,
                                            _P, _P, _P]),
@@ -401,6 +407,81 @@ class Demodulator:
         if rc < 0:
             raise DemodError(rc, "demod_batch_spectrum_async")
         return rc
+
+
+class Streams:
+    """demod_streams_t: n_streams independent streams behind one detector,
+    one batch per push (include/demod.h, "many streams, one launch")."""
+
+    def __init__(self, n_streams: int, cfg: Optional[DemodCfg] = None, **kw):
+        self._lib = load_library()
+        self.cfg = cfg if cfg is not None else make_cfg(**kw)
+        self.n_streams = int(n_streams)
+        err = ctypes.c_int(0)
+        h = self._lib.demod_streams_create(ctypes.byref(self.cfg), self.n_streams, ctypes.byref(err))
+        if not h:
+            raise DemodError(err.value, "demod_streams_create")
+        self._h = h
+
+    @property
+    def k(self) -> int:
+        return int(self.cfg.k)
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._lib.demod_streams_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def reset(self, stream: int) -> None:
+        rc = self._lib.demod_streams_reset(self._h, int(stream))
+        if rc < 0:
+            raise DemodError(rc, "demod_streams_reset")
+
+    def pending(self, stream: int) -> int:
+        rc = self._lib.demod_streams_pending(self._h, int(stream))
+        if rc < 0:
+            raise DemodError(rc, "demod_streams_pending")
+        return rc
+
+    def push(self, packets, mags: bool = False, cap: Optional[int] = None):
+        """packets: one int16 array (interleaved if stereo) or None per stream.
+        Returns the per-stream symbol arrays (and magnitude arrays)."""
+        if len(packets) != self.n_streams:
+            raise DemodError(DEMOD_BAD_ARG, "one packet (or None) per stream")
+        ch = int(self.cfg.channels)
+        arrs = [np.ascontiguousarray(p, dtype=np.int16) if p is not None else None for p in packets]
+        frames = np.array([0 if a is None else a.size // ch for a in arrs], dtype=np.uintp)
+        for a in arrs:
+            if a is not None and a.size % ch:
+                raise DemodError(DEMOD_BAD_ARG, "pcm length not a multiple of channels")
+        ptrs = (ctypes.c_void_p * self.n_streams)(*[None if a is None or a.size == 0 else a.ctypes.data
+                                                    for a in arrs])
+        if cap is None:
+            cap = int(self._lib.demod_streams_max_symbols(self._h, frames.ctypes.data))
+        sym = np.empty(max(cap, 1), dtype=np.uint8)
+        mag = np.empty((max(cap, 1), self.k), dtype=np.float32) if mags else None
+        counts = np.zeros(self.n_streams, dtype=np.uint32)
+        rc = self._lib.demod_streams_push(self._h, ctypes.cast(ptrs, ctypes.c_void_p), frames.ctypes.data,
+                                          _ptr(sym), _ptr(mag), cap, counts.ctypes.data)
+        if rc < 0:
+            raise DemodError(rc, "demod_streams_push")
+        edges = np.concatenate([[0], np.cumsum(counts.astype(np.int64))])
+        out_s = [sym[edges[i]:edges[i + 1]] for i in range(self.n_streams)]
+        if not mags:
+            return out_s
+        return out_s, [mag[edges[i]:edges[i + 1]] for i in range(self.n_streams)]
 
 
 def synth_fsk(cfg: DemodCfg, seed: int, n_windows: int, amplitude: int, sigma: int,

@@ -723,6 +723,21 @@ int demod_batch_spectrum_async(demod_t *st, const int16_t *d_pcm, size_t n_windo
     return enqueue_fft(st, d_pcm, n_windows, d_symbols, d_mags, d_spectrum, (hipStream_t)stream);
 }
 
+// The mono samples of n_frames frames (cfg.channels interleaved): the
+// channel cfg.channel_mode selects, or (L + R) >> 1.
+static void mono_frames(const demod_cfg_t &c, const int16_t *pcm, size_t n_frames, int16_t *dst)
+{
+    if (c.channels == 1) {
+        if (n_frames) std::memcpy(dst, pcm, n_frames * sizeof(int16_t));
+    } else if (c.channel_mode == DEMOD_CH_DOWNMIX) {
+        for (size_t i = 0; i < n_frames; ++i)
+            dst[i] = (int16_t)(((int32_t)pcm[2 * i] + (int32_t)pcm[2 * i + 1]) >> 1);
+    } else {
+        const int ch = c.channel_mode == DEMOD_CH_RIGHT ? 1 : 0;
+        for (size_t i = 0; i < n_frames; ++i) dst[i] = pcm[2 * i + ch];
+    }
+}
+
 int demodulate_mags(demod_t *st, const int16_t *pcm, size_t n_frames, uint8_t *symbols,
                     float *mags, size_t max_symbols)
 {
@@ -756,16 +771,7 @@ int demodulate_mags(demod_t *st, const int16_t *pcm, size_t n_frames, uint8_t *s
         m = st->scratch.data();
     }
     if (have) std::memcpy(m, st->carry.data(), have * sizeof(int16_t));
-    int16_t *dst = m + have;
-    if (c.channels == 1) {
-        if (n_frames) std::memcpy(dst, pcm, n_frames * sizeof(int16_t));
-    } else if (c.channel_mode == DEMOD_CH_DOWNMIX) {
-        for (size_t i = 0; i < n_frames; ++i)
-            dst[i] = (int16_t)(((int32_t)pcm[2 * i] + (int32_t)pcm[2 * i + 1]) >> 1);
-    } else {
-        const int ch = c.channel_mode == DEMOD_CH_RIGHT ? 1 : 0;
-        for (size_t i = 0; i < n_frames; ++i) dst[i] = pcm[2 * i + ch];
-    }
+    mono_frames(c, pcm, n_frames, m + have);
     if (W) {
         const size_t used = (W - 1) * c.hop + c.n;
         int rc = run_host(st, m, used, W, symbols, mags);
@@ -781,6 +787,171 @@ int demodulate(demod_t *st, const int16_t *pcm, size_t n_frames, uint8_t *symbol
                size_t max_symbols)
 {
     return demodulate_mags(st, pcm, n_frames, symbols, nullptr, max_symbols);
+}
+
+}  // extern "C"
+
+// Many streams behind one detector handle. The handle is created with
+// hop = n: a push copies every complete window of every stream, n samples
+// each, into one contiguous batch of independent windows (for hop < n the
+// overlapping samples are copied once per window), so one H2D copy, one
+// detector launch and one D2H copy serve all streams. Each window is
+// evaluated alone, as the direct kernels evaluate it, which is bit-identical
+// to the segment-shared kernels a per-stream handle would use at hop < n.
+struct demod_streams {
+    demod_cfg_t cfg;                      // the streams' configuration (hop as given)
+    demod_t *st = nullptr;                // detector handle, hop = n, mono
+    std::vector<std::vector<int16_t>> carry;
+    std::vector<size_t> skip;             // lead-in frames still to drop per stream
+};
+
+extern "C" {
+
+demod_streams_t *demod_streams_create(const demod_cfg_t *cfg, size_t n_streams, int *error)
+{
+    int rc = validate(cfg);
+    if (rc == DEMOD_OK && (n_streams < 1 || n_streams > ((size_t)1 << 24))) rc = DEMOD_BAD_ARG;
+    if (rc != DEMOD_OK) {
+        if (error) *error = rc;
+        return nullptr;
+    }
+    demod_streams_t *ms = new (std::nothrow) demod_streams();
+    if (!ms) {
+        if (error) *error = DEMOD_ALLOC_FAIL;
+        return nullptr;
+    }
+    ms->cfg = *cfg;
+    demod_cfg_t dc = *cfg;
+    dc.hop = dc.n;
+    dc.channels = 1;
+    dc.channel_mode = DEMOD_CH_LEFT;
+    dc.lead_in = 0;
+    ms->st = demod_create(&dc, &rc);
+    if (!ms->st) {
+        delete ms;
+        if (error) *error = rc;
+        return nullptr;
+    }
+    try {
+        ms->carry.resize(n_streams);
+        ms->skip.assign(n_streams, cfg->lead_in);
+    } catch (...) {
+        demod_destroy(ms->st);
+        delete ms;
+        if (error) *error = DEMOD_ALLOC_FAIL;
+        return nullptr;
+    }
+    if (error) *error = DEMOD_OK;
+    return ms;
+}
+
+void demod_streams_destroy(demod_streams_t *ms)
+{
+    if (!ms) return;
+    demod_destroy(ms->st);
+    delete ms;
+}
+
+int demod_streams_reset(demod_streams_t *ms, size_t stream)
+{
+    if (!ms || stream >= ms->carry.size()) return DEMOD_BAD_ARG;
+    ms->carry[stream].clear();
+    ms->skip[stream] = ms->cfg.lead_in;
+    return DEMOD_OK;
+}
+
+int demod_streams_pending(const demod_streams_t *ms, size_t stream)
+{
+    if (!ms || stream >= ms->carry.size()) return DEMOD_BAD_ARG;
+    return (int)ms->carry[stream].size();
+}
+
+static size_t streams_windows(const demod_streams_t *ms, size_t s, size_t n_frames)
+{
+    const size_t fresh = n_frames > ms->skip[s] ? n_frames - ms->skip[s] : 0;
+    const size_t total = ms->carry[s].size() + fresh;
+    return total < ms->cfg.n ? 0 : (total - ms->cfg.n) / ms->cfg.hop + 1;
+}
+
+long long demod_streams_max_symbols(const demod_streams_t *ms, const size_t *n_frames)
+{
+    if (!ms || !n_frames) return DEMOD_BAD_ARG;
+    long long w = 0;
+    for (size_t s = 0; s < ms->carry.size(); ++s) w += (long long)streams_windows(ms, s, n_frames[s]);
+    return w;
+}
+
+int demod_streams_push(demod_streams_t *ms, const int16_t *const *pcm, const size_t *n_frames,
+                       uint8_t *symbols, float *mags, size_t cap, uint32_t *counts)
+{
+    if (!ms || !n_frames || !counts) return DEMOD_BAD_ARG;
+    const demod_cfg_t &c = ms->cfg;
+    const size_t S = ms->carry.size(), n = c.n, hop = c.hop;
+    if (!pcm)
+        for (size_t s = 0; s < S; ++s)
+            if (n_frames[s]) return DEMOD_BAD_ARG;
+    size_t W = 0;
+    for (size_t s = 0; s < S; ++s) {
+        if (n_frames[s] && !pcm[s]) return DEMOD_BAD_ARG;
+        if (n_frames[s] > ((size_t)1 << 40)) return DEMOD_BAD_ARG;
+        W += streams_windows(ms, s, n_frames[s]);
+    }
+    if (W > cap) return DEMOD_BUFFER_TOO_SMALL;
+    if (W > 0x7FFFFFFF || W * n > ((size_t)1 << 40)) return DEMOD_BAD_ARG;
+    if (W && !symbols) return DEMOD_BAD_ARG;
+    demod_t *st = ms->st;
+    DeviceGuard guard(st->device);
+    HIP_TRY(guard.err);
+    // the streams' mono samples appended to their carries (undone on failure)
+    std::vector<size_t> old(S);
+    try {
+        for (size_t s = 0; s < S; ++s) {
+            old[s] = ms->carry[s].size();
+            const size_t drop = std::min(ms->skip[s], n_frames[s]);
+            const size_t f = n_frames[s] - drop;
+            ms->carry[s].resize(old[s] + f);
+            if (f) mono_frames(c, pcm[s] + drop * c.channels, f, ms->carry[s].data() + old[s]);
+        }
+    } catch (...) {
+        for (size_t s = 0; s < S; ++s) ms->carry[s].resize(std::min(old[s], ms->carry[s].size()));
+        return DEMOD_ALLOC_FAIL;
+    }
+    auto undo = [&]() {
+        for (size_t s = 0; s < S; ++s) ms->carry[s].resize(old[s]);
+    };
+    if (W) {
+        // every complete window, n samples each, stream after stream, in the
+        // pinned staging buffer the host path copies from
+        int rc = ensure_host(st, std::max(W * n, kSmallHostSamples), kSmallHostSamples / 8);
+        if (rc != DEMOD_OK) {
+            undo();
+            return rc;
+        }
+        int16_t *b = st->h_in;
+        for (size_t s = 0; s < S; ++s) {
+            const size_t w = ms->carry[s].size() < n ? 0 : (ms->carry[s].size() - n) / hop + 1;
+            const int16_t *src = ms->carry[s].data();
+            if (hop == n) {
+                std::memcpy(b, src, w * n * sizeof(int16_t));
+                b += w * n;
+            } else {
+                for (size_t i = 0; i < w; ++i, b += n) std::memcpy(b, src + i * hop, n * sizeof(int16_t));
+            }
+        }
+        rc = run_host(st, st->h_in, W * n, W, symbols, mags);
+        if (rc < 0) {
+            undo();
+            return rc;
+        }
+    }
+    for (size_t s = 0; s < S; ++s) {
+        const size_t total = ms->carry[s].size();
+        const size_t w = total < n ? 0 : (total - n) / hop + 1;
+        counts[s] = (uint32_t)w;
+        ms->carry[s].erase(ms->carry[s].begin(), ms->carry[s].begin() + (ptrdiff_t)(w * hop));
+        ms->skip[s] -= std::min(ms->skip[s], n_frames[s]);
+    }
+    return (int)W;
 }
 
 int demod_synth_fsk(const demod_cfg_t *cfg, uint64_t seed, uint64_t w0, size_t n_windows,

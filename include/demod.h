@@ -176,6 +176,45 @@ int demod_batch_spectrum_async(demod_t *st, const int16_t *d_pcm, size_t n_windo
                                uint8_t *d_symbols, float *d_mags, float *d_spectrum,
                                void *stream);
 
+/* ---- many streams, one launch (config 5 as a service) ----------------- */
+/*
+ * n_streams independent streams that share one configuration, each behaving
+ * exactly like its own demod_t from that cfg (its own carry buffer and
+ * lead-in). The reference runs one decoder per device (playback.cpp:157-165);
+ * a receiver of many streams would otherwise make one demodulate() call --
+ * one H2D copy, one kernel launch, one D2H copy -- per stream per packet.
+ * demod_streams_push takes one packet per stream and demodulates every
+ * complete window of every stream in ONE batch: one copy in, one detector
+ * launch, one copy out.
+ */
+typedef struct demod_streams demod_streams_t;
+
+/* NULL on failure, *error set. n_streams >= 1. */
+demod_streams_t *demod_streams_create(const demod_cfg_t *cfg, size_t n_streams, int *error);
+void demod_streams_destroy(demod_streams_t *ms);
+
+/* demod_reset for one stream (drop its carry, re-arm cfg.lead_in). */
+int demod_streams_reset(demod_streams_t *ms, size_t stream);
+
+/* Mono samples stream `stream` carries between pushes. */
+int demod_streams_pending(const demod_streams_t *ms, size_t stream);
+
+/* Upper bound on the symbols the next push with these packet sizes emits. */
+long long demod_streams_max_symbols(const demod_streams_t *ms, const size_t *n_frames);
+
+/*
+ * pcm[i]: host pointer to n_frames[i] frames of stream i (`channels`
+ * interleaved int16, as for demodulate; NULL allowed when n_frames[i] == 0).
+ * Symbols of stream 0, then stream 1, ... are written to symbols[0..];
+ * counts[i] receives the number stream i emitted; mags (nullable, host)
+ * receives k floats |X_k|^2 per symbol in the same order. Returns the total,
+ * or a negative code; if cap is too small nothing is consumed and
+ * DEMOD_BUFFER_TOO_SMALL is returned. Symbols and magnitudes equal what
+ * per-stream demodulate() calls would return.
+ */
+int demod_streams_push(demod_streams_t *ms, const int16_t *const *pcm, const size_t *n_frames,
+                       uint8_t *symbols, float *mags, size_t cap, uint32_t *counts);
+
 /* ---- ip.proto framing (ToReceiver{AudioData{bytes}}, delimited) ------- */
 
 /* Bytes demod_frame_encode needs for a payload of len bytes. */

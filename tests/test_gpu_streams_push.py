@@ -1,0 +1,144 @@
+"""Many streams behind one detector (demod_streams_push, include/demod.h):
+each stream must behave exactly like its own demod_t from the same cfg fed
+the same packets — same symbols, same magnitudes (bits: every window is
+evaluated alone in both cases), same pending count — and match the oracle's
+streaming restatement (oracle.Stream), while all streams' windows go through
+one batch per push.
+"""
+import numpy as np
+import pytest
+
+from decision import check_decisions
+
+pytestmark = pytest.mark.gpu
+
+MAG_TOL = 1e-5
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch as t
+    if not t.cuda.is_available():
+        pytest.skip("no GPU visible")
+    return t
+
+
+def streams_vs_single(A, O, n_streams, freqs, hop, channels=1, mode=0, lead_in=0, method=0,
+                      rounds=12, seed=0, max_frames=4000):
+    n = 1024
+    rng = np.random.default_rng(seed)
+    # each stream its own seeded signal, long enough for the rounds
+    per = rounds * max_frames // n + 2
+    sig = []
+    for s in range(n_streams):
+        L, _ = O.synth_fsk(freqs, n, per, 1000 * seed + s, 8000, 400)
+        if channels == 2:
+            R, _ = O.synth_fsk(freqs, n, per, 1000 * seed + s + 500, 8000, 400)
+            sig.append(np.stack([L.reshape(-1), R.reshape(-1)], axis=1).reshape(-1))
+        else:
+            sig.append(L.reshape(-1))
+    pos = [0] * n_streams
+    kw = dict(freqs=freqs, hop=hop, channels=channels, channel_mode=mode, lead_in=lead_in,
+              method=method)
+    singles = [A.Demodulator(**kw) for _ in range(n_streams)]
+    refs = [O.Stream(freqs, n=n, hop=hop, channels=channels, channel_mode=mode, lead_in=lead_in)
+            for _ in range(n_streams)]
+    total = 0
+    with A.Streams(n_streams, **kw) as ms:
+        for r in range(rounds):
+            pkts = []
+            for s in range(n_streams):
+                f = int(rng.choice([0, 1, 7, 2880, int(rng.integers(1, max_frames))]))
+                if rng.random() < 0.15:
+                    pkts.append(None)
+                    continue
+                a = sig[s][pos[s] * channels:(pos[s] + f) * channels]
+                pos[s] += f
+                pkts.append(a)
+            got_s, got_m = ms.push(pkts, mags=True)
+            for s in range(n_streams):
+                a = pkts[s] if pkts[s] is not None else np.zeros(0, np.int16)
+                one_s, one_m = singles[s].demodulate(a, mags=True)
+                ref_s, ref_P = refs[s].push(a)
+                assert np.array_equal(got_s[s], one_s), (r, s)
+                assert np.array_equal(got_m[s].view(np.uint32), one_m.view(np.uint32)), (r, s)
+                assert got_s[s].size == ref_s.size, (r, s)
+                if ref_s.size:
+                    err = (np.abs(got_m[s].astype(np.float64) - ref_P).max(axis=1) /
+                           np.maximum(ref_P.max(axis=1), 1e-30)).max()
+                    if hop == n:
+                        assert err <= MAG_TOL, (r, s, err)
+                        check_decisions(got_s[s], got_m[s], ref_s, ref_P)
+                    else:
+                        assert (got_s[s] == ref_s).mean() > 0.9
+                assert ms.pending(s) == singles[s].pending() == refs[s].pending(), (r, s)
+                total += got_s[s].size
+    for d in singles:
+        d.close()
+    assert total > 0
+
+
+@pytest.mark.parametrize("n_streams", [1, 3, 64])
+def test_mono_hop_n(A, O, torch, n_streams):
+    streams_vs_single(A, O, n_streams, A.FSK2_FREQS, 1024, seed=n_streams)
+
+
+@pytest.mark.parametrize("hop", [256, 512, 1000, 64])
+def test_overlapping_windows(A, O, torch, hop):
+    """hop < n: each window's n samples are copied into the batch; the
+    per-stream handles run the segment-shared kernels (bit-identical)."""
+    streams_vs_single(A, O, 9, A.FSK8_FREQS, hop, seed=hop)
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_stereo_and_lead_in(A, O, torch, mode):
+    streams_vs_single(A, O, 7, A.FSK8_FREQS, 1024, channels=2, mode=mode,
+                      lead_in=A.DEMOD_OPUS_LOOKAHEAD, seed=10 + mode)
+
+
+@pytest.mark.parametrize("method", [2, 4, 1])
+def test_other_detectors(A, O, torch, method):
+    f = A.FSK2_FREQS if method != 4 else tuple(46.875 * (32 + 9 * i) for i in range(8))
+    streams_vs_single(A, O, 5, f, 1024, method=method, seed=20 + method, rounds=6)
+
+
+def test_reset_buffer_too_small_and_errors(A, O, torch):
+    """reset drops one stream's carry and re-arms its lead-in; a cap below
+    the push's window count consumes nothing."""
+    n = 1024
+    pcm, _ = O.synth_fsk(A.FSK2_FREQS, n, 8, 5, 8000, 400)
+    flat = pcm.reshape(-1)
+    with A.Streams(2, freqs=A.FSK2_FREQS, lead_in=100) as ms:
+        with pytest.raises(A.DemodError) as e:
+            ms.push([flat[:3000], flat[:3000]], cap=3)
+        assert e.value.code == A.DEMOD_BUFFER_TOO_SMALL
+        assert ms.pending(0) == 0 and ms.pending(1) == 0
+        out = ms.push([flat[:3000], flat[:500]])
+        assert [o.size for o in out] == [2, 0]
+        assert ms.pending(0) == 3000 - 100 - 2048 and ms.pending(1) == 400
+        ms.reset(1)
+        assert ms.pending(1) == 0
+        out = ms.push([None, flat[:1124]])
+        assert [o.size for o in out] == [0, 1]      # lead-in of 100 re-armed
+        with pytest.raises(A.DemodError):
+            ms.push([flat[:10]])                     # one packet per stream
+        with pytest.raises(A.DemodError):
+            ms.reset(2)
+    with pytest.raises(A.DemodError):
+        A.Streams(0, freqs=A.FSK2_FREQS)
+
+
+def test_many_streams_one_push(A, O, torch):
+    """1024 streams x one 60 ms packet (2880 frames) per push, as a receiver
+    of config 5's streams would call it: symbols equal the oracle's stream of
+    every stream."""
+    n, S = 1024, 1024
+    pcm, _ = O.synth_fsk(A.FSK2_FREQS, n, 3 * S, 77, 8000, 400)
+    flat = pcm.reshape(S, -1)
+    refs = [O.Stream(A.FSK2_FREQS, n=n) for _ in range(S)]
+    with A.Streams(S, freqs=A.FSK2_FREQS) as ms:
+        for r in range(2):
+            pk = [flat[s, r * 1440:(r + 1) * 1440] for s in range(S)]
+            got = ms.push(pk)
+            for s in range(S):
+                assert np.array_equal(got[s], refs[s].push(pk[s])[0]), (r, s)
