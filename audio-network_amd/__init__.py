@@ -139,6 +139,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "demod_destroy": (None, [_P]),
         "demod_reset": (ctypes.c_int, [_P]),
         "demod_pending": (ctypes.c_int, [_P]),
+        "demod_slide_windows": (ctypes.c_int, [_P]),
         "demod_method": (ctypes.c_int, [_P]),
         "demod_max_symbols": (ctypes.c_int, [_P, _SZ]),
         "demod_batch_launches": (ctypes.c_int, [_P, _SZ, ctypes.c_int]),
@@ -321,6 +322,11 @@ class Demodulator:
 
     def pending(self) -> int:
         return int(self._lib.demod_pending(self._h))
+
+    @property
+    def slide_windows(self) -> int:
+        """Windows per tile of the segment-shared kernel (0: windows alone)."""
+        return int(self._lib.demod_slide_windows(self._h))
 
     def max_symbols(self, n_frames: int) -> int:
         return int(self._lib.demod_max_symbols(self._h, n_frames))

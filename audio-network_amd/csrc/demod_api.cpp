@@ -424,6 +424,12 @@ int demod_method(const demod_t *st)
                                        : DEMOD_METHOD_GOERTZEL;
 }
 
+int demod_slide_windows(const demod_t *st)
+{
+    if (!st) return DEMOD_BAD_ARG;
+    return st->slide_wt;
+}
+
 int demod_pending(const demod_t *st)
 {
     if (!st) return DEMOD_BAD_ARG;

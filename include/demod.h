@@ -118,6 +118,13 @@ int demod_reset(demod_t *st);
 /* Detector the handle runs (DEMOD_METHOD_GOERTZEL / _FOLDED / _RESIDUE / _FFT). */
 int demod_method(const demod_t *st);
 
+/* Overlapping windows (n = 1024, hop = 64 H < n): the windows per tile the
+ * detector's segment-shared kernel evaluates together (plain bank or fold,
+ * DESIGN.md §4.8); 0 when every window is evaluated alone. The results are
+ * the same either way. (FSKD_NO_SLIDE=1 in the environment at demod_create
+ * turns the shared kernels off, for measurements.) */
+int demod_slide_windows(const demod_t *st);
+
 /* Number of mono samples currently carried between demodulate() calls. */
 int demod_pending(const demod_t *st);
 

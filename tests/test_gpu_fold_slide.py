@@ -52,6 +52,8 @@ def demod(A, freqs, hop, flat, W, direct=False, method=FOLDED):
     try:
         with A.Demodulator(n=1024, hop=hop, freqs=freqs, method=method) as d:
             assert d.method == FOLDED
+            # the two runs really take different kernels
+            assert d.slide_windows == (0 if (direct or hop % 64) else wt(hop))
             return d.batch(flat, n_windows=W, mags=True)
     finally:
         if direct:
@@ -177,6 +179,7 @@ def test_large_stream_hop256(A, torch):
             mag = torch.empty(W * K, dtype=torch.float32, device="cuda")
             with A.Demodulator(freqs=A.FSK8_FREQS, hop=hop) as d:
                 assert d.method == FOLDED
+                assert (d.slide_windows == 0) == direct
                 d.batch_device(d_pcm, W, sym, mag)
             torch.cuda.synchronize()
             out.append((sym, mag))

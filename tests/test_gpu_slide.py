@@ -43,6 +43,7 @@ def run(A, O, freqs, hop, W, seed, amplitude=8000, sigma=400, method=GOERTZEL):
     Wh = min(W, (flat.size - n) // hop + 1)
     with A.Demodulator(n=n, hop=hop, freqs=freqs, method=method) as d:
         assert d.method == GOERTZEL
+        assert d.slide_windows == (wt(hop) if hop % 64 == 0 and hop < n else 0)
         sym, mag = d.batch(flat, n_windows=Wh, mags=True)
     ref_sym, ref_P = O.goertzel(flat, freqs, n, hop, Wh)
     denom = np.maximum(ref_P.max(axis=1), 1e-30)

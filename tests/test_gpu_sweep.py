@@ -284,6 +284,7 @@ def test_random_segment_shared(A, O, torch, i):
         try:
             with A.Demodulator(n=n, hop=hop, freqs=freqs, method=method) as d:
                 assert d.method == method
+                assert (d.slide_windows == 0) == direct
                 out.append(d.batch(flat, n_windows=Wh, mags=True))
         finally:
             if direct:
