@@ -470,7 +470,8 @@ def run_config(A, D, torch, dist, args, config, rank, world, local, use_dist, st
               else "residue_tile_kernel<%d,4>" if demod.method == A.METHOD_RESIDUE
               else "goertzel_tile_kernel<%d,4>") % K)
     pmc_name = ("fsk8odd" if (config == "fsk8" and plan == "odd") else
-                "fft1024" if (config == "fft" and hop == 1024) else config)
+                ("fft1024" if hop == 1024 else "fft") + ("spec" if d_spec is not None else "")
+                if config == "fft" else config)
     r = {
         "config": config, "freqs": freqs, "K": K, "n": n, "hop": hop, "W": W, "n_eval": n_eval,
         "total_windows": total_windows, "ms_per_step": ms_per_step, "kernel_ms": kernel_ms,
@@ -539,8 +540,7 @@ def summary(r) -> dict:
         out["roofline_hbm_frac"] = round(
             r["roofline"]["alg_bytes_per_launch"] / (r["kernel_ms"] / 1e3) / 1e9 / HBM_PEAK_GBPS, 4)
         out["hbm_alg_bytes_per_launch"] = r["roofline"]["alg_bytes_per_launch"]
-        if not r.get("spectrum"):
-            out["hbm_traffic"] = r["roofline"]["traffic"]
+        out["hbm_traffic"] = r["roofline"]["traffic"]
     else:
         out["roofline"] = r["roofline"]
     return out
