@@ -67,6 +67,23 @@ int main(void)
         CHECK(demod_pending(st) == 2880 - 2048, "carry %d", demod_pending(st));
         demod_destroy(st);
         printf("gpu demodulate: symbol %d OK\n", out[0]);
+
+        /* the same packet on three streams at once (one batch), the middle
+         * stream silent this round */
+        demod_streams_t *ms = demod_streams_create(&cfg, 3, &err);
+        CHECK(ms != NULL, "demod_streams_create: %s", demod_strerror(err));
+        const int16_t *pk[3] = {stereo, NULL, stereo};
+        const size_t nf[3] = {2880, 0, 2880};
+        uint8_t all[8];
+        uint32_t counts[3];
+        CHECK(demod_streams_max_symbols(ms, nf) == 4, "streams bound");
+        n = demod_streams_push(ms, pk, nf, all, NULL, sizeof all, counts);
+        CHECK(n == 4 && counts[0] == 2 && counts[1] == 0 && counts[2] == 2, "streams push %d", n);
+        CHECK(all[0] == truth && all[2] == truth, "streams symbols %d %d", all[0], all[2]);
+        CHECK(demod_streams_pending(ms, 0) == 2880 - 2048 && demod_streams_pending(ms, 1) == 0,
+              "streams carry");
+        demod_streams_destroy(ms);
+        printf("gpu demod_streams_push: 3 streams OK\n");
     }
 
     /* framing: 100 symbols -> ToReceiver frames -> back */

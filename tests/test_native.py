@@ -26,3 +26,4 @@ def test_config1_native_gpu_branch():
     r = _build_and_run()
     assert r.returncode == 0, r.stdout + r.stderr
     assert "gpu demodulate: symbol" in r.stdout
+    assert "gpu demod_streams_push: 3 streams OK" in r.stdout
