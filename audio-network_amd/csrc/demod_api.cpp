@@ -797,18 +797,24 @@ int demodulate(demod_t *st, const int16_t *pcm, size_t n_frames, uint8_t *symbol
 
 }  // extern "C"
 
-// Many streams behind one detector handle. The handle is created with
-// hop = n: a push copies every complete window of every stream, n samples
-// each, into one contiguous batch of independent windows (for hop < n the
-// overlapping samples are copied once per window), so one H2D copy, one
-// detector launch and one D2H copy serve all streams. Each window is
-// evaluated alone, as the direct kernels evaluate it, which is bit-identical
-// to the segment-shared kernels a per-stream handle would use at hop < n.
+// Many streams behind one detector handle (mono, the streams' n and hop). A
+// push lays the streams' runs of complete windows end to end in one batch,
+// each run starting on a multiple of hop, so the batch is an ordinary
+// hop-strided window sequence: stream s's windows are batch windows
+// first[s] .. first[s] + W_s - 1, and the ceil(L_s / hop) - W_s windows that
+// start inside its run but end past it (n / hop - 1 of them when hop divides
+// n; none at hop = n) straddle into the next run and are computed and
+// dropped. One H2D copy of each run (the overlapping samples once), one
+// detector launch (at hop = 64 H the segment-shared kernels, as a per-stream
+// handle would run) and one D2H copy serve all streams.
 struct demod_streams {
-    demod_cfg_t cfg;                      // the streams' configuration (hop as given)
-    demod_t *st = nullptr;                // detector handle, hop = n, mono
+    demod_cfg_t cfg;                      // the streams' configuration
+    demod_t *st = nullptr;                // detector handle: same n, hop, tones; mono
     std::vector<std::vector<int16_t>> carry;
     std::vector<size_t> skip;             // lead-in frames still to drop per stream
+    std::vector<size_t> first;            // per push: batch window of each stream's first
+    std::vector<uint8_t> sym;             // per push: batch symbols / magnitudes
+    std::vector<float> mag;
 };
 
 extern "C" {
@@ -828,7 +834,6 @@ demod_streams_t *demod_streams_create(const demod_cfg_t *cfg, size_t n_streams, 
     }
     ms->cfg = *cfg;
     demod_cfg_t dc = *cfg;
-    dc.hop = dc.n;
     dc.channels = 1;
     dc.channel_mode = DEMOD_CH_LEFT;
     dc.lead_in = 0;
@@ -841,6 +846,7 @@ demod_streams_t *demod_streams_create(const demod_cfg_t *cfg, size_t n_streams, 
     try {
         ms->carry.resize(n_streams);
         ms->skip.assign(n_streams, cfg->lead_in);
+        ms->first.assign(n_streams, 0);
     } catch (...) {
         demod_destroy(ms->st);
         delete ms;
@@ -926,28 +932,55 @@ int demod_streams_push(demod_streams_t *ms, const int16_t *const *pcm, const siz
         for (size_t s = 0; s < S; ++s) ms->carry[s].resize(old[s]);
     };
     if (W) {
-        // every complete window, n samples each, stream after stream, in the
-        // pinned staging buffer the host path copies from
-        int rc = ensure_host(st, std::max(W * n, kSmallHostSamples), kSmallHostSamples / 8);
+        // the streams' runs of complete windows end to end, each starting on a
+        // multiple of hop, in the pinned staging buffer the host path copies from
+        size_t Wb = 0;
+        for (size_t s = 0; s < S; ++s) {
+            const size_t total = ms->carry[s].size();
+            const size_t w = total < n ? 0 : (total - n) / hop + 1;
+            ms->first[s] = Wb;
+            if (w) Wb += ((w - 1) * hop + n + hop - 1) / hop;  // ceil(L_s / hop)
+        }
+        const size_t samples = (Wb - 1) * hop + n;  // the last run ends exactly here or earlier
+        int rc = ensure_host(st, std::max(Wb * hop + n, kSmallHostSamples), kSmallHostSamples / 8);
         if (rc != DEMOD_OK) {
             undo();
             return rc;
         }
-        int16_t *b = st->h_in;
-        for (size_t s = 0; s < S; ++s) {
-            const size_t w = ms->carry[s].size() < n ? 0 : (ms->carry[s].size() - n) / hop + 1;
-            const int16_t *src = ms->carry[s].data();
-            if (hop == n) {
-                std::memcpy(b, src, w * n * sizeof(int16_t));
-                b += w * n;
-            } else {
-                for (size_t i = 0; i < w; ++i, b += n) std::memcpy(b, src + i * hop, n * sizeof(int16_t));
-            }
+        try {
+            ms->sym.resize(Wb);
+            if (mags) ms->mag.resize(Wb * c.k);
+        } catch (...) {
+            undo();
+            return DEMOD_ALLOC_FAIL;
         }
-        rc = run_host(st, st->h_in, W * n, W, symbols, mags);
+        for (size_t s = 0; s < S; ++s) {
+            const size_t total = ms->carry[s].size();
+            const size_t w = total < n ? 0 : (total - n) / hop + 1;
+            if (!w) continue;
+            const size_t L = (w - 1) * hop + n, span = (L + hop - 1) / hop * hop;
+            int16_t *b = st->h_in + ms->first[s] * hop;
+            std::memcpy(b, ms->carry[s].data(), L * sizeof(int16_t));
+            // the straddling windows read up to the next run's start: keep
+            // the gap defined (their results are dropped)
+            if (span > L) std::memset(b + L, 0, (span - L) * sizeof(int16_t));
+        }
+        rc = run_host(st, st->h_in, samples, Wb, ms->sym.data(), mags ? ms->mag.data() : nullptr);
         if (rc < 0) {
             undo();
             return rc;
+        }
+        uint8_t *so = symbols;
+        float *mo = mags;
+        for (size_t s = 0; s < S; ++s) {
+            const size_t total = ms->carry[s].size();
+            const size_t w = total < n ? 0 : (total - n) / hop + 1;
+            std::memcpy(so, ms->sym.data() + ms->first[s], w);
+            so += w;
+            if (mags) {
+                std::memcpy(mo, ms->mag.data() + ms->first[s] * c.k, w * c.k * sizeof(float));
+                mo += w * c.k;
+            }
         }
     }
     for (size_t s = 0; s < S; ++s) {

@@ -192,7 +192,9 @@ int demod_batch_spectrum_async(demod_t *st, const int16_t *d_pcm, size_t n_windo
  * one H2D copy, one kernel launch, one D2H copy -- per stream per packet.
  * demod_streams_push takes one packet per stream and demodulates every
  * complete window of every stream in ONE batch: one copy in, one detector
- * launch, one copy out.
+ * launch, one copy out (the streams' runs laid end to end on hop
+ * boundaries; windows that would straddle two runs are computed and
+ * dropped).
  */
 typedef struct demod_streams demod_streams_t;
 
