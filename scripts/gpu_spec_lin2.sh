@@ -1,5 +1,7 @@
 # Spectrum store: linear slab with plain vs nt 16-byte stores, and a
-# write-only fill of the same buffer as the write reference.
+# write-only fill of the same buffer as the write reference. (Run when
+# launch_fft_quad read FSKD_SPL_NT to pick the nt variant; nt shipped and the
+# switch is gone, so both passes now run the shipped kernel.)
 set -o pipefail
 export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
