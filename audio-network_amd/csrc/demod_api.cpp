@@ -36,7 +36,7 @@ struct demod {
     float coef[kMaxTones] = {};
     float sgn[kMaxTones] = {};  // plain detector, Reinsch form: sign of cos(w_k)
     bool reinsch = false;       // plain detector: Reinsch-modified recurrence
-    bool dcls = false;          // residue detector: compile-time classes, slots permuted
+    int dcls = 0;               // residue detector: compile-time class pattern (residue.hip DC), slots permuted
     bool f16 = false;           // fold detector: fold by 16, slots permuted (Z0 tones, Z8 tones)
     unsigned long long perm = 0;  // DCLS: nibble s = tone index of kernel slot s
     int zcls[kMaxTones] = {};   // residue detector: class each tone reads
@@ -259,28 +259,37 @@ static int init_device_state(demod_t *st)
     // share a class (conjugates), class 0 carries (Z0, Z4)
     static const int kCls[8] = {0, 1, 3, 2, 0, 2, 3, 1};
     static const double kGam[8] = {0, 1, -1, 1, 0, -1, 1, -1};
-    // Residue detector, DCLS (residue.hip): at n = 1024 and K = 8 or 16 with
-    // K / 4 tones in every class (e.g. 8 tones on an odd bin spacing hit every
-    // residue once), kernel tone slot s holds tone slot_tone[s] with
-    // (s / 2) % 4 = its class, so the kernel selects classes at compile time
-    // (no LDS class file); the window_sum epilogue maps slots back (perm).
+    // Residue detector, compile-time classes (residue.hip DC): at n = 1024 and
+    // K = 8 or 16, kernel tone slot s holds tone slot_tone[s] with a fixed
+    // slot -> class pattern, so the kernel selects classes at compile time (no
+    // LDS class file) and forms only the classes it reads; the window_sum
+    // epilogue maps slots back (perm). Mode 1: K / 4 tones in every class
+    // (class (s / 2) % 4; e.g. 8 tones on an odd bin spacing hit every residue
+    // once); 2: half the tones in class 0 and half in class 3 (slots < K / 2
+    // class 0; even spacings 2 and 6); 3: every tone in class 0; 4: every tone
+    // in class 3. Other plans keep the LDS class file (mode 0).
     std::vector<uint32_t> slot_tone(c.k);
     for (uint32_t sl = 0; sl < c.k; ++sl) slot_tone[sl] = sl;
-    st->dcls = false;
+    st->dcls = 0;
     st->perm = 0;
     if (residue && st->log2g == 4 && (c.k == 8 || c.k == 16)) {
         std::vector<uint32_t> by_cls[4];
         for (uint32_t k = 0; k < c.k; ++k) by_cls[kCls[integer_bin(c, k) % 8]].push_back(k);
-        bool balanced = true;
-        for (int cl = 0; cl < 4; ++cl) balanced = balanced && by_cls[cl].size() == c.k / 4;
-        if (balanced) {
+        size_t cnt[4];
+        for (int cl = 0; cl < 4; ++cl) cnt[cl] = by_cls[cl].size();
+        const size_t K = c.k;
+        if (cnt[0] == K / 4 && cnt[1] == K / 4 && cnt[2] == K / 4 && cnt[3] == K / 4) st->dcls = 1;
+        else if (cnt[0] == K / 2 && cnt[3] == K / 2) st->dcls = 2;
+        else if (cnt[0] == K) st->dcls = 3;
+        else if (cnt[3] == K) st->dcls = 4;
+        if (st->dcls) {
             size_t next[4] = {0, 0, 0, 0};
             for (uint32_t sl = 0; sl < c.k; ++sl) {
-                const int cl = (int)((sl / 2) % 4);
+                const int cl = st->dcls == 1 ? (int)((sl / 2) % 4)
+                             : st->dcls == 2 ? (sl < K / 2 ? 0 : 3) : st->dcls == 3 ? 0 : 3;
                 slot_tone[sl] = by_cls[cl][next[cl]++];
                 st->perm |= (unsigned long long)slot_tone[sl] << (4 * sl);
             }
-            st->dcls = true;
         }
     }
     // Fold detector, F16 (fold.hip): n = 1024, K = 8 on multiples of 8 bins
@@ -527,7 +536,7 @@ static int enqueue_batch(demod_t *st, const int16_t *d_pcm, size_t n_windows, ui
         p.zcls[k] = st->zcls[k];
     }
     p.reinsch = st->reinsch ? 1 : 0;
-    p.dcls = st->dcls ? 1 : 0;
+    p.dcls = st->dcls;
     p.f16 = st->f16 ? 1 : 0;
     p.perm = st->perm;
     p.slide_wt = st->slide_wt;

@@ -33,7 +33,7 @@ struct GoertzelParams {
     float coef[kMaxTones];   // 2 cos(w_k); reinsch: lambda_k = 2 cos(w_k) - 2 sgn_k
     float sgn[kMaxTones];    // reinsch: sign of cos(w_k) (+1 / -1)
     int reinsch;             // goertzel.hip: Reinsch-modified recurrence (tones near 0 / fs/2)
-    int dcls;                // residue.hip: tone slot s reads class (s / 2) % 4 from registers
+    int dcls;                // residue.hip: compile-time slot -> class pattern (DC, 0 = LDS class file)
     unsigned long long perm; // DCLS / F16: nibble s = the host's index of tone slot s
     int f16;                 // fold.hip: fold by 16 (K = 8, four tones each on Z0 / Z8)
     int zcls[kMaxTones];     // residue.hip: residue class (0..3) tone k reads
@@ -106,7 +106,7 @@ constexpr int kDetResidue = 4;   // residue.hip: per-residue-class folding (any 
 
 hipError_t launch_detector(int detector, const GoertzelParams &p, hipStream_t s);
 // residue.hip: rotation table is [k][g][2] float4 {C1, C2}, {C3, C4}
-const void *residue_kernel_ptr(int k, int log2g, bool dcls = false, bool nt = true);
+const void *residue_kernel_ptr(int k, int log2g, int dcls = 0, bool nt = true);
 size_t residue_lds_bytes(int k, int log2g, int qp = 2);
 int tile_grid(long long n_windows, int log2g, int wpb = kWavesPerBlock, int wins_per_tile = 0);
 hipError_t synth_prepare();  // upload the sine table to the current device (once, locked)

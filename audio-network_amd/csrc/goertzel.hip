@@ -431,7 +431,7 @@ hipError_t launch_detector(int detector, const GoertzelParams &p, hipStream_t s)
 {
     const bool nt = p.cached == 0;
     const void *f = detector == kDetFolded    ? fold_kernel_ptr(p.k, p.log2g, p.f16 != 0, nt, p.slide_wt > 0)
-                  : detector == kDetResidue ? residue_kernel_ptr(p.k, p.log2g, p.dcls != 0, nt)
+                  : detector == kDetResidue ? residue_kernel_ptr(p.k, p.log2g, p.dcls, nt)
                                             : kernel_ptr(p.k, p.log2g, p.reinsch != 0, p.slide_wt > 0, nt);
     if (!f) return hipErrorInvalidValue;
     // a tile must hold every segment of its windows (fold: 4 R windows in

@@ -111,6 +111,41 @@ __device__ __forceinline__ void residue_classes_asm(f2 p02, f2 p46, f2 p13, f2 p
         : [p02] "v"(p02), [p46] "v"(p46), [p13] "v"(p13), [p57] "v"(p57), [kk] "s"(kk));
 }
 
+// Only classes 0 and / or 3 (every tone bin even: residues 0, 2, 4, 6), for
+// two folded samples at once (e = 0, 1 interleaved, so every packed result
+// is read two or more instructions after it is written): 5 packed ops per
+// sample for one class, 6 for both, against 11 for all four (the odd
+// residues' d terms and 1/sqrt2 products are not formed).
+//   Z03 = 2: (Z0, Z4) and (e1, e3);  1: (Z0, Z4) only;  3: (e1, e3) only.
+template <int Z03>
+__device__ __forceinline__ void residue_even_classes_asm(const f2 (&p02)[2], const f2 (&p46)[2],
+                                                         const f2 (&p13)[2], const f2 (&p57)[2],
+                                                         f2 (&z04)[2], f2 (&z6)[2])
+{
+    f2 a0, b0, a1, b1;
+    asm("v_pk_add_f32 %[a0], %[p02a], %[p46a]\n\t"                                    // (a0, a2)
+        "v_pk_add_f32 %[b0], %[p13a], %[p57a]\n\t"                                    // (a1, a3)
+        "v_pk_add_f32 %[a1], %[p02b], %[p46b]\n\t"
+        "v_pk_add_f32 %[b1], %[p13b], %[p57b]\n\t"
+        "v_pk_add_f32 %[a0], %[a0], %[a0] op_sel:[0,1] op_sel_hi:[0,1] neg_hi:[0,1]\n\t"  // (e0, e1)
+        "v_pk_add_f32 %[b0], %[b0], %[b0] op_sel:[0,1] op_sel_hi:[0,1] neg_hi:[0,1]\n\t"  // (e2, e3)
+        "v_pk_add_f32 %[a1], %[a1], %[a1] op_sel:[0,1] op_sel_hi:[0,1] neg_hi:[0,1]\n\t"
+        "v_pk_add_f32 %[b1], %[b1], %[b1] op_sel:[0,1] op_sel_hi:[0,1] neg_hi:[0,1]"
+        : [a0] "=&v"(a0), [b0] "=&v"(b0), [a1] "=&v"(a1), [b1] "=&v"(b1)
+        : [p02a] "v"(p02[0]), [p46a] "v"(p46[0]), [p13a] "v"(p13[0]), [p57a] "v"(p57[0]),
+          [p02b] "v"(p02[1]), [p46b] "v"(p46[1]), [p13b] "v"(p13[1]), [p57b] "v"(p57[1]));
+    if constexpr (Z03 != 3)
+        asm("v_pk_add_f32 %[z0], %[a0], %[b0] op_sel_hi:[0,0] neg_hi:[0,1]\n\t"      // (Z0, Z4)
+            "v_pk_add_f32 %[z1], %[a1], %[b1] op_sel_hi:[0,0] neg_hi:[0,1]"
+            : [z0] "=&v"(z04[0]), [z1] "=v"(z04[1])
+            : [a0] "v"(a0), [b0] "v"(b0), [a1] "v"(a1), [b1] "v"(b1));
+    if constexpr (Z03 != 1)
+        asm("v_pk_mov_b32 %[z0], %[a0], %[b0] op_sel:[1,1]\n\t"                      // (e1, e3)
+            "v_pk_mov_b32 %[z1], %[a1], %[b1] op_sel:[1,1]"
+            : [z0] "=&v"(z6[0]), [z1] "=v"(z6[1])
+            : [a0] "v"(a0), [b0] "v"(b0), [a1] "v"(a1), [b1] "v"(b1));
+}
+
 // Dynamic LDS: [K][G][2] float4 rotation constants (block), then per wave
 // [4 classes][QP sample pairs][64 lanes] float4 (4 QP KiB).
 constexpr int kResidueQP = 2;  // shipped: two sample pairs per LDS round
@@ -127,16 +162,23 @@ constexpr int kResidueQP = 2;  // shipped: two sample pairs per LDS round
 //         instruction, as the plain bank does, and regroup it through the
 //         wave's LDS slice (linear chunk q at 16 q; the class pairs reuse the
 //         slice afterwards) instead of the direct per-lane layout.
-//   DCLS  tone slot k reads class (k / 2) % 4 straight from registers (no LDS
-//         class file): for plans the host has permuted so that slot pairs
-//         (2c, 2c + 1) are the two residues of class c (every residue once at
-//         K = 8, e.g. any odd bin spacing).
+//   DC    compile-time classes: tone slot k reads its class straight from
+//         registers (no LDS class file), for plans the host has permuted
+//         into a fixed slot -> class pattern (window_sum maps slots back):
+//         1 = class (k / 2) % 4 (K / 4 tones per class: every residue once at
+//         K = 8, e.g. any odd bin spacing); 2 = slots < K / 2 class 0, the
+//         rest class 3 (even bins, half on residues 0 / 4 and half on 2 / 6:
+//         spacings 2 and 6); 3 = every slot class 0 (residues 0 / 4 only,
+//         e.g. spacing 4 or 12 from an odd multiple of 4); 4 = every slot
+//         class 3 (residues 2 / 6). Modes 2-4 form only the classes they read
+//         (residue_even_classes_asm). 0 = the LDS class file (any plan).
 template <int K, int LOG2G, int WPB = kWavesPerBlock, bool ASM = true, bool ROTV = false,
           int MINW = (K <= 8 ? 4 : 0), int QP = kResidueQP, bool PF = false, bool WS = true,
-          bool LDST = false, bool DCLS = false, bool NT = true>
+          bool LDST = false, int DC = 0, bool NT = true>
 __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MINW > 0 ? MINW : 1)))
 void residue_tile_kernel(GoertzelParams p)
 {
+    constexpr bool DCLS = DC > 0;
     extern __shared__ f4 lds_r[];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -238,7 +280,19 @@ void residue_tile_kernel(GoertzelParams p)
                         const uint32_t w = cur[m][d];
                         x[e][m] = e ? (float)((int)w >> 16) : (float)(int)(short)(w & 0xFFFFu);
                     }
-                if (ASM) {
+                if constexpr (DC >= 2) {
+                    const f2 p02[2] = {f2{x[0][0], x[0][2]}, f2{x[1][0], x[1][2]}};
+                    const f2 p46[2] = {f2{x[0][4], x[0][6]}, f2{x[1][4], x[1][6]}};
+                    const f2 p13[2] = {f2{x[0][1], x[0][3]}, f2{x[1][1], x[1][3]}};
+                    const f2 p57[2] = {f2{x[0][5], x[0][7]}, f2{x[1][5], x[1][7]}};
+                    f2 z04[2], z6[2];
+                    residue_even_classes_asm<DC == 2 ? 2 : DC == 3 ? 1 : 3>(p02, p46, p13, p57, z04, z6);
+#pragma unroll
+                    for (int e = 0; e < 2; ++e) {
+                        if constexpr (DC != 4) c[e][0] = z04[e];
+                        if constexpr (DC != 3) c[e][3] = z6[e];
+                    }
+                } else if (ASM) {
 #pragma unroll
                     for (int e = 0; e < 2; ++e)
                         residue_classes_asm(f2{x[e][0], x[e][2]}, f2{x[e][4], x[e][6]},
@@ -251,7 +305,8 @@ void residue_tile_kernel(GoertzelParams p)
                 if constexpr (DCLS) {
 #pragma unroll
                     for (int k = 0; k < K; ++k) {
-                        const int cl = (k / 2) % 4;
+                        const int cl = DC == 1 ? (k / 2) % 4 : DC == 2 ? (k < K / 2 ? 0 : 3)
+                                     : DC == 3 ? 0 : 3;
                         const f2 cc = f2{p.coef[k], p.coef[k]};
                         f2 a = __builtin_elementwise_fma(cc, s1[k], c[0][cl] - s2[k]);
                         s2[k] = s1[k];
@@ -328,35 +383,45 @@ size_t residue_lds_bytes(int k, int log2g, int qp)
     return ((size_t)k * (1u << log2g) * 2 + (size_t)kWavesPerBlock * 4 * qp * 64) * sizeof(f4);
 }
 
-// DCLS (K = 8, 16 at n = 1024, host-permuted plans with K / 4 tones per
-// class): 356-362 -> 312 us at K = 8 on bins 32 + 9i, the box's read ceiling
-// (profiles/round1/probe_dcls.log).
+// DC (K = 8, 16 at n = 1024, host-permuted plans): mode 1 (K / 4 tones per
+// class) 356-362 -> 312 us at K = 8 on bins 32 + 9i, the box's read ceiling
+// (profiles/round1/probe_dcls.log); modes 2-4 for even-bin plans.
+template <int K, int DC, bool NT>
+static const void *residue_dc_kernel()
+{
+    return reinterpret_cast<const void *>(
+        &residue_tile_kernel<K, 4, kWavesPerBlock, true, false, (K <= 8 ? 4 : 0), kResidueQP, false,
+                             true, false, DC, NT>);
+}
+
 template <int K, bool NT>
-static const void *residue_kernel_for_t(int log2g, bool dcls)
+static const void *residue_kernel_for_t(int log2g, int dcls)
 {
     if (log2g == 4) {
-        if constexpr (K == 8 || K == 16)
-            if (dcls)
-                return reinterpret_cast<const void *>(
-                    &residue_tile_kernel<K, 4, kWavesPerBlock, true, false, (K <= 8 ? 4 : 0),
-                                         kResidueQP, false, true, false, true, NT>);
-        return reinterpret_cast<const void *>(
-            &residue_tile_kernel<K, 4, kWavesPerBlock, true, false, (K <= 8 ? 4 : 0), kResidueQP,
-                                 false, true, false, false, NT>);
+        if constexpr (K == 8 || K == 16) {
+            switch (dcls) {
+            case 1: return residue_dc_kernel<K, 1, NT>();
+            case 2: return residue_dc_kernel<K, 2, NT>();
+            case 3: return residue_dc_kernel<K, 3, NT>();
+            case 4: return residue_dc_kernel<K, 4, NT>();
+            default: break;
+            }
+        }
+        return residue_dc_kernel<K, 0, NT>();
     }
     return reinterpret_cast<const void *>(
         &residue_tile_kernel<K, -1, kWavesPerBlock, true, false, (K <= 8 ? 4 : 0), kResidueQP, false,
-                             true, false, false, NT>);
+                             true, false, 0, NT>);
 }
 
 // nt: hop = n (each byte read once); overlapping windows keep their lines in L2
 template <int K>
-static const void *residue_kernel_for(int log2g, bool dcls, bool nt)
+static const void *residue_kernel_for(int log2g, int dcls, bool nt)
 {
     return nt ? residue_kernel_for_t<K, true>(log2g, dcls) : residue_kernel_for_t<K, false>(log2g, dcls);
 }
 
-const void *residue_kernel_ptr(int k, int log2g, bool dcls, bool nt)
+const void *residue_kernel_ptr(int k, int log2g, int dcls, bool nt)
 {
     switch (k) {
 #define FSKD_CASE(K) case K: return residue_kernel_for<K>(log2g, dcls, nt);

@@ -91,12 +91,22 @@ def test_residue_tone_counts_integer_bins(A, O, torch, k):
     ([40, 44, 33, 39, 35, 37, 42, 46], 256),                # 0,4,1,7,3,5,2,6 (pairs share a class)
     ([32 + 9 * i for i in range(16)], 1024),                # K = 16: every class 4 times
     ([200 - 9 * i for i in range(16)], 512),
+    # even bins (round 2, DC modes 2-4: only the classes read are formed)
+    ([32 + 2 * i for i in range(8)], 1024),                 # spacing 2: classes 0 | 3, 4 + 4
+    ([74 - 6 * i for i in range(8)], 1024),                 # spacing 6, descending
+    ([34 + 2 * i for i in range(16)][::-1], 512),           # K = 16, 8 + 8
+    ([36 + 4 * i for i in (5, 2, 7, 0, 3, 6, 1, 4)], 1024), # spacing 4 from 36: class 0 only
+    ([20 + 24 * i for i in range(8)], 256),                 # residues 4, 0, 4, ...: class 0 only
+    ([34 + 4 * i for i in range(8)], 1024),                 # residues 2 / 6: class 3 only
+    ([2 + 8 * i for i in range(16)][::-1], 1024),           # K = 16, class 3 only
 ])
 def test_residue_compile_time_classes(A, O, torch, bins, hop):
-    """Plans with K / 4 tones in every residue class (n = 1024, K = 8 or 16):
-    the residue detector permutes the tones so each kernel slot reads a fixed
-    class from registers (residue.hip DCLS) and the window_sum epilogue maps
-    magnitudes, the tie rule and the symbol back to the caller's tone order."""
+    """Plans with a compile-time class pattern (n = 1024, K = 8 or 16): K / 4
+    tones in every residue class, or even bins split K / 2 + K / 2 over
+    classes 0 and 3, or all in class 0 or all in class 3. The residue
+    detector permutes the tones so each kernel slot reads a fixed class from
+    registers (residue.hip DC) and the window_sum epilogue maps magnitudes,
+    the tie rule and the symbol back to the caller's tone order."""
     freqs = tuple(b * 46.875 for b in bins)
     run_case(A, O, freqs, W=700, hop=hop, seed=sum(bins), method=RESIDUE)
     # exact ties (all-zero window) still go to the caller's lowest tone index
