@@ -185,7 +185,7 @@ def test_random_stream(A, O, torch, i):
     check_decisions(gs, gm, ws, wP, denom)
 
 
-N_STRUCT_CASES = 24
+N_STRUCT_CASES = 40
 
 
 @pytest.mark.parametrize("i", range(N_STRUCT_CASES))
@@ -193,11 +193,23 @@ def test_random_permuted_plans(A, O, torch, i):
     """Plans that take the permuted-slot kernels at n = 1024 (DESIGN.md §4.2,
     §4.3): fold by 16 (K = 8, four tones on multiples of 16 bins and four on
     odd multiples of 8) and the residue kernel's compile-time classes (K = 8
-    or 16 with K / 4 tones per class), in random tone order, hop and level;
-    magnitudes and symbols in the caller's tone order."""
+    or 16 with K / 4 tones per class; cases 24+: even-bin plans, K / 2 tones
+    in each of classes 0 and 3 or all K in one of them), in random tone
+    order, hop and level; magnitudes and symbols in the caller's tone order."""
     rng = np.random.default_rng(0xC1A55 + i + SEED_OFFSET)
-    kind = ("fold16", "residue8", "residue16")[i % 3]
-    if kind == "fold16":
+    kind = (("fold16", "residue8", "residue16")[i % 3] if i < 24 else
+            ("even_split8", "even_one8", "even_split16", "even_one16")[i % 4])
+    if kind.startswith("even"):
+        K = 8 if kind.endswith("8") else 16
+        c0 = [b for b in range(4, 505) if b % 4 == 0]          # residues 0, 4: class 0
+        c3 = [b for b in range(2, 505) if b % 4 == 2]          # residues 2, 6: class 3
+        if kind.startswith("even_split"):
+            bins = np.concatenate([rng.choice(c0, K // 2, replace=False),
+                                   rng.choice(c3, K // 2, replace=False)])
+        else:
+            bins = rng.choice(c0 if rng.random() < 0.5 else c3, K, replace=False)
+        method = A.METHOD_RESIDUE
+    elif kind == "fold16":
         z0 = rng.choice(np.arange(1, 31) * 16, 4, replace=False)
         z8 = rng.choice(np.arange(0, 31) * 16 + 8, 4, replace=False)
         bins = np.concatenate([z0, z8])
