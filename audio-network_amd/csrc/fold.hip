@@ -75,10 +75,17 @@ __device__ __forceinline__ void fold_decide(const int (&acc)[8], const float4 *r
                 a2 = a1;
                 a1 = a;
             }
-            xr[2 * h] = r[2 * h].x * a1.x - r[2 * h].z * a2.x;
-            xi[2 * h] = r[2 * h].y * a1.x - r[2 * h].w * a2.x;
-            xr[2 * h + 1] = r[2 * h + 1].x * a1.y - r[2 * h + 1].z * a2.y;
-            xi[2 * h + 1] = r[2 * h + 1].y * a1.y - r[2 * h + 1].w * a2.y;
+            // rotation as packed (re, im) pairs: X = (A s1) - (B s2), 2 ops per tone
+            const f32x2f X0 = __builtin_elementwise_fma(
+                f32x2f{-r[2 * h].z, -r[2 * h].w}, f32x2f{a2.x, a2.x},
+                f32x2f{r[2 * h].x, r[2 * h].y} * f32x2f{a1.x, a1.x});
+            const f32x2f X1 = __builtin_elementwise_fma(
+                f32x2f{-r[2 * h + 1].z, -r[2 * h + 1].w}, f32x2f{a2.y, a2.y},
+                f32x2f{r[2 * h + 1].x, r[2 * h + 1].y} * f32x2f{a1.y, a1.y});
+            xr[2 * h] = X0.x;
+            xi[2 * h] = X0.y;
+            xr[2 * h + 1] = X1.x;
+            xi[2 * h + 1] = X1.y;
         }
         window_sum_decide_split8<true>(xr, xi, lane, w, live, p.sym, p.mag, p.perm);
     } else {
