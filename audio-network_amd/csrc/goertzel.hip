@@ -279,8 +279,17 @@ __global__ __launch_bounds__(64 * WPB) void goertzel_tile_kernel(GoertzelParams 
 #pragma unroll
                 for (int k = 0; k < K; ++k) {
                     const float2 z = lz[k * 64 + sg];   // (s1, s2) of segment j of window u
-                    xr[k] = r[k].x * z.x - r[k].z * z.y;
-                    xi[k] = r[k].y * z.x - r[k].w * z.y;
+                    if constexpr (WS) {
+                        // packed (re, im): (A s1) - (B s2), as the direct WS path below
+                        const f32x2 X = __builtin_elementwise_fma(
+                            f32x2{-r[k].z, -r[k].w}, f32x2{z.y, z.y},
+                            f32x2{r[k].x, r[k].y} * f32x2{z.x, z.x});
+                        xr[k] = X.x;
+                        xi[k] = X.y;
+                    } else {  // as the direct K <= 2 path below
+                        xr[k] = r[k].x * z.x - r[k].z * z.y;
+                        xi[k] = r[k].y * z.x - r[k].w * z.y;
+                    }
                 }
                 if constexpr (WS) {
                     window_sum_decide<K>(xr, xi, lane, w, live, p.sym, p.mag);
@@ -314,8 +323,12 @@ __global__ __launch_bounds__(64 * WPB) void goertzel_tile_kernel(GoertzelParams 
             float xr[K], xi[K];
 #pragma unroll
             for (int k = 0; k < K; ++k) {
-                xr[k] = r[k].x * s1[k] - r[k].z * s2[k];
-                xi[k] = r[k].y * s1[k] - r[k].w * s2[k];
+                // packed (re, im): (A s1) - (B s2), 2 ops per tone
+                const f32x2 X = __builtin_elementwise_fma(f32x2{-r[k].z, -r[k].w},
+                                                          f32x2{s2[k], s2[k]},
+                                                          f32x2{r[k].x, r[k].y} * f32x2{s1[k], s1[k]});
+                xr[k] = X.x;
+                xi[k] = X.y;
             }
             window_sum_decide<K>(xr, xi, lane, w, w < p.n_windows, p.sym, p.mag);
             return;
