@@ -330,6 +330,28 @@ __global__ __launch_bounds__(64 * WPB) void fold_tile_kernel(GoertzelParams p)
 //   consecutive windows, running the sums forward from its first. Every
 //   group has R windows, so no pass of the epilogue idles (a 64-segment tile
 //   at hop 256 holds 13 windows: 4 passes for 13).
+// acc (lo, hi) += the sign-extended int16 halves of n, minus those of o: four
+// SDWA integer ops (the extraction is the operand select; hipcc reaches the
+// same count from C here, but not for the first window's sums below, where
+// it built bfe / ashr extracts plus v_add3: 9 more VALU per tile).
+__device__ __forceinline__ void slide_add_sub(int &lo, int &hi, uint32_t n, uint32_t o)
+{
+    asm("v_add_u32_sdwa %0, sext(%2), %0 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:DWORD\n\t"
+        "v_add_u32_sdwa %1, sext(%2), %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD\n\t"
+        "v_sub_u32_sdwa %0, %0, sext(%3) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_sub_u32_sdwa %1, %1, sext(%3) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1"
+        : "+v"(lo), "+v"(hi)
+        : "v"(n), "v"(o));
+}
+// acc (lo, hi) += the sign-extended int16 halves of n (two SDWA adds)
+__device__ __forceinline__ void slide_add(int &lo, int &hi, uint32_t n)
+{
+    asm("v_add_u32_sdwa %0, sext(%2), %0 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:DWORD\n\t"
+        "v_add_u32_sdwa %1, sext(%2), %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD"
+        : "+v"(lo), "+v"(hi)
+        : "v"(n));
+}
+
 template <int K, bool F16>
 __global__ __launch_bounds__(64 * kPlainWPB) void fold_slide_kernel(GoertzelParams p)
 {
@@ -389,10 +411,7 @@ __global__ __launch_bounds__(64 * kPlainWPB) void fold_slide_kernel(GoertzelPara
                     const u32x4f d = wl[8 * (u * H + 2 * m2 + par) + chunk];
                     const uint32_t d4[4] = {d.x, d.y, d.z, d.w};
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        acc[2 * q] += (int)(short)(d4[q] & 0xFFFFu);
-                        acc[2 * q + 1] += (int)d4[q] >> 16;
-                    }
+                    for (int q = 0; q < 4; ++q) slide_add(acc[2 * q], acc[2 * q + 1], d4[q]);
                 }
             } else {
                 if (H & 1) {
@@ -410,10 +429,7 @@ __global__ __launch_bounds__(64 * kPlainWPB) void fold_slide_kernel(GoertzelPara
                         const uint32_t o4[4] = {o.x, o.y, o.z, o.w};
                         const uint32_t n4[4] = {nw.x, nw.y, nw.z, nw.w};
 #pragma unroll
-                        for (int q = 0; q < 4; ++q) {
-                            acc[2 * q] += (int)(short)(n4[q] & 0xFFFFu) - (int)(short)(o4[q] & 0xFFFFu);
-                            acc[2 * q + 1] += ((int)n4[q] >> 16) - ((int)o4[q] >> 16);
-                        }
+                        for (int q = 0; q < 4; ++q) slide_add_sub(acc[2 * q], acc[2 * q + 1], n4[q], o4[q]);
                     }
                 }
             }
