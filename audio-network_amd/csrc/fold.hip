@@ -307,6 +307,29 @@ __global__ __launch_bounds__(64 * WPB) void fold_tile_kernel(GoertzelParams p)
     }
 }
 
+// acc (lo, hi) += the sign-extended int16 halves of n, minus those of o: four
+// SDWA integer ops (the extraction is the operand select; hipcc reaches the
+// same count from C here, but not for the first window's sums in
+// fold_slide_kernel, where
+// it built bfe / ashr extracts plus v_add3: 9 more VALU per tile).
+__device__ __forceinline__ void slide_add_sub(int &lo, int &hi, uint32_t n, uint32_t o)
+{
+    asm("v_add_u32_sdwa %0, sext(%2), %0 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:DWORD\n\t"
+        "v_add_u32_sdwa %1, sext(%2), %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD\n\t"
+        "v_sub_u32_sdwa %0, %0, sext(%3) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_sub_u32_sdwa %1, %1, sext(%3) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1"
+        : "+v"(lo), "+v"(hi)
+        : "v"(n), "v"(o));
+}
+// acc (lo, hi) += the sign-extended int16 halves of n (two SDWA adds)
+__device__ __forceinline__ void slide_add(int &lo, int &hi, uint32_t n)
+{
+    asm("v_add_u32_sdwa %0, sext(%2), %0 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:DWORD\n\t"
+        "v_add_u32_sdwa %1, sext(%2), %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD"
+        : "+v"(lo), "+v"(hi)
+        : "v"(n));
+}
+
 // Overlapping windows (n = 1024, hop = 64 H < n) for fold-eligible plans:
 // the folded sums of a window are sums of its 64-sample segments. With
 // seg_s the segments of the stream and window u starting at segment uH,
@@ -330,28 +353,6 @@ __global__ __launch_bounds__(64 * WPB) void fold_tile_kernel(GoertzelParams p)
 //   consecutive windows, running the sums forward from its first. Every
 //   group has R windows, so no pass of the epilogue idles (a 64-segment tile
 //   at hop 256 holds 13 windows: 4 passes for 13).
-// acc (lo, hi) += the sign-extended int16 halves of n, minus those of o: four
-// SDWA integer ops (the extraction is the operand select; hipcc reaches the
-// same count from C here, but not for the first window's sums below, where
-// it built bfe / ashr extracts plus v_add3: 9 more VALU per tile).
-__device__ __forceinline__ void slide_add_sub(int &lo, int &hi, uint32_t n, uint32_t o)
-{
-    asm("v_add_u32_sdwa %0, sext(%2), %0 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:DWORD\n\t"
-        "v_add_u32_sdwa %1, sext(%2), %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD\n\t"
-        "v_sub_u32_sdwa %0, %0, sext(%3) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
-        "v_sub_u32_sdwa %1, %1, sext(%3) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1"
-        : "+v"(lo), "+v"(hi)
-        : "v"(n), "v"(o));
-}
-// acc (lo, hi) += the sign-extended int16 halves of n (two SDWA adds)
-__device__ __forceinline__ void slide_add(int &lo, int &hi, uint32_t n)
-{
-    asm("v_add_u32_sdwa %0, sext(%2), %0 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:DWORD\n\t"
-        "v_add_u32_sdwa %1, sext(%2), %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD"
-        : "+v"(lo), "+v"(hi)
-        : "v"(n));
-}
-
 template <int K, bool F16>
 __global__ __launch_bounds__(64 * kPlainWPB) void fold_slide_kernel(GoertzelParams p)
 {
