@@ -310,8 +310,8 @@ __global__ __launch_bounds__(64 * WPB) void fold_tile_kernel(GoertzelParams p)
 // acc (lo, hi) += the sign-extended int16 halves of n, minus those of o: four
 // SDWA integer ops (the extraction is the operand select; hipcc reaches the
 // same count from C here, but not for the first window's sums in
-// fold_slide_kernel, where
-// it built bfe / ashr extracts plus v_add3: 9 more VALU per tile).
+// fold_slide_kernel, where it built bfe / ashr extracts plus v_add3: 9 more
+// VALU per tile).
 __device__ __forceinline__ void slide_add_sub(int &lo, int &hi, uint32_t n, uint32_t o)
 {
     asm("v_add_u32_sdwa %0, sext(%2), %0 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:DWORD\n\t"
