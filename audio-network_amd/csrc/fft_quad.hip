@@ -757,12 +757,6 @@ __device__ __attribute__((always_inline)) inline void fft1024_quad_body(const Ff
     const int mybin = t < p.k ? p.bins[t] : 0;
     const int myslot = SPL ? q * 513 + mybin : quad_slot(mybin);
     float *pw = reinterpret_cast<float *>(slab[wave]);
-    // SPL: float index of (|X[kP]|^2, |X[512 - kP]|^2) of pair j, as
-    // row base + 32 j and mirror base + 32 (15 - j): lane t has kP = t + 32 j;
-    // lane 0 has kP = 16 + 32 j for j < 8 (like t = 16) and 32 j for j >= 8
-    const int te_lo = t == 0 ? 16 : t;
-    const int spl_a_lo = q * 513 + te_lo, spl_m_lo = q * 513 + 32 - te_lo;
-    const int spl_a_hi = q * 513 + t, spl_m_hi = q * 513 + 32 - t;
     __syncthreads();
 
     const long long n_groups = (p.n_windows + 3) >> 2;
@@ -893,6 +887,18 @@ __device__ __attribute__((always_inline)) inline void fft1024_quad_body(const Ff
         //    with X[kP] = S/2 + (W/2) D and the powers of both mirrors per pair
         const bool l0 = (t == 0);
         float *pq = pw + q * kQPow;
+        // SPL: float index of (|X[kP]|^2, |X[512 - kP]|^2) of pair j, as row
+        // base + 32 j and mirror base + 32 (15 - j): lane t has kP = t + 32 j;
+        // lane 0 has kP = 16 + 32 j for j < 8 (like t = 16) and 32 j for
+        // j >= 8. Formed here from the lane id, fenced from hoisting, so the
+        // four bases do not stay live across the group loop (with them the
+        // kernel hit 128 VGPRs and spilled 20 B per lane).
+        int tl = (int)(threadIdx.x & 63);
+        if constexpr (SPL) asm volatile("" : "+v"(tl));
+        const int tt = tl & 15, rowb = (tl >> 4) * 513;
+        const int te_lo = tt == 0 ? 16 : tt;
+        const int spl_a_lo = rowb + te_lo, spl_m_lo = rowb + 32 - te_lo;
+        const int spl_a_hi = rowb + tt, spl_m_hi = rowb + 32 - tt;
         f2 *const ps = reinterpret_cast<f2 *>(pq) + t;  // slot (j, t) at ps[16 j]
         // !SPEC: this lane's powers, pv[2 j + half], one 32-register tuple so a
         // uniform index reads it with v_movrels (no scratch, no select chain)
@@ -960,8 +966,8 @@ __device__ __attribute__((always_inline)) inline void fft1024_quad_body(const Ff
         if constexpr (SPEC) {
             if (l0) {
                 if constexpr (SPL) {
-                    pw[q * 513] = px.x;
-                    pw[q * 513 + 512] = px.y;
+                    pw[rowb] = px.x;
+                    pw[rowb + 512] = px.y;
                 } else {
                     pq[512] = px.x;
                     pq[513] = px.y;
@@ -971,8 +977,10 @@ __device__ __attribute__((always_inline)) inline void fft1024_quad_body(const Ff
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             // 5. tone pick (as fft1024_quad_kernel step 4)
-            if (t < p.k) pk = SPL ? pw[myslot] : pq[myslot];
-            if (live && t < p.k && p.mag) p.mag[w * p.k + t] = pk;
+            if (t < p.k) pk = SPL ? pw[rowb + mybin] : pq[myslot];
+            // SPL: the fenced lane id again, so the store address is formed
+            // here rather than held across the loop
+            if (live && t < p.k && p.mag) p.mag[w * p.k + (SPL ? tt : t)] = pk;
         } else {
             // 5. tone pick from registers: tone i's power sits in lane
             //    (slot >> 1) & 15 of each window row at pv[slot >> 5 | half]

@@ -97,6 +97,12 @@ int main(int argc, char **argv)
     vs.push_back({"ds_read_b64 (no read2 pairing)", [](const FftParams &p, hipStream_t s) { return p.hop < 1024 ? (p.spec ? launch_fft_quad_t<4, 4, 0, true, false, 0, 4, 1>(p, s) : launch_fft_quad_t<4, 4, 0, false, false, 0, 4, 1>(p, s)) : (p.spec ? launch_fft_quad_t<4, 4, 0, true, false, 2, 4, 1>(p, s) : launch_fft_quad_t<4, 4, 0, false, false, 2, 4, 1>(p, s)); }, {}});
     vs.push_back({"ds_read_b64 + b128 tables", [](const FftParams &p, hipStream_t s) { return p.hop < 1024 ? (p.spec ? launch_fft_quad_t<4, 4, 0, true, false, 0, 4, 2>(p, s) : launch_fft_quad_t<4, 4, 0, false, false, 0, 4, 2>(p, s)) : (p.spec ? launch_fft_quad_t<4, 4, 0, true, false, 2, 4, 2>(p, s) : launch_fft_quad_t<4, 4, 0, false, false, 2, 4, 2>(p, s)); }, {}});
     vs.push_back({"fused PF1 MINW0", [](const FftParams &p, hipStream_t s) { return p.spec ? launch_fft_quad_t<4, 0, 1, true>(p, s) : launch_fft_quad_t<4, 0, 1, false>(p, s); }, {}});
+    // round 2, late: the next group's loads during the transpose (PF 1) with
+    // the shipped fused kernel, at 3 and 4 waves per SIMD, and 3 waves alone
+    vs.push_back({"pfx: fused4 PF1 MINW3", [](const FftParams &p, hipStream_t s) { return p.spec ? launch_fft_quad_t<4, 3, 1, true, false, 0, 4>(p, s) : launch_fft_quad_t<4, 3, 1, false, false, 0, 4>(p, s); }, {}});
+    vs.push_back({"pfx: fused4 PF1 MINW4", [](const FftParams &p, hipStream_t s) { return p.spec ? launch_fft_quad_t<4, 4, 1, true, false, 0, 4>(p, s) : launch_fft_quad_t<4, 4, 1, false, false, 0, 4>(p, s); }, {}});
+    vs.push_back({"pfx: fused4 PF0 MINW3", [](const FftParams &p, hipStream_t s) { return p.spec ? launch_fft_quad_t<4, 3, 0, true, false, 0, 4>(p, s) : launch_fft_quad_t<4, 3, 0, false, false, 0, 4>(p, s); }, {}});
+    vs.push_back({"pfx: shipped", [](const FftParams &p, hipStream_t s) { return launch_fft_quad(p, s); }, {}});
     if (filter) {
         std::vector<Var> keep;
         for (size_t i = 0; i < vs.size(); ++i)
