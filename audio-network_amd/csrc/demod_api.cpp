@@ -822,6 +822,7 @@ struct demod_streams {
     std::vector<std::vector<int16_t>> carry;
     std::vector<size_t> skip;             // lead-in frames still to drop per stream
     std::vector<size_t> first;            // per push: batch window of each stream's first
+    std::vector<size_t> have;             // per push: carry lengths before it
     std::vector<uint8_t> sym;             // per push: batch symbols / magnitudes
     std::vector<float> mag;
 };
@@ -923,80 +924,84 @@ int demod_streams_push(demod_streams_t *ms, const int16_t *const *pcm, const siz
     demod_t *st = ms->st;
     DeviceGuard guard(st->device);
     HIP_TRY(guard.err);
-    // the streams' mono samples appended to their carries (undone on failure)
-    std::vector<size_t> old(S);
+    // every carry holds < n samples after a push: reserve n once so the
+    // carry updates below never allocate
+    std::vector<size_t> &have = ms->have;
     try {
+        have.resize(S);
         for (size_t s = 0; s < S; ++s) {
-            old[s] = ms->carry[s].size();
-            const size_t drop = std::min(ms->skip[s], n_frames[s]);
-            const size_t f = n_frames[s] - drop;
-            ms->carry[s].resize(old[s] + f);
-            if (f) mono_frames(c, pcm[s] + drop * c.channels, f, ms->carry[s].data() + old[s]);
+            ms->carry[s].reserve(n);
+            have[s] = ms->carry[s].size();
         }
     } catch (...) {
-        for (size_t s = 0; s < S; ++s) ms->carry[s].resize(std::min(old[s], ms->carry[s].size()));
         return DEMOD_ALLOC_FAIL;
     }
-    auto undo = [&]() {
-        for (size_t s = 0; s < S; ++s) ms->carry[s].resize(old[s]);
-    };
+    auto fresh = [&](size_t s) { return n_frames[s] - std::min(ms->skip[s], n_frames[s]); };
+    auto windows = [&](size_t total) { return total < n ? (size_t)0 : (total - n) / hop + 1; };
     if (W) {
         // the streams' runs of complete windows end to end, each starting on a
-        // multiple of hop, in the pinned staging buffer the host path copies from
+        // multiple of hop, in the pinned staging buffer the host path copies
+        // from. A stream's samples (carry, then its packet's mono frames) are
+        // written there directly, one host copy of the packet; its new carry
+        // (the samples past its last window's start + hop, < n) is taken from
+        // there before the next stream's run overwrites the part of it that
+        // lies past this run's ceil(L / hop) windows.
         size_t Wb = 0;
         for (size_t s = 0; s < S; ++s) {
-            const size_t total = ms->carry[s].size();
-            const size_t w = total < n ? 0 : (total - n) / hop + 1;
+            const size_t w = windows(have[s] + fresh(s));
             ms->first[s] = Wb;
             if (w) Wb += ((w - 1) * hop + n + hop - 1) / hop;  // ceil(L_s / hop)
         }
         const size_t samples = (Wb - 1) * hop + n;  // the last run ends exactly here or earlier
+        // + n: the last stream's tail reaches past Wb hops by < hop <= n
         int rc = ensure_host(st, std::max(Wb * hop + n, kSmallHostSamples), kSmallHostSamples / 8);
-        if (rc != DEMOD_OK) {
-            undo();
-            return rc;
-        }
+        if (rc != DEMOD_OK) return rc;
         try {
             ms->sym.resize(Wb);
             if (mags) ms->mag.resize(Wb * c.k);
         } catch (...) {
-            undo();
             return DEMOD_ALLOC_FAIL;
         }
         for (size_t s = 0; s < S; ++s) {
-            const size_t total = ms->carry[s].size();
-            const size_t w = total < n ? 0 : (total - n) / hop + 1;
+            const size_t f = fresh(s), total = have[s] + f, w = windows(total);
             if (!w) continue;
             const size_t L = (w - 1) * hop + n, span = (L + hop - 1) / hop * hop;
             int16_t *b = st->h_in + ms->first[s] * hop;
-            std::memcpy(b, ms->carry[s].data(), L * sizeof(int16_t));
+            if (have[s]) std::memcpy(b, ms->carry[s].data(), have[s] * sizeof(int16_t));
+            mono_frames(c, pcm[s] + (n_frames[s] - f) * c.channels, f, b + have[s]);
+            ms->carry[s].assign(b + w * hop, b + total);
             // the straddling windows read up to the next run's start: keep
             // the gap defined (their results are dropped)
             if (span > L) std::memset(b + L, 0, (span - L) * sizeof(int16_t));
         }
         rc = run_host(st, st->h_in, samples, Wb, ms->sym.data(), mags ? ms->mag.data() : nullptr);
         if (rc < 0) {
-            undo();
+            // nothing consumed: the old carries are the runs' first samples
+            // (have < n <= L, below anything a later run or gap fill wrote)
+            for (size_t s = 0; s < S; ++s)
+                if (windows(have[s] + fresh(s))) {
+                    const int16_t *b = st->h_in + ms->first[s] * hop;
+                    ms->carry[s].assign(b, b + have[s]);
+                }
             return rc;
         }
-        uint8_t *so = symbols;
-        float *mo = mags;
-        for (size_t s = 0; s < S; ++s) {
-            const size_t total = ms->carry[s].size();
-            const size_t w = total < n ? 0 : (total - n) / hop + 1;
+    }
+    uint8_t *so = symbols;
+    float *mo = mags;
+    for (size_t s = 0; s < S; ++s) {
+        const size_t f = fresh(s), total = have[s] + f, w = windows(total);
+        counts[s] = (uint32_t)w;
+        if (w) {
             std::memcpy(so, ms->sym.data() + ms->first[s], w);
             so += w;
             if (mags) {
                 std::memcpy(mo, ms->mag.data() + ms->first[s] * c.k, w * c.k * sizeof(float));
                 mo += w * c.k;
             }
+        } else if (f) {
+            ms->carry[s].resize(total);  // < n: within the reserved capacity
+            mono_frames(c, pcm[s] + (n_frames[s] - f) * c.channels, f, ms->carry[s].data() + have[s]);
         }
-    }
-    for (size_t s = 0; s < S; ++s) {
-        const size_t total = ms->carry[s].size();
-        const size_t w = total < n ? 0 : (total - n) / hop + 1;
-        counts[s] = (uint32_t)w;
-        ms->carry[s].erase(ms->carry[s].begin(), ms->carry[s].begin() + (ptrdiff_t)(w * hop));
         ms->skip[s] -= std::min(ms->skip[s], n_frames[s]);
     }
     return (int)W;
