@@ -462,32 +462,52 @@ class Streams:
         return rc
 
     def push(self, packets, mags: bool = False, cap: Optional[int] = None):
-        """packets: one int16 array (interleaved if stereo) or None per stream.
+        """packets: one int16 array (interleaved if stereo) or None per stream,
+        or one 2-D array whose rows are the streams' packets (equal lengths;
+        its row addresses are computed, not read array by array).
         Returns the per-stream symbol arrays (and magnitude arrays)."""
-        if len(packets) != self.n_streams:
-            raise DemodError(DEMOD_BAD_ARG, "one packet (or None) per stream")
         ch = int(self.cfg.channels)
-        arrs = [np.ascontiguousarray(p, dtype=np.int16) if p is not None else None for p in packets]
-        frames = np.array([0 if a is None else a.size // ch for a in arrs], dtype=np.uintp)
-        for a in arrs:
-            if a is not None and a.size % ch:
+        S = self.n_streams
+        if isinstance(packets, np.ndarray) and packets.ndim == 2:
+            if packets.shape[0] != S:
+                raise DemodError(DEMOD_BAD_ARG, "one packet row per stream")
+            rows_ok = (packets.dtype == np.int16 and packets.strides[0] >= 0
+                       and (packets.shape[1] <= 1 or packets.strides[1] == 2))
+            # rows need only be contiguous each (a column slice of a longer
+            # recording is not copied)
+            keep = packets if rows_ok else np.ascontiguousarray(packets, dtype=np.int16)
+            if keep.shape[1] % ch:
                 raise DemodError(DEMOD_BAD_ARG, "pcm length not a multiple of channels")
-        ptrs = (ctypes.c_void_p * self.n_streams)(*[None if a is None or a.size == 0 else a.ctypes.data
-                                                    for a in arrs])
+            frames = np.full(S, keep.shape[1] // ch, dtype=np.uintp)
+            ptrs = np.zeros(S, dtype=np.uintp)
+            if keep.shape[1]:
+                ptrs += np.uintp(keep.ctypes.data)
+                ptrs += np.arange(S, dtype=np.uintp) * np.uintp(keep.strides[0])
+        else:
+            if len(packets) != S:
+                raise DemodError(DEMOD_BAD_ARG, "one packet (or None) per stream")
+            keep = [np.ascontiguousarray(p, dtype=np.int16) if p is not None else None for p in packets]
+            frames = np.array([0 if a is None else a.size // ch for a in keep], dtype=np.uintp)
+            for a in keep:
+                if a is not None and a.size % ch:
+                    raise DemodError(DEMOD_BAD_ARG, "pcm length not a multiple of channels")
+            ptrs = np.array([0 if a is None or a.size == 0 else a.ctypes.data for a in keep],
+                            dtype=np.uintp)
         if cap is None:
             cap = int(self._lib.demod_streams_max_symbols(self._h, frames.ctypes.data))
         sym = np.empty(max(cap, 1), dtype=np.uint8)
         mag = np.empty((max(cap, 1), self.k), dtype=np.float32) if mags else None
-        counts = np.zeros(self.n_streams, dtype=np.uint32)
-        rc = self._lib.demod_streams_push(self._h, ctypes.cast(ptrs, ctypes.c_void_p), frames.ctypes.data,
+        counts = np.zeros(S, dtype=np.uint32)
+        rc = self._lib.demod_streams_push(self._h, ptrs.ctypes.data, frames.ctypes.data,
                                           _ptr(sym), _ptr(mag), cap, counts.ctypes.data)
+        del keep
         if rc < 0:
             raise DemodError(rc, "demod_streams_push")
-        edges = np.concatenate([[0], np.cumsum(counts.astype(np.int64))])
-        out_s = [sym[edges[i]:edges[i + 1]] for i in range(self.n_streams)]
+        e = [0] + np.cumsum(counts, dtype=np.int64).tolist()
+        out_s = [sym[e[i]:e[i + 1]] for i in range(S)]
         if not mags:
             return out_s
-        return out_s, [mag[edges[i]:edges[i + 1]] for i in range(self.n_streams)]
+        return out_s, [mag[e[i]:e[i + 1]] for i in range(S)]
 
 
 def synth_fsk(cfg: DemodCfg, seed: int, n_windows: int, amplitude: int, sigma: int,

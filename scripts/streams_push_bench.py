@@ -46,6 +46,16 @@ def main():
                     times.append(dt)
                     syms += sum(o.size for o in out)
         t_push = float(np.median(times))
+        # the same packets as one 2-D array (rows = streams, a column slice)
+        with A.Streams(S, **kw) as ms:
+            times2 = []
+            for r in range(R + 3):
+                t0 = time.perf_counter()
+                ms.push(pk[:, r * F * channels:(r + 1) * F * channels])
+                dt = time.perf_counter() - t0
+                if r >= 3:
+                    times2.append(dt)
+        t_rows = float(np.median(times2))
         # the same pushes through the C ABI alone: pointer arrays and output
         # buffers built outside the timer (what a C caller pays)
         import ctypes
@@ -81,6 +91,7 @@ def main():
         print(json.dumps({"lib": args.lib or "in-tree", "streams": S, "channels": channels, "hop": hop, "packet_frames": F,
                           "push_ms": round(t_push * 1e3, 3),
                           "push_abi_ms": round(t_abi * 1e3, 3),
+                          "push_rows_ms": round(t_rows * 1e3, 3),
                           "per_stream_calls_ms": round(t_one * 1e3, 3),
                           "speedup": round(t_one / t_push, 1),
                           "realtime_factor_push": round(S * 0.06 / t_push, 1),

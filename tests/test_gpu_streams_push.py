@@ -142,3 +142,29 @@ def test_many_streams_one_push(A, O, torch):
             got = ms.push(pk)
             for s in range(S):
                 assert np.array_equal(got[s], refs[s].push(pk[s])[0]), (r, s)
+
+
+@pytest.mark.parametrize("channels", [1, 2])
+def test_rows_of_one_array(A, O, torch, channels):
+    """A 2-D array of packets (rows = streams, here column slices of a longer
+    recording, so rows are not adjacent in memory) gives the same symbols and
+    magnitudes as the same packets passed as a list."""
+    S, F, n = 33, 2880, 1024
+    pcm, _ = O.synth_fsk(A.FSK8_FREQS, n, 9 * S * channels, 3, 8000, 400)
+    rec = pcm.reshape(S, -1)                       # each row one stream's recording (>= 3 F frames)
+    kw = dict(freqs=A.FSK8_FREQS, channels=channels)
+    with A.Streams(S, **kw) as a, A.Streams(S, **kw) as b:
+        for r in range(3):
+            block = rec[:, r * F * channels:(r + 1) * F * channels]
+            assert not block.flags.c_contiguous
+            s1, m1 = a.push(block, mags=True)
+            s2, m2 = b.push([np.array(x) for x in block], mags=True)
+            for s in range(S):
+                assert np.array_equal(s1[s], s2[s])
+                assert np.array_equal(m1[s].view(np.uint32), m2[s].view(np.uint32))
+                assert a.pending(s) == b.pending(s)
+        with pytest.raises(A.DemodError):
+            a.push(rec[:S - 1, :F * channels])
+        if channels == 2:
+            with pytest.raises(A.DemodError):
+                a.push(rec[:, :3])
