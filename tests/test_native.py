@@ -27,3 +27,19 @@ def test_config1_native_gpu_branch():
     assert r.returncode == 0, r.stdout + r.stderr
     assert "gpu demodulate: symbol" in r.stdout
     assert "gpu demod_streams_push: 3 streams OK" in r.stdout
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_wire_codecs_under_sanitizers(seed):
+    """The ABI's byte codecs (csrc/demod_frame.c, csrc/demod_session.c: what
+    fskrx parses off the network) built with AddressSanitizer + UBSan and
+    fuzzed on exact-size buffers (tests/native/fuzz_wire.c): round trips at
+    every payload size, truncations, mutations, random bytes; any read past
+    an input or undefined behaviour aborts the run."""
+    subprocess.run(["make", "-C", NATIVE, "-s", "fuzz_wire"], check=True, capture_output=True)
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1",
+               UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1")
+    r = subprocess.run([os.path.join(NATIVE, "fuzz_wire"), "200000", str(seed)],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "fuzz_wire OK" in r.stdout
