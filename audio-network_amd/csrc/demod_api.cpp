@@ -51,6 +51,15 @@ struct demod {
     uint8_t *h_sym = nullptr;           // pinned
     float *h_mag = nullptr;             // pinned [h_out_cap][k]
     size_t h_out_cap = 0;               // windows
+    // packet-sized calls: the kernel reads the window samples from, and
+    // writes its results to, mapped coherent host memory (no copies)
+    int zc = 0;                         // 0: not set up, 1: ready, -1: unavailable
+    int16_t *z_in = nullptr;            // host view [kZeroCopySamples]
+    uint8_t *z_sym = nullptr;
+    float *z_mag = nullptr;
+    int16_t *zd_in = nullptr;           // device views of the same memory
+    uint8_t *zd_sym = nullptr;
+    float *zd_mag = nullptr;
     hipStream_t copy_stream = nullptr;  // H2D of large host-pointer calls
     hipEvent_t copied[2] = {};          // device slot b holds its chunk
     hipEvent_t consumed[2] = {};        // the kernel reading slot b has run
@@ -372,6 +381,9 @@ static void free_state(demod_t *st)
     if (st->h_in) (void)hipHostFree(st->h_in);
     if (st->h_sym) (void)hipHostFree(st->h_sym);
     if (st->h_mag) (void)hipHostFree(st->h_mag);
+    if (st->z_in) (void)hipHostFree(st->z_in);
+    if (st->z_sym) (void)hipHostFree(st->z_sym);
+    if (st->z_mag) (void)hipHostFree(st->z_mag);
     if (st->copy_stream) (void)hipStreamSynchronize(st->copy_stream);
     for (int b = 0; b < 2; ++b) {
         if (st->copied[b]) (void)hipEventDestroy(st->copied[b]);
@@ -627,13 +639,55 @@ static int ensure_host(demod_t *st, size_t samples, size_t windows)
     return DEMOD_OK;
 }
 
-// Small calls (a 60 ms packet is 2 windows): one pinned round trip on one
-// stream — 20 us per packet, against ~50 us through the chunked path's
-// pageable copies and cross-stream events.
+// Packet-sized calls (a 60 ms packet plus the carry is <= 3903 samples):
+// mapped, coherent (uncached on the device) pinned buffers. The kernel's
+// buffer loads read the samples over PCIe and its stores write the results
+// back, so a call is one launch and one synchronize instead of an H2D copy, a
+// launch, a D2H copy and the synchronize. The kernels' loads are bounded by
+// the buffer descriptor's record count, so nothing past the call's samples is
+// touched. If the runtime cannot map the memory the copy path below serves.
+static constexpr size_t kZeroCopySamples = 1 << 14;   // 32 KiB: 16 windows at hop n
+
+static int ensure_zero_copy(demod_t *st)
+{
+    if (st->zc) return st->zc;
+    if (std::getenv("FSKD_NO_ZERO_COPY")) return st->zc = -1;  // measurement switch
+    const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent;
+    const size_t wmax = kZeroCopySamples / 8;  // hop >= 8
+    bool ok = hipHostMalloc(&st->z_in, kZeroCopySamples * sizeof(int16_t), fl) == hipSuccess &&
+              hipHostMalloc(&st->z_sym, wmax, fl) == hipSuccess &&
+              hipHostMalloc(&st->z_mag, wmax * st->cfg.k * sizeof(float), fl) == hipSuccess &&
+              hipHostGetDevicePointer((void **)&st->zd_in, st->z_in, 0) == hipSuccess &&
+              hipHostGetDevicePointer((void **)&st->zd_sym, st->z_sym, 0) == hipSuccess &&
+              hipHostGetDevicePointer((void **)&st->zd_mag, st->z_mag, 0) == hipSuccess &&
+              ((uintptr_t)st->zd_in & 15) == 0;
+    if (!ok) (void)hipGetLastError();
+    st->zc = ok ? 1 : -1;
+    return st->zc;
+}
+
+static int run_host_zero_copy(demod_t *st, const int16_t *pcm, size_t n_samples, size_t n_windows,
+                              uint8_t *symbols, float *mags)
+{
+    std::memcpy(st->z_in, pcm, n_samples * sizeof(int16_t));
+    int rc = enqueue_batch(st, st->zd_in, n_windows, st->zd_sym, mags ? st->zd_mag : nullptr,
+                           st->stream);
+    if (rc < 0) return rc;
+    HIP_TRY(hipStreamSynchronize(st->stream));
+    std::memcpy(symbols, st->z_sym, n_windows);
+    if (mags) std::memcpy(mags, st->z_mag, n_windows * st->cfg.k * sizeof(float));
+    return (int)n_windows;
+}
+
+// Small calls: one pinned round trip on one stream — 20 us per packet,
+// against ~50 us through the chunked path's pageable copies and cross-stream
+// events.
 static int run_host_small(demod_t *st, const int16_t *pcm, size_t n_samples, size_t n_windows,
                           uint8_t *symbols, float *mags)
 {
     int rc;
+    if (n_samples <= kZeroCopySamples && ensure_zero_copy(st) == 1)
+        return run_host_zero_copy(st, pcm, n_samples, n_windows, symbols, mags);
     if ((rc = ensure_dev(st, n_samples, n_windows, mags != nullptr)) != DEMOD_OK) return rc;
     if ((rc = ensure_host(st, kSmallHostSamples, kSmallHostSamples / 8)) != DEMOD_OK) return rc;
     if (pcm != st->h_in) std::memcpy(st->h_in, pcm, n_samples * sizeof(int16_t));
