@@ -168,3 +168,53 @@ def test_rows_of_one_array(A, O, torch, channels):
         if channels == 2:
             with pytest.raises(A.DemodError):
                 a.push(rec[:, :3])
+
+
+@pytest.mark.parametrize("hop,channels", [(1024, 1), (1024, 2), (256, 1)])
+def test_threaded_staging(A, O, torch, hop, channels):
+    """Pushes big enough to stage on several host threads (>= 4 MiB of run
+    samples: 1024 streams x ~4000 frames), ragged and empty packets so the
+    thread ranges hold streams with and without windows: every stream's
+    symbols equal the oracle's stream, and a sample of 24 streams equals its
+    own single handle bit for bit (symbols, magnitudes, carry). At hop < n
+    the oracle bar is agreement on >= 99.9 % of the windows."""
+    n, S, R = 1024, 1024, 3
+    rng = np.random.default_rng(hop + channels)
+    pcm, _ = O.synth_fsk(A.FSK8_FREQS, n, 16 * S * channels, 40 + hop, 8000, 400)
+    rec = pcm.reshape(S, -1)                      # 16 * channels windows per stream
+    kw = dict(freqs=A.FSK8_FREQS, hop=hop, channels=channels)
+    probe = sorted(rng.choice(S, 24, replace=False).tolist())
+    singles = {s: A.Demodulator(**kw) for s in probe}
+    refs = [O.Stream(A.FSK8_FREQS, n=n, hop=hop, channels=channels) for _ in range(S)]
+    pos = np.zeros(S, dtype=np.int64)
+    staged = 0
+    try:
+        with A.Streams(S, **kw) as ms:
+            for r in range(R):
+                pk = []
+                for s in range(S):
+                    f = 0 if rng.random() < 0.05 else int(rng.integers(2000, 6000))
+                    pk.append(rec[s, pos[s] * channels:(pos[s] + f) * channels])
+                    pos[s] += f
+                staged += sum(p.size // channels for p in pk)
+                got_s, got_m = ms.push(pk, mags=True)
+                same = total = 0
+                for s in range(S):
+                    ref_s, _ = refs[s].push(pk[s])
+                    assert got_s[s].size == ref_s.size, (r, s)
+                    if hop == n:
+                        assert np.array_equal(got_s[s], ref_s), (r, s)
+                    same += int((got_s[s] == ref_s).sum())
+                    total += ref_s.size
+                    assert ms.pending(s) == refs[s].pending(), (r, s)
+                # windows straddling a symbol boundary can be near-ties (§4.8)
+                assert same >= 0.999 * total, (r, same, total)
+                for s in probe:
+                    one_s, one_m = singles[s].demodulate(pk[s], mags=True)
+                    assert np.array_equal(got_s[s], one_s), (r, s)
+                    assert np.array_equal(got_m[s].view(np.uint32), one_m.view(np.uint32)), (r, s)
+                    assert ms.pending(s) == singles[s].pending(), (r, s)
+    finally:
+        for d in singles.values():
+            d.close()
+    assert staged / R > 2 * (1 << 20)            # several threads per push (one per 2 MiB)
