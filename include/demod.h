@@ -149,6 +149,10 @@ int demod_batch_launches(const demod_t *st, size_t n_windows, int with_mags);
  * If max_symbols is too small nothing is consumed and
  * DEMOD_BUFFER_TOO_SMALL is returned.
  * mags (nullable, host): receives k floats |X_k|^2 per emitted symbol.
+ * Packet-sized calls (<= 16 Ki samples of carry + packet) run the kernel on
+ * mapped, coherent pinned memory: one launch and one synchronize, no copies
+ * (FSKD_NO_ZERO_COPY=1 in the environment at the handle's first such call
+ * selects the copy path; a measurement switch, results are the same).
  */
 int demodulate(demod_t *st, const int16_t *pcm, size_t n_frames,
                uint8_t *symbols, size_t max_symbols);
