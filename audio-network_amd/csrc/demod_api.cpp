@@ -33,7 +33,14 @@ struct demod {
     float *d_tw512 = nullptr;   // FFT detector tables
     float *d_tw1024 = nullptr;
     int *d_bins = nullptr;
+    int fft_bins[kMaxTones] = {};  // FFT detector: tone bins round(f n / fs)
     int fft_slot[kMaxTones] = {};  // FFT detector: where each tone bin's power sits (fft_quad_slot)
+    // decision rescue (rescue.hip)
+    bool rescue = false;        // K >= 2 and not switched off (FSKD_NO_RESCUE=1)
+    float amb_tq = 0.f;         // detectors' ambiguity threshold: amb_tq sqrt(P_max)
+    float amb_floor = 0.f;
+    double rcoef[kMaxTones] = {};  // 2 cos(2 pi f_k / fs) in double, the caller's tone order
+    double *d_rtw = nullptr;    // FFT: radix-2 twiddles (cos, sin)(-2 pi j / len), [n - 1]
     float coef[kMaxTones] = {};
     float sgn[kMaxTones] = {};  // plain detector, Reinsch form: sign of cos(w_k)
     bool reinsch = false;       // plain detector: Reinsch-modified recurrence
@@ -174,6 +181,14 @@ static int validate(const demod_cfg_t *c)
     return DEMOD_OK;
 }
 
+// Decision rescue threshold factor tau. The largest fp32
+// power error any detector showed against the double oracle, as a fraction
+// r of sqrt(P_max n sum x^2), over every signal family of
+// scripts/precision_probe.py, is 2.67e-6 (plain bank, clean tones;
+// fold / residue 1.2e-6, FFT 2.6e-7: profiles/round3/precision_probe.log).
+// A margin carries the errors of two powers: tau = 2 r x 6 (safety).
+constexpr double kAmbTau = 3.2e-5;
+
 static int init_device_state(demod_t *st)
 {
     const demod_cfg_t &c = st->cfg;
@@ -235,8 +250,25 @@ static int init_device_state(demod_t *st)
         for (uint32_t k = 0; k < c.k; ++k) {
             long b = std::lround(c.freqs[k] * c.n / c.fs);
             bins[k] = (int)std::min<long>(std::max<long>(b, 0), c.n / 2);
+            st->fft_bins[k] = bins[k];
             st->fft_slot[k] = fft_quad_slot(bins[k]);
         }
+        // the rescue's radix-2 twiddles: stage len (2 .. n), j < len / 2 at
+        // len / 2 - 1 + j, each the (cos, sin) of (-2 pi / len) j exactly as
+        // the double FFT of the definition evaluates it (one libm sincos of
+        // the same rounded argument)
+        std::vector<double> rtw(2 * (size_t)(c.n - 1));
+        for (uint32_t len = 2; len <= c.n; len <<= 1) {
+            const double ang = -(2.0 * M_PI) / (double)len;
+            for (uint32_t j = 0; j < len / 2; ++j) {
+                double sn, cs;
+                sincos(ang * (double)j, &sn, &cs);
+                rtw[2 * (len / 2 - 1 + j)] = cs;
+                rtw[2 * (len / 2 - 1 + j) + 1] = sn;
+            }
+        }
+        HIP_TRY(hipMalloc(&st->d_rtw, rtw.size() * sizeof(double)));
+        HIP_TRY(hipMemcpy(st->d_rtw, rtw.data(), rtw.size() * sizeof(double), hipMemcpyHostToDevice));
         HIP_TRY(hipMalloc(&st->d_tw512, t1.size() * sizeof(float)));
         HIP_TRY(hipMalloc(&st->d_tw1024, t2.size() * sizeof(float)));
         HIP_TRY(hipMalloc(&st->d_bins, bins.size() * sizeof(int)));
@@ -358,6 +390,20 @@ static int init_device_state(demod_t *st)
     }
     HIP_TRY(hipMalloc(&st->d_rot, rot.size() * sizeof(float4)));
     HIP_TRY(hipMemcpy(st->d_rot, rot.data(), rot.size() * sizeof(float4), hipMemcpyHostToDevice));
+    // Decision rescue: the double coefficients of the
+    // definition's recurrence (the same libm cos of the same rounded argument
+    // as the double oracle), and the detectors' ambiguity threshold
+    // tau sqrt(Q) sqrt(P_max), Q = n^2 2^30 (>= n sum x^2 for int16 input),
+    // plus the floor tau^2 Q / 16 below which the fp32 error's second-order
+    // term could reach the margin.
+    for (uint32_t k = 0; k < c.k; ++k) st->rcoef[k] = 2.0 * std::cos(2.0 * M_PI * c.freqs[k] / c.fs);
+    const char *no_rescue = std::getenv("FSKD_NO_RESCUE");  // measurement switch
+    st->rescue = c.k >= 2 && !(no_rescue && no_rescue[0] == '1');
+    if (st->rescue) {
+        const double sq = (double)c.n * 32768.0;  // sqrt(Q)
+        st->amb_tq = (float)(kAmbTau * sq);
+        st->amb_floor = (float)(kAmbTau * kAmbTau * sq * sq / 16.0);
+    }
     st->slide_wt = 0;
     if (slide && st->detector == kDetGoertzel)
         st->slide_wt = (64 - 16) / (int)(c.hop / 64) + 1;  // the last window's 16 segments end in the tile
@@ -376,6 +422,7 @@ static void free_state(demod_t *st)
     if (st->d_tw512) (void)hipFree(st->d_tw512);
     if (st->d_tw1024) (void)hipFree(st->d_tw1024);
     if (st->d_bins) (void)hipFree(st->d_bins);
+    if (st->d_rtw) (void)hipFree(st->d_rtw);
     if (st->d_in) (void)hipFree(st->d_in);
     if (st->d_sym) (void)hipFree(st->d_sym);
     if (st->d_mag) (void)hipFree(st->d_mag);
@@ -493,8 +540,35 @@ int demod_batch_launches(const demod_t *st, size_t n_windows, int with_mags)
     if (!st) return DEMOD_BAD_ARG;
     if (n_windows == 0) return 0;
     const size_t per = launch_slice(st, n_windows, with_mags != 0);
-    const size_t n = (n_windows + per - 1) / per;
+    const size_t n = (n_windows + per - 1) / per + (st->rescue ? 1 : 0);
     return n > 0x7FFFFFFF ? 0x7FFFFFFF : (int)n;
+}
+
+// The decision rescue over a batch's windows (rescue.hip), after its detector
+// launches on the same stream.
+static int enqueue_rescue(demod_t *st, const int16_t *d_pcm, size_t n_windows, uint8_t *d_sym,
+                          float *d_mag, float *d_spec, hipStream_t s)
+{
+    if (!st->rescue || n_windows == 0) return DEMOD_OK;
+    RescueParams r;
+    std::memset(&r, 0, sizeof(r));
+    r.pcm = d_pcm;
+    r.n_windows = (long long)n_windows;
+    r.hop = st->cfg.hop;
+    r.n = (int)st->cfg.n;
+    r.k = (int)st->cfg.k;
+    r.fft = st->detector == kDetFft ? 1 : 0;
+    r.sym = d_sym;
+    r.sym_aligned4 = ((uintptr_t)d_sym & 3) == 0;
+    r.mag = d_mag;
+    r.spec = d_spec;
+    r.tw = st->d_rtw;
+    for (uint32_t k = 0; k < st->cfg.k; ++k) {
+        r.bins[k] = st->fft_bins[k];
+        r.coef[k] = st->rcoef[k];
+    }
+    HIP_TRY(launch_rescue(r, s));
+    return DEMOD_OK;
 }
 
 int demod_max_symbols(const demod_t *st, size_t n_frames)
@@ -522,8 +596,11 @@ static int enqueue_fft(demod_t *st, const int16_t *d_pcm, size_t n_windows, uint
     p.sym = d_sym;
     p.mag = d_mag;
     p.spec = d_spec;
+    p.amb_tq = st->amb_tq;
+    p.amb_floor = st->amb_floor;
     HIP_TRY(launch_fft_quad(p, s));
-    return (int)n_windows;
+    const int rc = enqueue_rescue(st, d_pcm, n_windows, d_sym, d_mag, d_spec, s);
+    return rc < 0 ? rc : (int)n_windows;
 }
 
 
@@ -560,6 +637,8 @@ static int enqueue_batch(demod_t *st, const int16_t *d_pcm, size_t n_windows, ui
     // same line (2-FSK: 0.325 -> 0.305 ms), and overlapping
     // windows find their shared lines there
     p.xcd_swizzle = 1;
+    p.amb_tq = st->amb_tq;
+    p.amb_floor = st->amb_floor;
     const size_t per = launch_slice(st, n_windows, d_mag != nullptr);
     for (size_t w0 = 0; w0 < n_windows; w0 += per) {
         const size_t cnt = std::min(per, n_windows - w0);
@@ -569,7 +648,8 @@ static int enqueue_batch(demod_t *st, const int16_t *d_pcm, size_t n_windows, ui
         p.mag = d_mag ? d_mag + w0 * st->cfg.k : nullptr;
         HIP_TRY(launch_detector(st->detector, p, s));
     }
-    return (int)n_windows;
+    const int rc = enqueue_rescue(st, d_pcm, n_windows, d_sym, d_mag, nullptr, s);
+    return rc < 0 ? rc : (int)n_windows;
 }
 
 static int ensure_dev(demod_t *st, size_t samples, size_t windows, bool mags)

@@ -44,7 +44,59 @@ struct GoertzelParams {
     // 1: overlapping windows (hop < n) share lines between tiles, so the loads
     // keep them in L2 (plain policy); 0: each byte is read once (nt)
     int cached;
+    // decision rescue (rescue.hip): ambiguity test constants
+    float amb_tq;            // threshold = amb_tq * sqrt(P_max); 0: no flagging
+    float amb_floor;         // 0 < P_max < amb_floor: always ambiguous
 };
+
+// Decision rescue. A detector's fp32 powers carry an error
+// |dP_k| <= r sqrt(P_max NE), NE = n sum x^2 <= Q = n^2 2^30 for int16 input
+// (r measured per detector, scripts/precision_probe.py). Where the fp32 top-2
+// margin is below amb_tq sqrt(P_max) (amb_tq = tau sqrt(Q), tau = 12 r), or
+// P_max is so small that the second-order term could dominate, the fp32
+// argmax may differ from the exact one: the detector sets kSymAmbiguous on
+// the window's symbol and rescue_kernel re-decides it with the definition's
+// double-precision arithmetic (bit-identical to oracle/fsk_oracle.c).
+// P_max == 0 (every tone power exactly zero: silence) is decided as a tie
+// (tone 0) without a rescue.
+constexpr uint8_t kSymAmbiguous = 0x80;
+
+__device__ __forceinline__ bool amb_margin(float p1, float p2, float tq, float fl)
+{
+    return tq > 0.f && p1 > 0.f && (p1 - p2 < tq * __builtin_amdgcn_sqrtf(p1) || p1 < fl);
+}
+
+// Sequential argmax (ties to the lowest k) that also keeps the runner-up, for
+// the detectors' K-tone chains where every lane holds every P_k.
+template <int K>
+__device__ __forceinline__ int chain_argmax(const float (&P)[K], float &p1, float &p2)
+{
+    float best = -1.f, second = -1.f;
+    int arg = 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        if (P[k] > best) {
+            second = best;
+            best = P[k];
+            arg = k;
+        } else if (P[k] > second) {
+            second = P[k];
+        }
+    }
+    p1 = best;
+    p2 = second;
+    return arg;
+}
+
+// The symbol byte a chain decision stores (K >= 2: ambiguous windows flagged).
+template <int K>
+__device__ __forceinline__ uint8_t chain_symbol(const float (&P)[K], float tq, float fl)
+{
+    float p1, p2;
+    const int arg = chain_argmax<K>(P, p1, p2);
+    const bool amb = K >= 2 && amb_margin(p1, p2, tq, fl);
+    return (uint8_t)(arg | (amb ? kSymAmbiguous : 0));
+}
 
 // Output store; NTS = non-temporal (streamed once, never re-read by the kernel).
 template <bool NTS, typename T>
@@ -83,7 +135,27 @@ struct FftParams {
     uint8_t *sym;
     float *mag;              // [n_windows][k] or nullptr
     float *spec;             // [n_windows][513] or nullptr
+    float amb_tq;            // decision rescue, as GoertzelParams
+    float amb_floor;
 };
+
+// rescue.hip: re-decides every window whose symbol carries kSymAmbiguous.
+struct RescueParams {
+    const int16_t *pcm;      // window w at pcm + w * hop (the batch's first window)
+    long long n_windows;
+    long long hop;
+    int n;
+    int k;
+    int fft;                 // 0: Goertzel recurrence, 1: radix-2 FFT (n = 1024)
+    uint8_t *sym;
+    int sym_aligned4;        // sym is 4-byte aligned: dword scans
+    float *mag;              // [n_windows][k] or nullptr
+    float *spec;             // [n_windows][n / 2 + 1] or nullptr (fft)
+    const double *tw;        // fft: [n - 1] (cos, sin), stage len at len / 2 - 1 + j
+    int bins[kMaxTones];     // fft: tone bins
+    double coef[kMaxTones];  // Goertzel: 2 cos(2 pi f_k / fs), the caller's tone order
+};
+hipError_t launch_rescue(const RescueParams &p, hipStream_t s);
 
 struct SynthParams {
     uint64_t seed;

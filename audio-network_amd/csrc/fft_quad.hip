@@ -961,7 +961,7 @@ __device__ __attribute__((always_inline)) inline void fft1024_quad_body(const Ff
         asm("v_pk_add_f32 %0, %1, %1 op_sel:[0,1] op_sel_hi:[0,1] neg_hi:[0,1]" : "=v"(px) : "v"(b[0]));
         px = px * px;
         const bool live = w < p.n_windows;
-        float pk = -1.f;
+        float pk = -1.f, pk2 = -1.f;  // the best (and runner-up) tone power this lane holds
         int arg = t < p.k ? t : kMaxTones;  // kMaxTones: this lane holds no tone
         if constexpr (SPEC) {
             if (l0) {
@@ -995,15 +995,22 @@ __device__ __attribute__((always_inline)) inline void fft1024_quad_body(const Ff
                 const float val = f >= 512 ? (f == 512 ? px.x : px.y) : pv[((f >> 5) << 1) | (f & 1)];
                 if (own && live && p.mag) p.mag[w * p.k + i] = val;
                 if (own && val > pk) {
+                    pk2 = pk;
                     pk = val;
                     arg = i;
+                } else if (own && val > pk2) {
+                    pk2 = val;
                 }
             }
         }
         // row argmax, ties to the lowest tone: the two DPP max passes of
         // window_sum.h (powers >= 0, so their bits order as unsigned)
-        arg = (int)ws_argmax<false>(__float_as_uint(pk), arg < kMaxTones, arg);
-        if (live && t == 0) p.sym[w] = (uint8_t)arg;
+        const bool owns = arg < kMaxTones;
+        float mx;
+        arg = (int)ws_argmax_m<false>(__float_as_uint(pk), owns, arg, 0u, false, 0, mx);
+        // decision rescue: a runner-up within the threshold
+        const bool amb = p.k >= 2 && ws_ambiguous(mx, pk, owns, pk2, pk2 >= 0.f, p.amb_tq, p.amb_floor);
+        if (live && t == 0) p.sym[w] = (uint8_t)(arg | (amb ? kSymAmbiguous : 0));
         if constexpr (SPEC && SPL) {
             if (p.spec) {
                 // the group's live windows: floats [0, L) of the slab = the

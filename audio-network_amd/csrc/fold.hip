@@ -87,7 +87,8 @@ __device__ __forceinline__ void fold_decide(const int (&acc)[8], const float4 *r
             xr[2 * h + 1] = X1.x;
             xi[2 * h + 1] = X1.y;
         }
-        window_sum_decide_split8<true>(xr, xi, lane, w, live, p.sym, p.mag, p.perm);
+        window_sum_decide_split8<true>(xr, xi, lane, w, live, p.sym, p.mag, p.perm, p.amb_tq,
+                                       p.amb_floor);
     } else {
         float xr[K], xi[K];
         constexpr int HP = K / 2;  // packed tone pairs; an odd last tone runs scalar
@@ -117,7 +118,7 @@ __device__ __forceinline__ void fold_decide(const int (&acc)[8], const float4 *r
             xr[K - 1] = r[K - 1].x * s1 - r[K - 1].z * s2;
             xi[K - 1] = r[K - 1].y * s1 - r[K - 1].w * s2;
         }
-        window_sum_decide<K>(xr, xi, lane, w, live, p.sym, p.mag);
+        window_sum_decide<K>(xr, xi, lane, w, live, p.sym, p.mag, 0, p.amb_tq, p.amb_floor);
     }
 }
 
@@ -271,11 +272,10 @@ __global__ __launch_bounds__(64 * WPB) void fold_tile_kernel(GoertzelParams p)
                 xi[k] = rk.y * t1[k] - rk.w * t2[k];
             }
             const long long w = wbase + win_in_tile;
-            window_sum_decide<K>(xr, xi, lane, w, w < p.n_windows, p.sym, p.mag);
+            window_sum_decide<K>(xr, xi, lane, w, w < p.n_windows, p.sym, p.mag, 0, p.amb_tq,
+                                 p.amb_floor);
             continue;
         }
-        float best = -1.f;
-        int arg = 0;
         float P[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) {
@@ -292,12 +292,11 @@ __global__ __launch_bounds__(64 * WPB) void fold_tile_kernel(GoertzelParams p)
             re = group_sum_f(re, log2g);
             im = group_sum_f(im, log2g);
             P[k] = fmaf(re, re, im * im);
-            if (P[k] > best) { best = P[k]; arg = k; }
         }
 
         const long long w = wbase + win_in_tile;
         if (w < p.n_windows) {
-            if (j == 0) out_store<NTS>(p.sym + w, (uint8_t)arg);
+            if (j == 0) out_store<NTS>(p.sym + w, chain_symbol<K>(P, p.amb_tq, p.amb_floor));
             if (p.mag) {
 #pragma unroll
                 for (int k = 0; k < K; ++k)

@@ -292,19 +292,16 @@ __global__ __launch_bounds__(64 * WPB) void goertzel_tile_kernel(GoertzelParams 
                     }
                 }
                 if constexpr (WS) {
-                    window_sum_decide<K>(xr, xi, lane, w, live, p.sym, p.mag);
+                    window_sum_decide<K>(xr, xi, lane, w, live, p.sym, p.mag, 0, p.amb_tq, p.amb_floor);
                 } else {
-                    float best = -1.f;
-                    int arg = 0;
                     float P[K];
 #pragma unroll
                     for (int k = 0; k < K; ++k) {
                         const float re = group_sum(xr[k], 4), im = group_sum(xi[k], 4);
                         P[k] = fmaf(re, re, im * im);
-                        if (P[k] > best) { best = P[k]; arg = k; }
                     }
                     if (live) {
-                        if (seg == 0) out_store<NTS>(p.sym + w, (uint8_t)arg);
+                        if (seg == 0) out_store<NTS>(p.sym + w, chain_symbol<K>(P, p.amb_tq, p.amb_floor));
                         if (p.mag) {
 #pragma unroll
                             for (int k = 0; k < K; ++k)
@@ -330,11 +327,10 @@ __global__ __launch_bounds__(64 * WPB) void goertzel_tile_kernel(GoertzelParams 
                 xr[k] = X.x;
                 xi[k] = X.y;
             }
-            window_sum_decide<K>(xr, xi, lane, w, w < p.n_windows, p.sym, p.mag);
+            window_sum_decide<K>(xr, xi, lane, w, w < p.n_windows, p.sym, p.mag, 0, p.amb_tq,
+                                 p.amb_floor);
             return;
         }
-        float best = -1.f;
-        int arg = 0;
         float P[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) {
@@ -343,11 +339,10 @@ __global__ __launch_bounds__(64 * WPB) void goertzel_tile_kernel(GoertzelParams 
             re = group_sum(re, log2g);
             im = group_sum(im, log2g);
             P[k] = fmaf(re, re, im * im);
-            if (P[k] > best) { best = P[k]; arg = k; }
         }
 
         if (w < p.n_windows) {
-            if (seg == 0) out_store<NTS>(p.sym + w, (uint8_t)arg);
+            if (seg == 0) out_store<NTS>(p.sym + w, chain_symbol<K>(P, p.amb_tq, p.amb_floor));
             if (p.mag) {
 #pragma unroll
                 for (int k = 0; k < K; ++k)

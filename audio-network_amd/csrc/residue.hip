@@ -353,22 +353,20 @@ void residue_tile_kernel(GoertzelParams p)
         }
         const long long w = wbase + win_in_tile;
         if constexpr (WS && LOG2G == 4) {
-            window_sum_decide<K, DCLS>(xr, xi, lane, w, w < p.n_windows, p.sym, p.mag, p.perm);
+            window_sum_decide<K, DCLS>(xr, xi, lane, w, w < p.n_windows, p.sym, p.mag, p.perm,
+                                       p.amb_tq, p.amb_floor);
             continue;
         }
         static_assert(!DCLS || (WS && LOG2G == 4), "DCLS un-permutes in the window_sum epilogue");
-        float best = -1.f;
-        int arg = 0;
         float P[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const float re = group_sum_r(xr[k], log2g);
             const float im = group_sum_r(xi[k], log2g);
             P[k] = fmaf(re, re, im * im);
-            if (P[k] > best) { best = P[k]; arg = k; }
         }
         if (w < p.n_windows) {
-            if (j == 0) p.sym[w] = (uint8_t)arg;
+            if (j == 0) p.sym[w] = chain_symbol<K>(P, p.amb_tq, p.amb_floor);
             if (p.mag) {
 #pragma unroll
                 for (int k = 0; k < K; ++k)

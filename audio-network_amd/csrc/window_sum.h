@@ -87,13 +87,23 @@ __device__ __forceinline__ void ws_stage(float (&v)[V], int lane)
     }
 }
 
+// Sum over a 16-lane row, every lane ending with the total.
+__device__ __forceinline__ unsigned ws_rowsum_u(unsigned c)
+{
+    c += ws_dpp_u<0xB1>(c);
+    c += ws_dpp_u<0x4E>(c);
+    c += ws_dpp_u<0x141>(c);
+    c += ws_dpp_u<0x140>(c);
+    return c;
+}
+
 // Exact argmax over a 16-lane row (one window): lane candidates (bits of a
 // power P >= 0, ok, tone index o); a second candidate per lane when TWO (K > 8).
 // Returns the winning tone in every lane of the row: the largest P, and among
-// equal P the lowest o.
+// equal P the lowest o. `mx` receives the row's largest power.
 template <bool TWO>
-__device__ __forceinline__ unsigned ws_argmax(unsigned pb0, bool ok0, int o0, unsigned pb1 = 0u,
-                                              bool ok1 = false, int o1 = 0)
+__device__ __forceinline__ unsigned ws_argmax_m(unsigned pb0, bool ok0, int o0, unsigned pb1,
+                                                bool ok1, int o1, float &mx)
 {
     unsigned m = ok0 ? pb0 : 0u;
     if constexpr (TWO) m = max(m, ok1 ? pb1 : 0u);
@@ -101,6 +111,7 @@ __device__ __forceinline__ unsigned ws_argmax(unsigned pb0, bool ok0, int o0, un
     m = max(m, ws_dpp_u<0x4E>(m));
     m = max(m, ws_dpp_u<0x141>(m));
     m = max(m, ws_dpp_u<0x140>(m));
+    mx = __uint_as_float(m);
     // every lane now holds the row's max; key 16 - o marks the lanes holding it
     unsigned key = (ok0 && pb0 == m) ? (unsigned)(16 - o0) : 0u;
     if constexpr (TWO) key = max(key, (ok1 && pb1 == m) ? (unsigned)(16 - o1) : 0u);
@@ -111,15 +122,39 @@ __device__ __forceinline__ unsigned ws_argmax(unsigned pb0, bool ok0, int o0, un
     return 16u - key;
 }
 
+template <bool TWO>
+__device__ __forceinline__ unsigned ws_argmax(unsigned pb0, bool ok0, int o0, unsigned pb1 = 0u,
+                                              bool ok1 = false, int o1 = 0)
+{
+    float mx;
+    return ws_argmax_m<TWO>(pb0, ok0, o0, pb1, ok1, o1, mx);
+}
+
+// Decision-rescue test over a row (demod_internal.h
+// amb_margin): the window is ambiguous when a second tone's power lies within
+// the threshold of the row's max mx (the max's own lane counts once), or mx is
+// below the floor; mx == 0 is silence, decided without a rescue. Every lane
+// of the row gets the same answer.
+__device__ __forceinline__ bool ws_ambiguous(float mx, float a0, bool ok0, float a1, bool ok1,
+                                             float tq, float fl)
+{
+    if (!(tq > 0.f)) return false;
+    const float thr = tq * __builtin_amdgcn_sqrtf(mx);
+    const unsigned c = ws_rowsum_u((ok0 && mx - a0 < thr ? 1u : 0u) + (ok1 && mx - a1 < thr ? 1u : 0u));
+    return mx > 0.f && (c >= 2u || mx < fl);
+}
+
 // X[k] = this lane's partial (re, im) of tone k. Writes the symbol of window
 // w (lane j == 0) and, if mag, its K magnitudes; `live` = w is a real window.
 // PERM: the kernel's tone slot s holds the host's tone (perm >> 4 s) & 15
 // (residue.hip DCLS); magnitudes, the tie rule and the symbol use that index.
+// tq / fl: the decision rescue's ambiguity test (tq = 0: off); an ambiguous
+// window's symbol carries kSymAmbiguous for rescue_kernel.
 template <int K, bool PERM = false>
 __device__ __forceinline__ void window_sum_decide(const float (&re)[K], const float (&im)[K],
                                                   int lane, long long w, bool live,
                                                   uint8_t *sym, float *mag,
-                                                  unsigned long long perm = 0)
+                                                  unsigned long long perm, float tq, float fl)
 {
     static_assert(K >= 1 && K <= 16, "tones");
     constexpr int KP = K <= 1 ? 1 : K <= 2 ? 2 : K <= 4 ? 4 : K <= 8 ? 8 : 16;
@@ -155,9 +190,11 @@ __device__ __forceinline__ void window_sum_decide(const float (&re)[K], const fl
         if (ok0) mag[w * K + o0] = P0;
         if (ok1) mag[w * K + o1] = P1;
     }
-    const unsigned arg = ws_argmax<(V > 16)>(__float_as_uint(P0), ok0, o0, __float_as_uint(P1),
-                                             ok1, o1);
-    if (live && j == 0) sym[w] = (uint8_t)arg;
+    float mx;
+    const unsigned arg = ws_argmax_m<(V > 16)>(__float_as_uint(P0), ok0, o0, __float_as_uint(P1),
+                                               ok1, o1, mx);
+    const bool amb = K >= 2 && ws_ambiguous(mx, P0, ok0, P1, ok1, tq, fl);
+    if (live && j == 0) sym[w] = (uint8_t)(arg | (amb ? kSymAmbiguous : 0u));
 }
 
 // The same epilogue for K = 8 when the kernel has already split the tones by
@@ -169,7 +206,7 @@ template <bool PERM = false>
 __device__ __forceinline__ void window_sum_decide_split8(const float (&re)[4], const float (&im)[4],
                                                          int lane, long long w, bool live,
                                                          uint8_t *sym, float *mag,
-                                                         unsigned long long perm = 0)
+                                                         unsigned long long perm, float tq, float fl)
 {
     constexpr int K = 8;
     float v[8];
@@ -189,8 +226,10 @@ __device__ __forceinline__ void window_sum_decide_split8(const float (&re)[4], c
     const float P0 = sq + ws_dpp<0xB1>(sq);
     const int o0 = PERM ? (int)((perm >> (4 * t0)) & 15u) : t0;
     if (live && mag && re_lane) mag[w * K + o0] = P0;
-    const unsigned arg = ws_argmax<false>(__float_as_uint(P0), re_lane, o0);
-    if (live && j == 0) sym[w] = (uint8_t)arg;
+    float mx;
+    const unsigned arg = ws_argmax_m<false>(__float_as_uint(P0), re_lane, o0, 0u, false, 0, mx);
+    const bool amb = ws_ambiguous(mx, P0, re_lane, 0.f, false, tq, fl);
+    if (live && j == 0) sym[w] = (uint8_t)(arg | (amb ? kSymAmbiguous : 0u));
 }
 
 }  // namespace fskd

@@ -58,16 +58,32 @@ def test_bench_help_lists_the_contract_flags():
         assert flag in out
 
 
-def test_decision_checker_accepts_exact_argmax_and_band_ties():
+def test_decision_checker_requires_the_oracle_symbol_everywhere():
     ref_P = np.array([[10.0, 1.0], [1.0, 10.0], [5.0, 5.0 * (1 - BAND / 2)], [0.0, 0.0]])
     ref_sym = ref_P.argmax(axis=1)
     mag = ref_P.astype(np.float32).copy()
     sym = mag.argmax(axis=1)
     assert check_decisions(sym, mag, ref_sym, ref_P) == 2      # the near tie and the zero window
-    # inside the band the GPU may resolve the near tie the other way
+    # a near tie the fp32 powers resolve the other way is a mismatch: the
+    # rescue must have decided it in double
     mag2 = mag.copy()
     mag2[2] = [4.9999, 5.0]
-    assert check_decisions(mag2.argmax(axis=1), mag2, ref_sym, ref_P) == 2
+    with pytest.raises(AssertionError):
+        check_decisions(mag2.argmax(axis=1), mag2, ref_sym, ref_P)
+    # a rescued window: double decision, fp32-rounded powers tied
+    ref3 = np.array([[1.0 + 2e-9, 1.0]])
+    assert check_decisions(np.array([0]), ref3.astype(np.float32), np.array([0]), ref3) == 1
+    # ... but never a leftover ambiguous flag
+    with pytest.raises(AssertionError):
+        check_decisions(np.array([0x80]), None, np.array([0]), ref3)
+
+
+def test_decision_checker_silence_exemption_needs_the_energy_scale():
+    ref_P = np.array([[1e-16, 3e-16]])                         # rounding noise of a zero tone content
+    mag = np.zeros((1, 2), np.float32)
+    with pytest.raises(AssertionError):
+        check_decisions(np.array([0]), mag, np.array([1]), ref_P)
+    assert check_decisions(np.array([0]), mag, np.array([1]), ref_P, denom=np.array([1e9])) == 1
 
 
 def test_decision_checker_rejects_wrong_decisions():
@@ -77,5 +93,5 @@ def test_decision_checker_rejects_wrong_decisions():
     with pytest.raises(AssertionError):                        # not the argmax of its own powers
         check_decisions(np.array([1, 1]), mag, ref_sym, ref_P)
     bad = mag[:, ::-1].copy()
-    with pytest.raises(AssertionError):                        # differs from the oracle outside the band
+    with pytest.raises(AssertionError):                        # differs from the oracle
         check_decisions(bad.argmax(axis=1), bad, ref_sym, ref_P)

@@ -5,10 +5,14 @@ eps in {0, 1e-7 .. 1e-4}, in both orders (so the higher-index tone is
 sometimes the larger one), with random phases. int16 rounding then spreads
 the realised power ratios over a few 1e-6 around eps: many windows fall
 inside 2^-19 (the band the round-1 packed-key argmax resolved to the lower
-tone whatever the powers said). The decision must be the exact argmax of
-the returned fp32 powers (ties to the lowest tone) on every window, and the
-oracle's wherever its margin is outside the fp32 band (tests/decision.py).
+tone whatever the powers said), far inside the fp32 error of the powers.
+Every decision must equal the double oracle's (tests/decision.py): the
+detectors flag these windows and the decision rescue decides them with the
+oracle's own double arithmetic (rescue.hip). With the rescue
+switched off (FSKD_NO_RESCUE=1, a measurement switch) the fp32 decisions
+differ from the oracle on some of them: the rescue is what makes them exact.
 """
+import os
 import zlib
 
 import numpy as np
@@ -97,13 +101,27 @@ def test_near_ties_follow_exact_argmax(A, O, torch, plan, method):
     assert tight.sum() >= 20, tight.sum()
     assert (tight & hi_wins).sum() >= 5, (tight & hi_wins).sum()
     assert in_band > 0
+    # the same windows decided in fp32 alone: some differ from the oracle
+    old = os.environ.get("FSKD_NO_RESCUE")
+    os.environ["FSKD_NO_RESCUE"] = "1"
+    try:
+        with A.Demodulator(freqs=freqs, method=method) as d:
+            sym32 = d.batch(x)
+    finally:
+        if old is None:
+            del os.environ["FSKD_NO_RESCUE"]
+        else:
+            os.environ["FSKD_NO_RESCUE"] = old
+    assert (sym32 & 0x80).sum() == 0
+    assert (sym32 != ref_sym).sum() > 0
+    assert (sym32 == sym).mean() > 0.9
 
 
 @pytest.mark.parametrize("plan,method", [("FSK8_FREQS", FOLDED), ("FSK8_ODD", RESIDUE),
                                          ("FSK8_FREQS", GOERTZEL)])
 def test_exact_fp32_ties_go_to_lowest_tone(A, torch, plan, method):
-    """Windows with every tone at exactly 0 power (silence, and tones off the
-    plan on another bin) — exact ties in fp32 — decide the lowest tone."""
+    """Windows with every tone at exactly 0 power (silence) — exact ties in
+    fp32 and in double — decide the lowest tone, without a rescue."""
     freqs = A.FSK8_FREQS if plan == "FSK8_FREQS" else FSK8_ODD
     x = np.zeros((4, 1024), np.int16)
     with A.Demodulator(freqs=freqs, method=method) as d:

@@ -259,18 +259,15 @@ def test_zero_and_extreme_input(A, O, torch, method):
     denom = np.maximum(ref_P.max(axis=1), energy)
     err = (np.abs(mag[1:].astype(np.float64) - ref_P[1:]).max(axis=1) / denom[1:]).max()
     assert err <= MAG_TOL
-    # Symbols must match wherever the decision is well-posed. DC (rows 1, 2)
-    # and Nyquist (row 3) windows put exactly zero true energy on both tones
-    # (and the unit impulse, row 5, exactly equal energy on both):
-    # both P are rounding noise (oracle: ~1e-16 vs ~1e-22), a tie in exact
-    # arithmetic that no finite-precision argmax can reproduce bit-for-bit.
-    Ps = np.sort(ref_P, axis=1)
-    margin = (Ps[:, -1] - Ps[:, -2]) / np.maximum(denom, 1e-30)
-    posed = margin > 4 * MAG_TOL
-    assert set(np.flatnonzero(~posed)) <= {0, 1, 2, 3, 5}  # 5: impulse, P = 1 at every tone
-    assert (sym[posed] == ref_sym[posed]).all()
-    # and on every window, ties included: the exact argmax of the returned powers
-    check_decisions(sym, mag, ref_sym, ref_P, np.maximum(denom, 1e-30))
+    # Every symbol equals the double oracle's, including the windows whose
+    # tone content is exactly zero or exactly tied: DC (rows 1, 2) and Nyquist
+    # (row 3) put zero true power on both tones, the unit impulse (row 5)
+    # exactly equal power; their fp32 margins are inside the error bound, so
+    # the rescue decides them with the oracle's own double arithmetic
+    # (DESIGN.md §2a). The energy scale lets a window whose fp32 tone powers
+    # are exactly 0 pass as silence (tests/decision.py).
+    n_band = check_decisions(sym, mag, ref_sym, ref_P, np.maximum(denom, 1e-30))
+    assert n_band >= 4  # rows 0 (all zero), 1, 2, 3 and 5 are exact ties
 
 
 @pytest.mark.parametrize("method", [GOERTZEL, RESIDUE])
@@ -298,10 +295,6 @@ def test_extreme_input_every_residue_class(A, O, torch, method):
     xe = x.astype(np.float64)
     denom = np.maximum(np.maximum(ref_P.max(axis=1), n * (xe * xe).sum(axis=1) / 2), 1.0)
     assert (np.abs(mag.astype(np.float64) - ref_P).max(axis=1) / denom).max() <= MAG_TOL
-    Ps = np.sort(ref_P, axis=1)
-    posed = (Ps[:, -1] - Ps[:, -2]) / denom > 4 * MAG_TOL
-    assert posed[[4, 5, 6, 7, 8, 9, 10]].all()
-    assert (sym[posed] == ref_sym[posed]).all()
     check_decisions(sym, mag, ref_sym, ref_P, denom)
 
 
@@ -310,9 +303,10 @@ def test_extreme_input_every_residue_class(A, O, torch, method):
 def test_ties_k8(A, O, torch, freqs, method):
     """window_sum.h decision rule (K = 8 kernels): an exact tie (the all-zero
     window: every power 0) goes to the lowest tone. A unit impulse puts
-    exactly equal power x^2 on every tone too, but the fp32 powers differ by
+    exactly equal power x^2 on every tone too; the fp32 powers differ by
     ~1e-6 relative (rounding of the rotation constants, amplified by the
-    recurrence): the symbol is then the exact argmax of those fp32 powers."""
+    recurrence), inside the error bound, so the rescue decides these windows
+    with the oracle's double arithmetic and the symbol is the oracle's."""
     f = {"FSK8_FREQS": A.FSK8_FREQS, "FSK8_ODD": FSK8_ODD,
          "NONINT8": tuple(1234.5 + 1111.1 * i for i in range(8))}[freqs]
     n = 1024
@@ -326,9 +320,8 @@ def test_ties_k8(A, O, torch, freqs, method):
     ref_sym, ref_P = O.goertzel(x, f, n)
     for r in range(1, 5):
         assert np.abs(mag[r] / ref_P[r] - 1).max() <= MAG_TOL  # every tone at x^2
-    # the impulse windows are exact mathematical ties: the pick is still the
-    # exact argmax of the returned fp32 powers
-    check_decisions(sym, mag, ref_sym, ref_P)
+    # the impulse windows are exact mathematical ties, decided as the oracle does
+    assert check_decisions(sym, mag, ref_sym, ref_P) >= 4
 
 
 def test_device_pointers_and_async(A, O, torch):
