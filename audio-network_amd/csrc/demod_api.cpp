@@ -11,9 +11,12 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
-#include <thread>
+#include <condition_variable>
 #include <cstring>
+#include <functional>
+#include <mutex>
 #include <new>
+#include <thread>
 #include <vector>
 
 #include "../../include/demod.h"
@@ -181,13 +184,21 @@ static int validate(const demod_cfg_t *c)
     return DEMOD_OK;
 }
 
-// Decision rescue threshold factor tau. The largest fp32
-// power error any detector showed against the double oracle, as a fraction
-// r of sqrt(P_max n sum x^2), over every signal family of
-// scripts/precision_probe.py, is 2.67e-6 (plain bank, clean tones;
-// fold / residue 1.2e-6, FFT 2.6e-7: profiles/round3/precision_probe.log).
-// A margin carries the errors of two powers: tau = 2 r x 6 (safety).
-constexpr double kAmbTau = 3.2e-5;
+// Decision rescue threshold factor tau per detector. The
+// largest fp32 power error each detector showed against the double oracle,
+// as a fraction r of sqrt(P_max n sum x^2), over every signal family and
+// kernel path of scripts/precision_probe.py (profiles/round3/
+// precision_probe.log): plain bank (direct, SLIDE, Reinsch, any n) 2.67e-6,
+// fold / fold-slide / residue 1.19e-6, FFT 2.64e-7. A margin carries the
+// errors of two powers: tau = 2 r x 6 (safety).
+// The fold / residue figure was measured at n = 1024; other window lengths
+// keep the plain bank's.
+static double amb_tau(int detector, int log2g)
+{
+    if (detector == kDetFft) return 12.0 * 2.64e-7;
+    if ((detector == kDetFolded || detector == kDetResidue) && log2g == 4) return 12.0 * 1.19e-6;
+    return 12.0 * 2.67e-6;
+}
 
 static int init_device_state(demod_t *st)
 {
@@ -401,8 +412,9 @@ static int init_device_state(demod_t *st)
     st->rescue = c.k >= 2 && !(no_rescue && no_rescue[0] == '1');
     if (st->rescue) {
         const double sq = (double)c.n * 32768.0;  // sqrt(Q)
-        st->amb_tq = (float)(kAmbTau * sq);
-        st->amb_floor = (float)(kAmbTau * kAmbTau * sq * sq / 16.0);
+        const double tau = amb_tau(st->detector, st->log2g);
+        st->amb_tq = (float)(tau * sq);
+        st->amb_floor = (float)(tau * tau * sq * sq / 16.0);
     }
     st->slide_wt = 0;
     if (slide && st->detector == kDetGoertzel)
@@ -952,6 +964,77 @@ int demodulate(demod_t *st, const int16_t *pcm, size_t n_frames, uint8_t *symbol
 // dropped. One H2D copy of each run (the overlapping samples once), one
 // detector launch (at hop = 64 H the segment-shared kernels, as a per-stream
 // handle would run) and one D2H copy serve all streams.
+// Persistent staging threads of one streams handle (the
+// first build spawned and joined up to 7 std::threads inside every push).
+// Workers sleep on a condition variable between pushes; run() hands worker k
+// the stream range [k per, (k + 1) per), does range 0 on the calling thread
+// and waits for the rest. A worker that cannot be started leaves its range
+// to the caller.
+struct StagePool {
+    std::vector<std::thread> th;
+    std::mutex mu;
+    std::condition_variable go, done;
+    const std::function<void(size_t, size_t)> *job = nullptr;
+    size_t per = 0, S = 0, active = 0, pending = 0;
+    unsigned long long gen = 0;
+    bool stop = false;
+
+    ~StagePool()
+    {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            stop = true;
+        }
+        go.notify_all();
+        for (auto &t : th) t.join();
+    }
+    void worker(size_t k)
+    {
+        unsigned long long seen = 0;
+        std::unique_lock<std::mutex> lk(mu);
+        for (;;) {
+            go.wait(lk, [&] { return stop || gen != seen; });
+            if (stop) return;
+            seen = gen;
+            if (k >= active) continue;
+            const size_t a = k * per, e = std::min(S, a + per);
+            const auto *f = job;
+            lk.unlock();
+            if (a < e) (*f)(a, e);
+            lk.lock();
+            if (--pending == 0) done.notify_one();
+        }
+    }
+    // f(a, e) stages streams [a, e); T ranges in all (T - 1 on workers)
+    void run(size_t T, size_t n, const std::function<void(size_t, size_t)> &f)
+    {
+        while (th.size() + 1 < T) {
+            try {
+                const size_t k = th.size() + 1;
+                th.emplace_back([this, k] { worker(k); });
+            } catch (...) {
+                break;
+            }
+        }
+        T = std::min(T, th.size() + 1);
+        const size_t pr = (n + T - 1) / T;
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            job = &f;
+            per = pr;
+            S = n;
+            active = T;
+            pending = T - 1;
+            ++gen;
+        }
+        if (T > 1) go.notify_all();
+        f(0, std::min(n, pr));
+        std::unique_lock<std::mutex> lk(mu);
+        done.wait(lk, [&] { return pending == 0; });
+        job = nullptr;
+    }
+};
+
 struct demod_streams {
     demod_cfg_t cfg;                      // the streams' configuration
     demod_t *st = nullptr;                // detector handle: same n, hop, tones; mono
@@ -961,7 +1044,53 @@ struct demod_streams {
     std::vector<size_t> have;             // per push: carry lengths before it
     std::vector<uint8_t> sym;             // per push: batch symbols / magnitudes
     std::vector<float> mag;
+    StagePool pool;                       // staging threads of large pushes
+    // FSKD_STREAMS_MAPPED=1 (measurement switch, read at create): the push
+    // stages into mapped pinned memory that the detector reads in place over
+    // PCIe and writes its results back to, instead of one H2D copy of the
+    // staging buffer and a D2H copy of the results
+    bool mapped = false;
+    int16_t *zm_in = nullptr, *zmd_in = nullptr;
+    size_t zm_cap = 0;                    // samples
+    uint8_t *zm_sym = nullptr, *zmd_sym = nullptr;
+    float *zm_mag = nullptr, *zmd_mag = nullptr;
+    size_t zm_wcap = 0;                   // windows
+    ~demod_streams()
+    {
+        if (zm_in) (void)hipHostFree(zm_in);
+        if (zm_sym) (void)hipHostFree(zm_sym);
+        if (zm_mag) (void)hipHostFree(zm_mag);
+    }
 };
+
+// Mapped staging of a push (demod_streams::mapped): samples and windows.
+static int ensure_mapped(demod_streams_t *ms, size_t samples, size_t windows)
+{
+    const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent;
+    if (samples > ms->zm_cap) {
+        if (ms->zm_in) (void)hipHostFree(ms->zm_in);
+        ms->zm_in = ms->zmd_in = nullptr;
+        ms->zm_cap = 0;
+        const size_t cap = samples + samples / 4 + 4096;
+        HIP_TRY(hipHostMalloc(&ms->zm_in, cap * sizeof(int16_t), fl));
+        HIP_TRY(hipHostGetDevicePointer((void **)&ms->zmd_in, ms->zm_in, 0));
+        ms->zm_cap = cap;
+    }
+    if (windows > ms->zm_wcap) {
+        if (ms->zm_sym) (void)hipHostFree(ms->zm_sym);
+        if (ms->zm_mag) (void)hipHostFree(ms->zm_mag);
+        ms->zm_sym = ms->zmd_sym = nullptr;
+        ms->zm_mag = ms->zmd_mag = nullptr;
+        ms->zm_wcap = 0;
+        const size_t cap = windows + windows / 4 + 64;
+        HIP_TRY(hipHostMalloc(&ms->zm_sym, cap, fl));
+        HIP_TRY(hipHostMalloc(&ms->zm_mag, cap * ms->cfg.k * sizeof(float), fl));
+        HIP_TRY(hipHostGetDevicePointer((void **)&ms->zmd_sym, ms->zm_sym, 0));
+        HIP_TRY(hipHostGetDevicePointer((void **)&ms->zmd_mag, ms->zm_mag, 0));
+        ms->zm_wcap = cap;
+    }
+    return DEMOD_OK;
+}
 
 extern "C" {
 
@@ -989,6 +1118,8 @@ demod_streams_t *demod_streams_create(const demod_cfg_t *cfg, size_t n_streams, 
         if (error) *error = rc;
         return nullptr;
     }
+    const char *mp = std::getenv("FSKD_STREAMS_MAPPED");
+    ms->mapped = mp && mp[0] == '1';
     try {
         ms->carry.resize(n_streams);
         ms->skip.assign(n_streams, cfg->lead_in);
@@ -1089,9 +1220,15 @@ int demod_streams_push(demod_streams_t *ms, const int16_t *const *pcm, const siz
             ms->first[s] = Wb;
             if (w) Wb += ((w - 1) * hop + n + hop - 1) / hop;  // ceil(L_s / hop)
         }
+        // Wb also counts the straddling windows that are computed and
+        // dropped, up to ~W n / hop: the batch must still fit an int count
+        if (Wb > 0x7FFFFFFF || Wb * hop > ((size_t)1 << 40)) return DEMOD_BAD_ARG;
         const size_t samples = (Wb - 1) * hop + n;  // the last run ends exactly here or earlier
-        int rc = ensure_host(st, std::max(Wb * hop + n, kSmallHostSamples), kSmallHostSamples / 8);
+        int rc = ms->mapped ? ensure_mapped(ms, Wb * hop + n, Wb)
+                            : ensure_host(st, std::max(Wb * hop + n, kSmallHostSamples),
+                                          kSmallHostSamples / 8);
         if (rc != DEMOD_OK) return rc;
+        int16_t *const stage_base = ms->mapped ? ms->zm_in : st->h_in;
         try {
             ms->sym.resize(Wb);
             if (mags) ms->mag.resize(Wb * c.k);
@@ -1103,7 +1240,7 @@ int demod_streams_push(demod_streams_t *ms, const int16_t *const *pcm, const siz
             if (!w) return;
             const size_t L = (w - 1) * hop + n, span = (L + hop - 1) / hop * hop;
             const size_t end = std::min(total, span);  // hv < n <= L <= end
-            int16_t *b = st->h_in + ms->first[s] * hop;
+            int16_t *b = stage_base + ms->first[s] * hop;
             const int16_t *src = pcm[s] + (n_frames[s] - f) * c.channels;
             std::vector<int16_t> &cs = ms->carry[s];
             if (hv) std::memcpy(b, cs.data(), hv * sizeof(int16_t));
@@ -1123,37 +1260,38 @@ int demod_streams_push(demod_streams_t *ms, const int16_t *const *pcm, const siz
         };
         // threads: ~1 per 2 MiB of staged samples, at most kPushThreads (1 per
         // MiB measured no better: 0.47 / 0.75 / 0.54-0.61 ms against 0.49-0.53 /
-        // 0.67 / 0.55-0.59 for mono / stereo / hop 256 at 1024 streams)
+        // 0.67 / 0.55-0.59 for mono / stereo / hop 256 at 1024 streams); the
+        // threads persist in the handle's pool between pushes
         size_t T = std::min<size_t>(kPushThreads, Wb * hop / (1u << 20));
         T = std::min(T, S);
         if (T >= 2) {
-            std::vector<std::thread> pool;
-            const size_t per = (S + T - 1) / T;
-            size_t done_to = S;
-            try {
-                for (size_t k = 1; k < T; ++k) {
-                    const size_t a = k * per, e = std::min(S, a + per);
-                    if (a >= e) break;
-                    pool.emplace_back([&stage, a, e]() {
-                        for (size_t s = a; s < e; ++s) stage(s);
-                    });
-                }
-            } catch (...) {
-                done_to = pool.size() * per + per;  // ranges no thread took: run them here
-            }
-            for (size_t s = 0; s < std::min(per, S); ++s) stage(s);
-            for (size_t s = std::min(done_to, S); s < S; ++s) stage(s);
-            for (auto &th : pool) th.join();
+            const std::function<void(size_t, size_t)> range = [&stage](size_t a, size_t e) {
+                for (size_t s = a; s < e; ++s) stage(s);
+            };
+            ms->pool.run(T, S, range);
         } else {
             for (size_t s = 0; s < S; ++s) stage(s);
         }
-        rc = run_host(st, st->h_in, samples, Wb, ms->sym.data(), mags ? ms->mag.data() : nullptr);
+        if (ms->mapped) {
+            // the detector reads the staged runs in place and writes the
+            // results straight into mapped host memory: one launch (and the
+            // rescue's), one synchronize
+            rc = enqueue_batch(st, ms->zmd_in, Wb, ms->zmd_sym, mags ? ms->zmd_mag : nullptr,
+                               st->stream);
+            if (rc >= 0 && hipStreamSynchronize(st->stream) != hipSuccess) rc = DEMOD_DEVICE_ERROR;
+            if (rc >= 0) {
+                std::memcpy(ms->sym.data(), ms->zm_sym, Wb);
+                if (mags) std::memcpy(ms->mag.data(), ms->zm_mag, Wb * c.k * sizeof(float));
+            }
+        } else {
+            rc = run_host(st, st->h_in, samples, Wb, ms->sym.data(), mags ? ms->mag.data() : nullptr);
+        }
         if (rc < 0) {
             // nothing consumed: the old carries are the runs' first samples
             // (have < n <= L, below the run's gap fill; no other run writes there)
             for (size_t s = 0; s < S; ++s)
                 if (windows(have[s] + fresh(s))) {
-                    const int16_t *b = st->h_in + ms->first[s] * hop;
+                    const int16_t *b = stage_base + ms->first[s] * hop;
                     ms->carry[s].assign(b, b + have[s]);
                 }
             return rc;
@@ -1190,6 +1328,16 @@ int demod_synth_fsk(const demod_cfg_t *cfg, uint64_t seed, uint64_t w0, size_t n
     if (cfg->device < 0 || cfg->device >= kMaxDevices) return DEMOD_BAD_ARG;
     DeviceGuard guard(cfg->device);
     HIP_TRY(guard.err);
+    // the buffers must live on cfg->device (the launch goes there)
+    for (const void *q : {(const void *)d_pcm, (const void *)d_symbols}) {
+        if (!q) continue;
+        hipPointerAttribute_t a;
+        if (hipPointerGetAttributes(&a, q) != hipSuccess) {
+            (void)hipGetLastError();
+            continue;  // not a runtime allocation: left to the caller
+        }
+        if (a.type == hipMemoryTypeDevice && a.device != cfg->device) return DEMOD_BAD_ARG;
+    }
     HIP_TRY(synth_prepare());  // sine table on the current device (once, locked)
     SynthParams p;
     std::memset(&p, 0, sizeof(p));

@@ -715,10 +715,16 @@ constexpr int kFmtWord3 = 0xFAC | (3 << 12) | (5 << 15);
 // (9 ds_read_b128 + 9 dwordx4 stores per lane, 1 KiB per wave instruction);
 // 2 = the same with non-temporal stores (the spectrum is written once);
 // 0 = the quad_slot layout, 33 scattered dword stores per lane.
+// OVL (FUSED 4): round 1 of the transpose overlaps column 0's DFT-16. Column
+// 0's twiddles are read right behind round 0's column reads, round 1's writes
+// and reads follow, and column 0's DFT-16 runs while they are in flight (the
+// waits land on the first use of round 1's data, not before column 0's
+// math); the next group's round-0 writes are ordered behind them.
 template <int WPB = 4, int MINW = 4, int PF = 0, bool SPEC = true, bool FMT = false, int AUX = 2,
-          int FUSED = 0, int RD = 0, int SPL = 0>
+          int FUSED = 0, int RD = 0, int SPL = 0, int OVL = 0>
 __device__ __attribute__((always_inline)) inline void fft1024_quad_body(const FftParams &p)
 {
+    static_assert(!OVL || (FUSED >= 4 && PF == 0), "OVL: the FUSED 4 column DFT-16, loads at the top");
     static_assert(!SPL || SPEC, "SPL: the linear power slab of the spectrum store");
     using namespace quad;
     __shared__ __attribute__((aligned(16))) f2 slab[WPB][kQSlab];
@@ -813,8 +819,72 @@ __device__ __attribute__((always_inline)) inline void fft1024_quad_body(const Ff
         //    k1 = t' (round 0) and k1b (round 1) of its window
         f2 b[32];  // b[n2] = A_n2[t'], b[16 + n2] = A_n2[k1b]
         f2 *win = slab[wave] + q * kQWin;
+        // twp(sl, m): the pair (m, m + 1) of slot sl, m even
+        auto twp = [&](int sl, int m, f2 &lo, f2 &hi) {
+            if constexpr (RD >= 2) {
+                const f4 x = *reinterpret_cast<const f4 *>(&tw2[tw2_at(sl, m, t)]);
+                lo = (f2){x.x, x.y};
+                hi = (f2){x.z, x.w};
+            } else {
+                lo = tw2[tw2_at(sl, m, t)];
+                hi = tw2[tw2_at(sl, m + 1, t)];
+            }
+        };
+        auto twv = [&](int sl, int m) -> f2 { return tw2[tw2_at(sl, m, t)]; };
+        // one column's DFT-16 (FUSED 4) with its ten twiddles given
+        auto col16 = [&](f2 *bb, f2 v, f2 v2, f2 g0, f2 g0s, f2 g1, f2 g1s, f2 g2, f2 g2s, f2 g3,
+                         f2 g3s) {
+            dft4x2_fused_v<4>(bb + 0, bb + 1, v, v2, v, v2);
+            dft4x2_fused_v<4>(bb + 2, bb + 3, v, v2, v, v2);
+            dft4x2_fused_v<1>(bb + 0, bb + 4, g0, g0s, g1, g1s);
+            dft4x2_fused_v<1>(bb + 8, bb + 12, g2, g2s, g3, g3s);
+            f2 tt[16];
+            static_for<0, 16>([&](auto e) {
+                constexpr int m = decltype(e)::value;  // m = 4 k1 + k2 holds Z[col + 32 (k1 + 4 k2)]
+                tt[(m / 4) + 4 * (m % 4)] = bb[m];
+            });
+            static_for<0, 16>([&](auto e) {
+                constexpr int m = decltype(e)::value;
+                bb[m] = tt[m];
+            });
+        };
+        if constexpr (OVL) {
+            // the previous group's round-1 reads stay ahead of these writes
+            // (LDS executes one wave's operations in order)
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            __builtin_amdgcn_wave_barrier();
 #pragma unroll
-        for (int r = 0; r < 2; ++r) {
+            for (int c = 0; c < 16; ++c) win[t * kQRow + c] = a[c];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+            for (int n2 = 0; n2 < 16; ++n2) b[n2] = win[n2 * kQRow + t];
+            f2 v, v2, g0, g0s, g1, g1s, g2, g2s, g3, g3s;
+            twp(0, 0, v, v2);
+            twp(0, 2, g0, g0s);
+            twp(0, 4, g1, g1s);
+            twp(0, 6, g2, g2s);
+            twp(0, 8, g3, g3s);
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll
+            for (int c = 0; c < 16; ++c) win[t * kQRow + c] = a[16 + c];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+            for (int n2 = 0; n2 < 16; ++n2) b[16 + n2] = win[n2 * kQRow + k1b - 16];
+            col16(b, v, v2, g0, g0s, g1, g1s, g2, g2s, g3, g3s);
+            twp(1, 0, v, v2);
+            twp(1, 2, g0, g0s);
+            twp(1, 4, g1, g1s);
+            twp(1, 6, g2, g2s);
+            twp(1, 8, g3, g3s);
+            col16(b + 16, v, v2, g0, g0s, g1, g1s, g2, g2s, g3, g3s);
+        }
+#pragma unroll
+        for (int r = 0; r < (OVL ? 0 : 2); ++r) {
 #pragma unroll
             for (int c = 0; c < 16; ++c) win[t * kQRow + c] = a[16 * r + c];
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -828,20 +898,8 @@ __device__ __attribute__((always_inline)) inline void fft1024_quad_body(const Ff
             __builtin_amdgcn_wave_barrier();
         }
         // 3. per column: DFT-16 over t of A_t[col] W512^{t col}, twiddles fused
-        // twp(sl, m): the pair (m, m + 1) of slot sl, m even
-        auto twp = [&](int sl, int m, f2 &lo, f2 &hi) {
-            if constexpr (RD >= 2) {
-                const f4 x = *reinterpret_cast<const f4 *>(&tw2[tw2_at(sl, m, t)]);
-                lo = (f2){x.x, x.y};
-                hi = (f2){x.z, x.w};
-            } else {
-                lo = tw2[tw2_at(sl, m, t)];
-                hi = tw2[tw2_at(sl, m + 1, t)];
-            }
-        };
-        auto twv = [&](int sl, int m) -> f2 { return tw2[tw2_at(sl, m, t)]; };
 #pragma unroll
-        for (int sl = 0; sl < 2; ++sl) {
+        for (int sl = 0; sl < (OVL ? 0 : 2); ++sl) {
             f2 *bb = b + 16 * sl;
             f2 v, v2;
             twp(sl, 0, v, v2);
@@ -1044,11 +1102,11 @@ __device__ __attribute__((always_inline)) inline void fft1024_quad_body(const Ff
 }
 
 template <int WPB = 4, int MINW = 4, int PF = 0, bool SPEC = true, bool FMT = false, int AUX = 2,
-          int FUSED = 0, int SPL = 0>
+          int FUSED = 0, int SPL = 0, int OVL = 0>
 __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MINW > 0 ? MINW : 1)))
 void fft1024_quad_kernel(FftParams p)
 {
-    fft1024_quad_body<WPB, MINW, PF, SPEC, FMT, AUX, FUSED, 0, SPL>(p);
+    fft1024_quad_body<WPB, MINW, PF, SPEC, FMT, AUX, FUSED, 0, SPL, OVL>(p);
 }
 
 // (a device-code attribute: the host pass of hipcc does not know the feature)
@@ -1073,15 +1131,15 @@ FSKD_NO_LDS_PAIRING void fft1024_quad_kernel_r64(FftParams p)
 // Persistent grid: as many blocks as fit the chip, each wave strides over
 // groups of 4 windows (the LDS twiddle tables are built once per block).
 template <int WPB, int MINW, int PF, bool SPEC, bool FMT = false, int AUX = 2, int FUSED = 0, int RD = 0,
-          int SPL = 0>
+          int SPL = 0, int OVL = 0>
 hipError_t launch_fft_quad_t(const FftParams &p, hipStream_t s)
 {
     void (*kern)(FftParams);
-    static_assert(!(RD > 0 && SPL > 0), "SPL: fft1024_quad_kernel only");
+    static_assert(!(RD > 0 && (SPL > 0 || OVL > 0)), "SPL / OVL: fft1024_quad_kernel only");
     if constexpr (RD > 0)
         kern = fft1024_quad_kernel_r64<WPB, MINW, PF, SPEC, FMT, AUX, FUSED, RD>;
     else
-        kern = fft1024_quad_kernel<WPB, MINW, PF, SPEC, FMT, AUX, FUSED, SPL>;
+        kern = fft1024_quad_kernel<WPB, MINW, PF, SPEC, FMT, AUX, FUSED, SPL, OVL>;
     int dev = 0, cus = 256, per_cu = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);

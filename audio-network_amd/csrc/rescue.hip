@@ -19,8 +19,8 @@
 // rescued powers are written (rounded to fp32) over the window's magnitudes
 // and, for the FFT, its whole spectrum.
 //
-// Layout: one wave per 4096 consecutive windows. It first reads their symbol
-// bytes (16 dword loads per lane, all in flight at once) and exits if none is
+// Layout: one wave per 4096 consecutive windows (FFT: 1024). It first reads
+// their symbol bytes (dword loads, all in flight at once) and exits if none is
 // flagged — the common case: one short pass over 1 byte per window. Otherwise
 // it compacts the flagged windows, in order, into an LDS list. Goertzel:
 // groups of up to 64 / K flagged windows are staged whole into LDS (stride
@@ -33,8 +33,11 @@
 
 namespace fskd {
 
-constexpr int kRescueChunk = 4096;        // windows whose symbols one wave scans
-constexpr int kRescueLdsBytes = 32768;    // Goertzel: staged samples per group
+// windows whose symbols one wave scans: Goertzel 4096; FFT 1024 (each
+// flagged window is a whole FFT for the wave, so more waves share them)
+constexpr int kRescueChunkG = 4096;
+constexpr int kRescueChunkF = 1024;
+constexpr int kRescueLdsBytes = 32768;    // Goertzel: staged samples per group (FFT: 16 KiB)
 
 typedef unsigned int u32x4q __attribute__((ext_vector_type(4)));
 
@@ -47,8 +50,9 @@ template <bool FFT>
 __global__ __launch_bounds__(64) void rescue_kernel(RescueParams p)
 {
 #pragma clang fp contract(off)
+    constexpr int kRescueChunk = FFT ? kRescueChunkF : kRescueChunkG;
     __shared__ unsigned short idx[kRescueChunk];
-    __shared__ __attribute__((aligned(16))) unsigned char smp[kRescueLdsBytes];
+    __shared__ __attribute__((aligned(16))) unsigned char smp[FFT ? 16384 : kRescueLdsBytes];
     __shared__ double pd[64];
     const int lane = threadIdx.x;
     const long long base = (long long)blockIdx.x * kRescueChunk;
@@ -203,7 +207,8 @@ hipError_t launch_rescue(const RescueParams &p, hipStream_t s)
     if (p.k < 2 || p.k > kMaxTones) return hipErrorInvalidValue;
     if (p.fft ? (p.n != 1024 || !p.tw) : (p.n < 64 || (p.n % 8) || 2 * p.n + 16 > kRescueLdsBytes))
         return hipErrorInvalidValue;
-    const long long blocks = (p.n_windows + kRescueChunk - 1) / kRescueChunk;
+    const int chunk = p.fft ? kRescueChunkF : kRescueChunkG;
+    const long long blocks = (p.n_windows + chunk - 1) / chunk;
     if (blocks > 0x7FFFFFFFLL) return hipErrorInvalidValue;
     if (p.fft)
         hipLaunchKernelGGL(rescue_kernel<true>, dim3((unsigned)blocks), dim3(64), 0, s, p);

@@ -2,19 +2,22 @@
 """bench.py — Goertzel FSK demodulation throughput on MI355X.
 
 Contract (driver): `python bench.py --gpus N --steps K --warmup W`; for N > 1
-launched by torch.distributed.run, one rank per GPU. Rank 0 prints ONE JSON
-line.
+launched by torch.distributed.run, one rank per GPU. Called with --gpus N > 1
+and no WORLD_SIZE in the environment, bench.py starts torch.distributed.run
+itself (as a child process, before any GPU call) and relays its output; a
+WORLD_SIZE different from --gpus is an error. Rank 0 prints ONE JSON line.
 
-Workload (BASELINE.json configs[1]): 2-FSK Goertzel on 2^20 windows x 1024
-int16 samples (2 GiB) per GPU, resident in HBM before timing. One step = one
-demod_batch_async launch over the whole batch (symbols + |X_k|^2 written to
-HBM) and, for N > 1, the RCCL all-gather of every rank's decoded symbols
-(the only collective of the path). Weak scaling: every rank
-demodulates its own 2^20 windows (disjoint slices of one seeded stream).
+Headline workload (BASELINE.json configs[1]): 2-FSK Goertzel on 2^20 windows
+x 1024 int16 samples (2 GiB) per GPU, resident in HBM before timing. One step
+= one demod_batch_async over the whole batch (the detector launch(es), symbols
++ |X_k|^2 written to HBM, and the decision rescue's launch)
+and, for N > 1, the RCCL all-gather of every rank's decoded symbols (the only
+collective of the path). Weak scaling: every rank demodulates
+its own 2^20 windows (disjoint slices of one seeded stream).
 
 value = samples demodulated by all ranks / wall time per step (Msamples/s).
 roofline = algorithmic bytes per launch (2048 B in + 1 B symbol + 4K B
-magnitudes per window) / mean kernel duration from HIP events
+magnitudes per window) / mean batch duration from HIP events
 recorded on the launch stream, vs the 8 TB/s HBM peak. traffic = HBM bytes per
 launch from the committed rocprofv3 PMC summary (profiles/), or null.
 cpu_baseline = the oracle's C restatement (OpenMP over the host cores this
@@ -22,11 +25,20 @@ process may use) on a bounded sample of the same windows (rank 0, N = 1 only),
 median of >= 5 timed repetitions; its output doubles as a parity check of the
 timed GPU output on that sample (parity_sample, with the top-2 decision-margin
 histogram SURVEY §7 asks for, at sigma 400 and at the sigma 2000 stress level).
+rescue = the same step with the decision rescue switched off
+(FSKD_NO_RESCUE=1), i.e. the rescue's cost.
 
-At N = 1 the default run also measures configs[2] (8-FSK) and configs[3]
-(sliding FFT, hop 256) with the same steps/warmup and reports them under
-"fsk8" and "fft_hop256", plus configs[3] with the full 513-bin spectrum
-stored as "fft_hop256_spectrum" (no CPU baseline for those).
+Extra entries of the default run:
+  * N = 1: configs[2] (8-FSK) "fsk8"; configs[3] (sliding FFT, hop 256)
+    "fft_hop256" with an oracle parity sample of 16384 consecutive windows, and
+    with the full 513-bin spectrum stored, "fft_hop256_spectrum"; configs[4]
+    "streams" (1024 streams, RCCL at world size 1, one HIP graph per step; a
+    child `bench.py --config streams --force-dist`); "host_e2e", the
+    PCIe-inclusive rate of a 2 GiB host-buffer demod_batch against the raw
+    host-to-device copy rate;
+  * N > 1: configs[4] "streams" sharded over the N ranks (strong scaling,
+    graph step, RCCL frame gather), with scaling_vs_n1 against the same
+    workload on rank 0's GPU alone in the same job.
 
 Defaults: 200 timed steps after 20 warmup steps (the warmup is at least 64
 launches, MIN_WARMUP), so each config keeps the GPU busy for 0.1-0.5 s
@@ -38,6 +50,7 @@ import json
 import math
 import os
 import socket
+import subprocess
 import sys
 import time
 
@@ -220,7 +233,8 @@ def free_port() -> int:
 
 
 def run_config(A, D, torch, dist, args, config, rank, world, local, use_dist, steps, warmup,
-               plan="survey", method_name="auto", hop_fft=256, no_mags=False, spectrum=False):
+               plan="survey", method_name="auto", hop_fft=256, no_mags=False, spectrum=False,
+               rescue_ab=False, parity_windows=0, n_streams_total=1024):
     """Allocate, synthesise, warm up and time one workload; returns a dict."""
     freqs = A.FSK8_FREQS if config == "fsk8" else A.FSK2_FREQS
     if config == "fsk8" and plan == "odd":
@@ -235,7 +249,7 @@ def run_config(A, D, torch, dist, args, config, rank, world, local, use_dist, st
     if config == "streams":
         # config 5: 1024 independent streams x 2^21 samples (2048 windows each);
         # rank r demodulates the contiguous stream shard D.shard_range(1024, r, N)
-        n_streams, wps = 1024, 2048
+        n_streams, wps = n_streams_total, 2048
         s_first, s_count = D.shard_range(n_streams, rank, world)
         W, w0, total_windows = s_count * wps, s_first * wps, n_streams * wps
     else:
@@ -409,23 +423,6 @@ def run_config(A, D, torch, dist, args, config, rank, world, local, use_dist, st
         all_sym = graphs[steps % 2][1]          # frames of the slot the last replay gathered
         st["i"] = steps + 1                     # the slot holding the last demodulated symbols
 
-    # Practical read ceiling of this box for the same access pattern: the
-    # read-only reference stream (8 KiB per wave, 16 B/lane nt loads, no
-    # compute; demod_read_ceiling_async) over the same input buffer, after the
-    # timed region, median of 20 launches (HIP events on the launch stream).
-    ceil_gbps = None
-    if config != "fft":
-        nb = (d_pcm.numel() * 2) // 8192 * 8192
-        cev = [mk(2) for _ in range(20)]
-        for _ in range(8):
-            A.read_ceiling_async(d_pcm, nb, stream=comp.cuda_stream)
-        for a, b in cev:
-            a.record(comp)
-            A.read_ceiling_async(d_pcm, nb, stream=comp.cuda_stream)
-            b.record(comp)
-        torch.cuda.synchronize()
-        ceil_gbps = nb / (float(np.median([a.elapsed_time(b) for a, b in cev])) / 1e3) / 1e9
-
     # correctness of the timed output: every symbol vs the transmitted one
     # (sliding windows straddle two symbols: compare the aligned ones only)
     d_sym = slots[(st["i"] - 1) % len(slots)]
@@ -487,14 +484,11 @@ def run_config(A, D, torch, dist, args, config, rank, world, local, use_dist, st
             "frac": round(achieved / HBM_PEAK_GBPS, 4),
             "traffic": pmc_traffic(pmc_name, W, hop),
             "alg_bytes_per_launch": alg_bytes,
-            # this box's read-only ceiling for the same access pattern
-            # (see above) and the kernel's achieved rate as a fraction of it
-            "read_ceiling": round(ceil_gbps, 1) if ceil_gbps else None,
-            "frac_of_read_ceiling": round(achieved / ceil_gbps, 4) if ceil_gbps else None,
             "kernel": kname,
             "launches_per_step": launches,
+            "timed": "the whole batch: detector launch(es) + the rescue launch (HIP events)",
         },
-        "d_pcm": d_pcm, "d_sym": d_sym, "d_mag": d_mag, "cfg": cfg,
+        "d_pcm": d_pcm, "d_sym": d_sym, "d_mag": d_mag, "d_true": d_true, "cfg": cfg,
         "spectrum": d_spec is not None,
     }
     if dev_framing or use_dist:
@@ -517,8 +511,82 @@ def run_config(A, D, torch, dist, args, config, rank, world, local, use_dist, st
                               "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
                               "frac": round(tf / VALU_PEAK_TFLOPS, 4),
                               "flop_per_window": fpw}
+    if rescue_ab and not use_dist:
+        # the same step with the decision rescue switched off: its cost
+        os.environ["FSKD_NO_RESCUE"] = "1"
+        try:
+            d0 = A.Demodulator(cfg)
+        finally:
+            del os.environ["FSKD_NO_RESCUE"]
+        sl = torch.empty_like(d_sym)
+
+        def step0():
+            if d_spec is not None:
+                d0.batch_spectrum_async(d_pcm, n_eval, sl, d_mag, d_spec, stream=comp.cuda_stream)
+            else:
+                d0.batch_async(d_pcm, n_eval, sl, d_mag, stream=comp.cuda_stream)
+        t_on, t_off = [], []
+        for _ in range(3):   # interleaved: this box's drift hits both alike
+            t_off.append(time_steps(torch, step0, steps, warm))
+            t_on.append(time_steps(torch, lambda: step(), steps, warm))
+        on, off = float(np.median(t_on)), float(np.median(t_off))
+        r["rescue"] = {"ms_per_step": round(on, 4), "ms_per_step_without_rescue": round(off, 4),
+                       "cost_frac": round((on - off) / off, 4),
+                       "launches_without": d0.batch_launches(n_eval, not no_mags),
+                       "how": "interleaved medians of 3 x %d steps each way" % steps}
+        d0.close()
+        del sl
+    if parity_windows and rank == 0:
+        r["parity_sample"] = parity_consecutive(A, d_pcm, slots[(st["i"] - 1) % len(slots)], d_mag,
+                                                freqs, n, hop, parity_windows, config == "fft")
     demod.close()
     return r
+
+
+def time_steps(torch, fn, steps, warm) -> float:
+    """ms per step of `fn` over `steps` launches after `warm` (synchronised)."""
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / steps * 1e3
+
+
+def parity_consecutive(A, d_pcm, d_sym, d_mag, freqs, n, hop, count, fft):
+    """GPU vs the oracle on the first `count` consecutive windows of the timed
+    output (at hop < n these include every window straddling two symbols):
+    symbol mismatches, windows whose oracle top-2 margin is inside the fp32
+    band (decided by the rescue), magnitude error relative to max_k P and the
+    count of windows above 1e-5 of max_k P."""
+    sys.path.insert(0, ROOT)
+    from oracle import oracle as O
+    W = min(count, d_sym.numel())
+    flat = d_pcm.reshape(-1)[:(W - 1) * hop + n].cpu().numpy()
+    _, _, _, threads, _ = cpu_share()
+    if fft:
+        sym, P = O.fft_demod(flat, freqs, n, hop, threads=threads)
+    else:
+        sym, P = O.goertzel(flat, freqs, n, hop, threads=threads)
+    gs = d_sym[:W].cpu().numpy()
+    out = {"windows_checked": int(W), "consecutive": True, "hop": hop,
+           "oracle": "oracle_fft_demod (double radix-2)" if fft else "oracle_goertzel (double)",
+           "symbol_mismatches": int((gs != sym).sum()),
+           "flag_bits_left": int((gs & 0x80).sum()),
+           "margin": margin_stats(P)}
+    if d_mag is not None:
+        gm = d_mag[:W].cpu().numpy().astype(np.float64)
+        rel = np.abs(gm - P).max(1) / np.maximum(P.max(1), 1e-300)
+        out["max_rel_mag_err"] = float(rel.max())
+        out["windows_above_1e-5_of_max_P"] = int((rel > 1e-5).sum())
+        x = flat.astype(np.float64)
+        c2 = np.concatenate([[0.0], np.cumsum(x * x)])
+        st_ = np.arange(W) * hop
+        energy = n * (c2[st_ + n] - c2[st_]) / 2
+        out["max_mag_err_of_energy"] = float((np.abs(gm - P).max(1) / np.maximum(energy, 1e-300)).max())
+    return out
 
 
 def summary(r) -> dict:
@@ -533,6 +601,9 @@ def summary(r) -> dict:
            "value": round(r["W"] * 1024 / (r["ms_per_step"] / 1e3) / 1e6, 1), "unit": "Msamples/s",
            "symbol_errors": r["sym_err"],
            "launches_per_step": r["roofline"]["launches_per_step"]}
+    for key in ("rescue", "parity_sample"):
+        if key in r:
+            out[key] = r[key]
     if r["config"] == "fft":
         out["roofline"] = r["roofline_valu"]
         # HBM: the unique input stream plus the outputs (with the spectrum:
@@ -544,6 +615,85 @@ def summary(r) -> dict:
     else:
         out["roofline"] = r["roofline"]
     return out
+
+
+def streams_child(args) -> dict:
+    """configs[4] at N = 1 as the 8-GPU run's step takes it: a child
+    `bench.py --config streams --force-dist` (RCCL at world size 1, one HIP
+    graph per step), its line reduced to the entry of this one."""
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT", "MASTER_ADDR"):
+        env.pop(k, None)
+    cmd = [sys.executable, "-u", os.path.abspath(__file__), "--config", "streams", "--force-dist",
+           "--steps", str(args.steps), "--warmup", str(args.warmup), "--no-cpu-baseline"]
+    r = subprocess.run(cmd, capture_output=True, timeout=600, cwd=ROOT, env=env)
+    lines = [ln for ln in r.stdout.decode().splitlines() if ln.startswith("{")]
+    if r.returncode != 0 or not lines:
+        return {"error": f"rc {r.returncode}", "stderr_tail": r.stderr.decode()[-800:]}
+    ln = json.loads(lines[-1])
+    keep = ("value", "unit", "ms_per_step", "kernel_ms", "kernel_ms_p10_p50_p90", "symbol_errors",
+            "overhead", "framing", "roofline", "rescue", "scaling", "n_gpus")
+    out = {k: ln[k] for k in keep if k in ln}
+    out["workload"] = ln["config"]["workload"]
+    out["how"] = "child: bench.py --config streams --force-dist (nccl, world size 1, graph step)"
+    return out
+
+
+def host_e2e(A, torch, r, reps=5) -> dict:
+    """The PCIe-inclusive path (never the headline value): the headline's 2 GiB
+    of windows from a pageable host array through demod_batch (chunked H2D on a
+    copy stream, kernels behind each chunk, results back), against the raw
+    host-to-device copy rate of the same bytes (pageable and pinned)."""
+    x = r["d_pcm"].cpu().numpy()
+    W, nbytes = x.shape[0], x.nbytes
+    with A.Demodulator(r["cfg"]) as d:
+        sym, mag = d.batch(x, mags=True)                 # warm: allocations, first copies
+        t = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            sym, mag = d.batch(x, mags=True)
+            t.append(time.perf_counter() - t0)
+    tb = float(np.median(t))
+    src = torch.from_numpy(x)
+    pin = src.pin_memory()
+    dst = torch.empty_like(r["d_pcm"])
+    rates = {}
+    for name, h in (("pageable", src), ("pinned", pin)):
+        dst.copy_(h)
+        torch.cuda.synchronize()
+        tt = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            dst.copy_(h)
+            torch.cuda.synchronize()
+            tt.append(time.perf_counter() - t0)
+        rates[name] = nbytes / float(np.median(tt)) / 1e9
+    true_sym = r["d_true"].cpu().numpy() if "d_true" in r else None
+    gbps = nbytes / tb / 1e9
+    out = {"workload": f"configs[1] windows from a pageable host buffer ({nbytes} B), demod_batch "
+                       "host pointers: symbols + |X_k|^2 back in host memory",
+           "ms_per_batch": round(tb * 1e3, 3), "GB_per_s": round(gbps, 2),
+           "Msamples_per_s": round(W * 1024 / tb / 1e6, 1),
+           "h2d_GB_per_s": {k: round(v, 2) for k, v in rates.items()},
+           "frac_of_pageable_h2d": round(gbps / rates["pageable"], 4),
+           "symbols_equal_device_path": bool((sym == r["d_sym"].cpu().numpy()).all()),
+           "reps": reps}
+    if true_sym is not None:
+        out["symbol_errors"] = int((sym != true_sym).sum())
+    del pin, dst
+    return out
+
+
+def self_launch(args) -> int:
+    """--gpus N > 1 without WORLD_SIZE: run N ranks under torch.distributed.run
+    (a child process started before this one touches the GPU); rank 0's line
+    is printed by the child."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1",
+           f"--master-port={free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.call(cmd, env=env)
 
 
 def main():
@@ -570,7 +720,8 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true",
-                    help="skip the configs[2] / configs[3] entries of the default N = 1 run")
+                    help="skip the extra entries (fsk8, fft_hop256*, streams, host_e2e at N = 1; "
+                         "streams at N > 1)")
     ap.add_argument("--force-dist", action="store_true",
                     help="initialise torch.distributed and run the gather even at N = 1 "
                          "(exercises the RCCL path on one GPU)")
@@ -581,7 +732,13 @@ def main():
                          "multi-rank path with several ranks sharing one GPU")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(self_launch(args))
+    world = int(env_world or "1")
+    if world != args.gpus and not (world == 1 and args.gpus == 1):
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
@@ -602,24 +759,59 @@ def main():
             dist.init_process_group("gloo", **init)
 
     A, D = load_pkg()
+    plain = world == 1 and not args.force_dist and args.method == "auto" and not args.no_mags
     r = run_config(A, D, torch, dist, args, args.config, rank, world, local, use_dist,
                    args.steps, args.warmup, plan=args.plan, method_name=args.method,
-                   hop_fft=args.hop, no_mags=args.no_mags, spectrum=args.spectrum)
+                   hop_fft=args.hop, no_mags=args.no_mags, spectrum=args.spectrum,
+                   rescue_ab=plain and args.config in ("fsk2", "fsk8", "fft"))
 
     extras = {}
-    if (world == 1 and args.config == "fsk2" and not args.no_extras and not args.force_dist
-            and args.method == "auto" and not args.no_mags):
+    if plain and args.config == "fsk2" and not args.no_extras:
         # configs[2] and configs[3], same steps / warmup, in their own buffers
         # (the main run's stay alive for the CPU baseline's parity sample)
-        main_keep = {k: r[k] for k in ("d_pcm", "d_sym", "d_mag")}
+        main_keep = {k: r[k] for k in ("d_pcm", "d_sym", "d_mag", "d_true")}
         for key, cfgname, spec in (("fsk8", "fsk8", False), ("fft_hop256", "fft", False),
                                    ("fft_hop256_spectrum", "fft", True)):
             rr = run_config(A, D, torch, dist, args, cfgname, rank, world, local, False,
-                            args.steps, args.warmup, hop_fft=256, spectrum=spec)
+                            args.steps, args.warmup, hop_fft=256, spectrum=spec,
+                            rescue_ab=not spec,
+                            parity_windows=16384 if (cfgname == "fft" and not spec) else 0)
             extras[key] = summary(rr)
             del rr
             torch.cuda.empty_cache()
         r.update(main_keep)
+        extras["host_e2e"] = host_e2e(A, torch, r)
+        torch.cuda.empty_cache()
+        extras["streams"] = streams_child(args)
+    elif world > 1 and args.config == "fsk2" and not args.no_extras:
+        # configs[4] over the N ranks (strong scaling), and the same workload on
+        # rank 0's GPU alone for scaling_vs_n1 (the other ranks wait)
+        for k in ("d_pcm", "d_sym", "d_mag", "d_true"):
+            r.pop(k, None)
+        torch.cuda.empty_cache()
+        args.graph = args.dist_backend == "nccl"
+        rs = run_config(A, D, torch, dist, args, "streams", rank, world, local, True,
+                        args.steps, args.warmup)
+        ent = {"workload": f"configs[4]: 1024 streams x 2048 windows sharded over {world} GPUs",
+               "scaling": "strong", "value": round(rs["total_windows"] * 1024 /
+                                                   (rs["ms_per_step"] / 1e3) / 1e6, 1),
+               "unit": "Msamples/s", "ms_per_step": round(rs["ms_per_step"], 4),
+               "kernel_ms": round(rs["kernel_ms"], 4), "symbol_errors": rs["sym_err"],
+               "framing": rs["framed"], "overhead": rs.get("overhead")}
+        del rs
+        torch.cuda.empty_cache()
+        dist.barrier()
+        if rank == 0:
+            r1 = run_config(A, D, torch, None, args, "streams", 0, 1, local, False,
+                            args.steps, args.warmup)
+            ent["n1_ms_per_step"] = round(r1["ms_per_step"], 4)
+            ent["n1_how"] = ("the same 1024 streams on rank 0's GPU alone in this job (eager: "
+                             "detector + framing, no gather)")
+            ent["scaling_vs_n1"] = round(r1["ms_per_step"] / ent["ms_per_step"], 3)
+            del r1
+            torch.cuda.empty_cache()
+        dist.barrier()
+        extras["streams"] = ent
 
     if rank == 0:
         samples = r["total_windows"] * r["n"]  # stream samples demodulated (each counted once)
@@ -673,6 +865,8 @@ def main():
             out["roofline_valu"] = r["roofline_valu"]
         if "overhead" in r:
             out["overhead"] = r["overhead"]
+        if "rescue" in r:
+            out["rescue"] = r["rescue"]
         if r["framed"]:
             out["framing"] = r["framed"]
         out.update(extras)
@@ -692,6 +886,7 @@ def main():
                           "sigma2000": stress_parity(A, O, r["cfg"], r["freqs"], 2000, 65536,
                                                      r["d_pcm"].device, torch, threads)}
             out["parity_sample"] = parity
+        out["extra_keys"] = sorted(extras)
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()

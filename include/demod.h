@@ -22,6 +22,16 @@
  * Threading: re-entrant across handles, not within one handle (one handle
  * serves one consumer, like the single playback task, playback.cpp:157-165).
  *
+ * Decisions: every symbol is the argmax of the tone powers as the double-
+ * precision definition computes them (ties to the lowest tone). The kernels
+ * decide in fp32; a window whose fp32 top-2 margin lies within the powers'
+ * error bound leaves its detector flagged, and a second launch on the same
+ * stream (the decision rescue) decides it again in double with
+ * the definition's own arithmetic and rewrites its symbol and powers. A batch
+ * is complete when its stream has passed that second launch; there is no
+ * state shared between batches, so batches of one handle may run on
+ * different streams.
+ *
  * Every compute entry point runs on the GPU (HIP, gfx950). There is no CPU
  * fallback: without a visible MI355X, demod_create() fails with
  * DEMOD_NO_DEVICE. The framing / packing helpers are pure host byte work.
@@ -131,11 +141,14 @@ int demod_pending(const demod_t *st);
 /* Upper bound on symbols the next demodulate(st, ., n_frames, ...) emits. */
 int demod_max_symbols(const demod_t *st, size_t n_frames);
 
-/* Kernel launches one demod_batch / demod_batch_async of n_windows makes
- * (with_mags: magnitudes requested). Goertzel-family batches whose symbol +
- * magnitude output exceeds ~10 MiB run as equal slices, so each launch's
- * output is written back from L2 in a burst instead of interleaved with the
- * input stream; profilers see that many dispatches. */
+/* Kernel launches one device-pointer demod_batch / demod_batch_async of
+ * n_windows makes (with_mags: magnitudes requested): the detector's, plus one
+ * for the decision rescue (K >= 2). Goertzel-family batches whose symbol +
+ * magnitude output exceeds ~10 MiB run as equal detector slices, so each
+ * launch's output is written back from L2 in a burst instead of interleaved
+ * with the input stream; profilers see that many
+ * dispatches. A host-pointer demod_batch over 4 MiB of samples runs in
+ * chunks of 65 536 windows, each chunk counted as a batch of its own. */
 int demod_batch_launches(const demod_t *st, size_t n_windows, int with_mags);
 
 /*
@@ -361,16 +374,19 @@ int demod_to_transmitter_decode(const uint8_t *in, size_t len, demod_receiver_in
  * input): windows w0 .. w0+W-1 of the stream, cfg->n mono samples each,
  * contiguous, symbols uniform
  * over cfg->k, amplitude `amplitude`, Irwin–Hall noise of std `sigma`.
- * d_pcm / d_symbols are device pointers; enqueued on `stream`. */
+ * d_pcm / d_symbols are device pointers on device cfg->device (checked:
+ * DEMOD_BAD_ARG for memory of another device); enqueued on `stream`. The
+ * sine table is uploaded to each device once per process: a
+ * hipDeviceReset() while the library is loaded is not supported. */
 int demod_synth_fsk(const demod_cfg_t *cfg, uint64_t seed, uint64_t w0,
                     size_t n_windows, int amplitude, int sigma, int16_t *d_pcm,
                     uint8_t *d_symbols, void *stream);
 
-/* Read-only reference stream (benchmarks): reads n_bytes (a multiple of
- * 8192, 16-byte aligned) of device memory with the detector kernels' access
+/* Read-only reference stream (probes): reads n_bytes (a multiple of 8192,
+ * 16-byte aligned) of device memory with the detector kernels' access
  * pattern (8 KiB per wave, coalesced 16 B/lane non-temporal loads) and
- * discards it, enqueued on `stream`. Its bandwidth is the practical HBM read
- * ceiling the detectors are reported against. */
+ * discards it, enqueued on `stream`. A reference point for probes, not a
+ * ceiling: the detector kernels measure slightly above it. */
 int demod_read_ceiling_async(const void *d_buf, size_t n_bytes, void *stream);
 
 /* ---- misc -------------------------------------------------------------- */

@@ -103,6 +103,21 @@ int main(int argc, char **argv)
     vs.push_back({"pfx: fused4 PF1 MINW4", [](const FftParams &p, hipStream_t s) { return p.spec ? launch_fft_quad_t<4, 4, 1, true, false, 0, 4>(p, s) : launch_fft_quad_t<4, 4, 1, false, false, 0, 4>(p, s); }, {}});
     vs.push_back({"pfx: fused4 PF0 MINW3", [](const FftParams &p, hipStream_t s) { return p.spec ? launch_fft_quad_t<4, 3, 0, true, false, 0, 4>(p, s) : launch_fft_quad_t<4, 3, 0, false, false, 0, 4>(p, s); }, {}});
     vs.push_back({"pfx: shipped", [](const FftParams &p, hipStream_t s) { return launch_fft_quad(p, s); }, {}});
+    // round 3: round 1 of the transpose overlapped with column 0's DFT-16 (OVL)
+    vs.push_back({"ovl: shipped", [](const FftParams &p, hipStream_t s) { return launch_fft_quad(p, s); }, {}});
+    vs.push_back({"ovl: OVL1", [](const FftParams &p, hipStream_t s) {
+        const bool lin = p.spec && ((uintptr_t)p.spec & 15) == 0;
+        if (p.hop < 1024)
+            return lin ? launch_fft_quad_t<4, 4, 0, true, false, 0, 4, 0, 2, 1>(p, s)
+                 : p.spec ? launch_fft_quad_t<4, 4, 0, true, false, 0, 4, 0, 0, 1>(p, s)
+                          : launch_fft_quad_t<4, 4, 0, false, false, 0, 4, 0, 0, 1>(p, s);
+        return lin ? launch_fft_quad_t<4, 4, 0, true, false, 2, 4, 0, 2, 1>(p, s)
+             : p.spec ? launch_fft_quad_t<4, 4, 0, true, false, 2, 4, 0, 0, 1>(p, s)
+                      : launch_fft_quad_t<4, 4, 0, false, false, 2, 4, 0, 0, 1>(p, s); }, {}});
+    vs.push_back({"ovl: OVL1 FMT", [](const FftParams &p, hipStream_t s) {
+        if (p.spec) return launch_fft_quad(p, s);  // tone-only variant
+        return p.hop < 1024 ? launch_fft_quad_t<4, 4, 0, false, true, 0, 4, 0, 0, 1>(p, s)
+                            : launch_fft_quad_t<4, 4, 0, false, true, 2, 4, 0, 0, 1>(p, s); }, {}});
     if (filter) {
         std::vector<Var> keep;
         for (size_t i = 0; i < vs.size(); ++i)

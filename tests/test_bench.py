@@ -95,3 +95,26 @@ def test_decision_checker_rejects_wrong_decisions():
     bad = mag[:, ::-1].copy()
     with pytest.raises(AssertionError):                        # differs from the oracle
         check_decisions(bad.argmax(axis=1), bad, ref_sym, ref_P)
+
+
+def test_world_size_must_match_gpus():
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4"],
+                       capture_output=True, timeout=120, cwd=ROOT, env=env)
+    assert r.returncode == 2 and b"WORLD_SIZE=2" in r.stderr
+
+
+def test_gpus_n_self_launches_torchrun(monkeypatch):
+    """--gpus N > 1 without WORLD_SIZE starts torch.distributed.run as a child
+    (before any GPU call) with N ranks on 127.0.0.1 and the same arguments."""
+    calls = []
+    monkeypatch.setattr(bench.subprocess, "call", lambda cmd, env=None: calls.append(cmd) or 0)
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "2", "--steps", "3"])
+    with pytest.raises(SystemExit) as e:
+        bench.main()
+    assert e.value.code == 0 and len(calls) == 1
+    cmd = calls[0]
+    assert cmd[1:3] == ["-m", "torch.distributed.run"]
+    assert "--nproc-per-node=2" in cmd and "--master-addr=127.0.0.1" in cmd
+    assert cmd[-4:] == ["--gpus", "2", "--steps", "3"]

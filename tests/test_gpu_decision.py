@@ -101,6 +101,13 @@ def test_near_ties_follow_exact_argmax(A, O, torch, plan, method):
     assert tight.sum() >= 20, tight.sum()
     assert (tight & hi_wins).sum() >= 5, (tight & hi_wins).sum()
     assert in_band > 0
+    # windows whose oracle margin is far inside the rescue threshold (~2.6e-4
+    # of P_max at this level) were rescued: their powers are the oracle's own
+    # double powers, rounded to fp32 (bit-identical arithmetic, rescue.hip)
+    Ps = np.sort(ref_P, axis=1)
+    sure = (Ps[:, -1] - Ps[:, -2]) < 1e-5 * Ps[:, -1]
+    assert sure.sum() >= 20
+    assert np.array_equal(mag[sure].view(np.uint32), ref_P[sure].astype(np.float32).view(np.uint32))
     # the same windows decided in fp32 alone: some differ from the oracle
     old = os.environ.get("FSKD_NO_RESCUE")
     os.environ["FSKD_NO_RESCUE"] = "1"

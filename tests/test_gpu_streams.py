@@ -96,3 +96,29 @@ def test_streams_two_ranks_on_one_gpu():
     assert line["symbol_errors"] == 0
     fr = line["framing"]
     assert fr["roundtrip_ok"] and fr["frames_bytes"] == 1024 * fr["frame_bytes_per_stream"]
+
+
+def test_self_launch_two_ranks_prints_n_gpus_2():
+    """A plain `bench.py --gpus 2` (no torch.distributed.run around it) starts
+    the two ranks itself; here they share the one GPU over
+    gloo. Rank 0's line reports n_gpus 2, and the configs[4] entry (strong
+    scaling over the two ranks) carries scaling_vs_n1 against the same 1024
+    streams on one GPU in the same job."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU visible")
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT", "MASTER_ADDR"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--gpus", "2",
+                        "--dist-backend", "gloo", "--windows", "65536", "--steps", "3",
+                        "--warmup", "1"], capture_output=True, timeout=600, cwd=ROOT, env=env)
+    out = r.stdout.decode()
+    assert r.returncode == 0, (out[-2000:], r.stderr.decode()[-4000:])
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out[-2000:]
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["symbol_errors"] == 0
+    s = line["streams"]
+    assert s["scaling"] == "strong" and s["symbol_errors"] == 0 and s["framing"]["roundtrip_ok"]
+    assert s["scaling_vs_n1"] > 0 and s["n1_ms_per_step"] > 0
