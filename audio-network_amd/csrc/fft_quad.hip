@@ -693,7 +693,8 @@ constexpr int kFmtWord3 = 0xFAC | (3 << 12) | (5 << 15);
 // PF: 1 = the next group's 32 loads go out during the transpose (32 VGPRs live
 // across stage 2 and the post-pass), 0 = each group loads at the top of its
 // iteration and the co-resident waves cover the latency (4 waves/SIMD at
-// MINW = 4 without spills: 104-116 VGPRs).
+// MINW = 4 without spills: 104-116 VGPRs), 2 (SPEC + SPL) = the next group's
+// loads go out after the post-pass, ahead of the spectrum stores.
 // SPEC: false = symbols (+ tone powers) only: the tone powers are picked
 // from the registers of the lanes that hold them (p.slot, a wave-uniform
 // index: s_set_gpr_idx) instead of going through the 2 KiB per-window power
@@ -724,7 +725,8 @@ template <int WPB = 4, int MINW = 4, int PF = 0, bool SPEC = true, bool FMT = fa
           int FUSED = 0, int RD = 0, int SPL = 0, int OVL = 0>
 __device__ __attribute__((always_inline)) inline void fft1024_quad_body(const FftParams &p)
 {
-    static_assert(!OVL || (FUSED >= 4 && PF == 0), "OVL: the FUSED 4 column DFT-16, loads at the top");
+    static_assert(!OVL || (FUSED >= 4 && PF != 1), "OVL: the FUSED 4 column DFT-16");
+    static_assert(PF != 2 || (SPEC && SPL), "PF 2: ahead of the linear-slab spectrum stores");
     static_assert(!SPL || SPEC, "SPL: the linear power slab of the spectrum store");
     using namespace quad;
     __shared__ __attribute__((aligned(16))) f2 slab[WPB][kQSlab];
@@ -890,7 +892,7 @@ __device__ __attribute__((always_inline)) inline void fft1024_quad_body(const Ff
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            if (PF && r == 0) load_group(g + stride < n_groups ? g + stride : g);
+            if (PF == 1 && r == 0) load_group(g + stride < n_groups ? g + stride : g);
             const int col = r == 0 ? t : k1b - 16;
 #pragma unroll
             for (int n2 = 0; n2 < 16; ++n2) b[16 * r + n2] = win[n2 * kQRow + col];
@@ -1070,6 +1072,14 @@ __device__ __attribute__((always_inline)) inline void fft1024_quad_body(const Ff
         const bool amb = p.k >= 2 && ws_ambiguous(mx, pk, owns, pk2, pk2 >= 0.f, p.amb_tq, p.amb_floor);
         if (live && t == 0) p.sym[w] = (uint8_t)(arg | (amb ? kSymAmbiguous : 0));
         if constexpr (SPEC && SPL) {
+            if constexpr (PF == 2) {
+                // the next group's loads go out ahead of this group's spectrum
+                // stores: vmcnt retires in order, so waiting for those loads
+                // no longer waits for these stores to be acknowledged
+                __builtin_amdgcn_sched_barrier(0);
+                load_group(g + stride < n_groups ? g + stride : g);
+                __builtin_amdgcn_sched_barrier(0);
+            }
             if (p.spec) {
                 // the group's live windows: floats [0, L) of the slab = the
                 // output run from window 4 g (16-byte aligned: 4 g x 513 x 4 B)

@@ -27,8 +27,8 @@
 // 2 n + 16 bytes: conflict-free 16-byte reads across windows), then lane
 // f K + t runs tone t of window f (K chains per window in parallel, the
 // dependent fp64 chain of n steps per lane); lane f K decides. FFT: one
-// window at a time, 16 KiB of double re / im in LDS, 8 butterflies per lane
-// per stage.
+// window at a time, 16 KiB of double re / im and the 16 KiB twiddle table in
+// LDS, 8 butterflies per lane per stage.
 #include "demod_internal.h"
 
 namespace fskd {
@@ -145,10 +145,14 @@ __global__ __launch_bounds__(64) void rescue_kernel(RescueParams p)
             __syncthreads();
         }
     } else {
-        // 3. FFT: one window at a time
+        // 3. FFT: one window at a time; the twiddle table is staged into LDS
+        // once (a global read per butterfly put an L2 round trip into each
+        // of the ten dependent stages)
         double *re = reinterpret_cast<double *>(smp);
         double *im = re + 1024;
-        const double2 *tw = reinterpret_cast<const double2 *>(p.tw);
+        __shared__ double2 tw[1023];
+        const double2 *gtw = reinterpret_cast<const double2 *>(p.tw);
+        for (int i = lane; i < 1023; i += 64) tw[i] = gtw[i];
         for (int g0 = 0; g0 < T; ++g0) {
             const long long w = base + idx[g0];
             const int16_t *x = p.pcm + w * p.hop;
@@ -158,9 +162,10 @@ __global__ __launch_bounds__(64) void rescue_kernel(RescueParams p)
                 im[r] = 0.0;
             }
             __syncthreads();
+#pragma unroll
             for (int half = 1; half < 1024; half <<= 1) {
                 const int len = 2 * half;
-#pragma unroll 2
+#pragma unroll
                 for (int q = lane; q < 512; q += 64) {
                     const int j = q & (half - 1);
                     const int a = (q / half) * len + j, b = a + half;

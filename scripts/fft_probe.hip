@@ -45,6 +45,8 @@ int main(int argc, char **argv)
     const int rounds = argc > 2 ? std::atoi(argv[2]) : 6;
     const int reps = argc > 3 ? std::atoi(argv[3]) : 10;
     const char *filter = argc > 4 ? argv[4] : nullptr;
+    // "spec": time with the full 513-bin spectrum stored (one shared buffer)
+    const bool time_spec = argc > 5 && std::strcmp(argv[5], "spec") == 0;
     const long long src_windows = 1LL << 20;
     const long long n_samples = src_windows * 1024;
     const long long W = (n_samples - 1024) / hop + 1;
@@ -114,6 +116,13 @@ int main(int argc, char **argv)
         return lin ? launch_fft_quad_t<4, 4, 0, true, false, 2, 4, 0, 2, 1>(p, s)
              : p.spec ? launch_fft_quad_t<4, 4, 0, true, false, 2, 4, 0, 0, 1>(p, s)
                       : launch_fft_quad_t<4, 4, 0, false, false, 2, 4, 0, 0, 1>(p, s); }, {}});
+    // spectrum: the next group's loads ahead of the spectrum stores (PF 2)
+    vs.push_back({"spl: shipped", [](const FftParams &p, hipStream_t s) { return launch_fft_quad(p, s); }, {}});
+    vs.push_back({"spl: PF2", [](const FftParams &p, hipStream_t s) {
+        const bool lin = p.spec && ((uintptr_t)p.spec & 15) == 0;
+        if (!lin) return launch_fft_quad(p, s);
+        return p.hop < 1024 ? launch_fft_quad_t<4, 4, 2, true, false, 0, 4, 0, 2>(p, s)
+                            : launch_fft_quad_t<4, 4, 2, true, false, 2, 4, 0, 2>(p, s); }, {}});
     vs.push_back({"ovl: OVL1 FMT", [](const FftParams &p, hipStream_t s) {
         if (p.spec) return launch_fft_quad(p, s);  // tone-only variant
         return p.hop < 1024 ? launch_fft_quad_t<4, 4, 0, false, true, 0, 4, 0, 0, 1>(p, s)
@@ -187,12 +196,16 @@ int main(int argc, char **argv)
         std::printf("check %-24s vs shipped: %lld symbol mismatches / %lld, max tone |dP|/peak %.2e, "
                     "spectrum (%lld windows) %.2e\n", vs[i].name.c_str(), mism, W, merr, SW, serr);
     }
-    // timing: round-robin, symbols + tone powers (the bench's batch_async shape)
+    // timing: round-robin, symbols + tone powers (the bench's batch_async
+    // shape), or with the full spectrum stored
+    float *big_spec = nullptr;
+    if (time_spec) CK(hipMalloc(&big_spec, (size_t)W * 513 * 4));
     for (int r = 0; r < rounds; ++r) {
         for (size_t i = 0; i < vs.size(); ++i) {
             FftParams p = base;
             p.sym = syms[i];
             p.mag = mags[i];
+            p.spec = big_spec;
             for (int w = 0; w < 3; ++w) CK(vs[i].launch(p, nullptr));
             for (int k = 0; k < reps; ++k) {
                 CK(hipEventRecord(e0, nullptr));
