@@ -40,6 +40,7 @@ struct demod {
     int fft_slot[kMaxTones] = {};  // FFT detector: where each tone bin's power sits (fft_quad_slot)
     // decision rescue (rescue.hip)
     bool rescue = false;        // K >= 2 and not switched off (FSKD_NO_RESCUE=1)
+    bool rescue_launch = true;  // FSKD_NO_RESCUE=flags: flag only, no rescue launch (diagnostics)
     float amb_tq = 0.f;         // detectors' ambiguity threshold: amb_tq sqrt(P_max)
     float amb_floor = 0.f;
     double rcoef[kMaxTones] = {};  // 2 cos(2 pi f_k / fs) in double, the caller's tone order
@@ -408,8 +409,12 @@ static int init_device_state(demod_t *st)
     // plus the floor tau^2 Q / 16 below which the fp32 error's second-order
     // term could reach the margin.
     for (uint32_t k = 0; k < c.k; ++k) st->rcoef[k] = 2.0 * std::cos(2.0 * M_PI * c.freqs[k] / c.fs);
-    const char *no_rescue = std::getenv("FSKD_NO_RESCUE");  // measurement switch
+    // measurement switches: FSKD_NO_RESCUE=1 turns the rescue off, =flags
+    // keeps the detectors' flags but skips the launch (the flagged windows'
+    // symbols keep bit 7: counting them is how bench.py reports the rate)
+    const char *no_rescue = std::getenv("FSKD_NO_RESCUE");
     st->rescue = c.k >= 2 && !(no_rescue && no_rescue[0] == '1');
+    st->rescue_launch = !(no_rescue && std::strcmp(no_rescue, "flags") == 0);
     if (st->rescue) {
         const double sq = (double)c.n * 32768.0;  // sqrt(Q)
         const double tau = amb_tau(st->detector, st->log2g);
@@ -552,7 +557,7 @@ int demod_batch_launches(const demod_t *st, size_t n_windows, int with_mags)
     if (!st) return DEMOD_BAD_ARG;
     if (n_windows == 0) return 0;
     const size_t per = launch_slice(st, n_windows, with_mags != 0);
-    const size_t n = (n_windows + per - 1) / per + (st->rescue ? 1 : 0);
+    const size_t n = (n_windows + per - 1) / per + (st->rescue && st->rescue_launch ? 1 : 0);
     return n > 0x7FFFFFFF ? 0x7FFFFFFF : (int)n;
 }
 
@@ -561,7 +566,7 @@ int demod_batch_launches(const demod_t *st, size_t n_windows, int with_mags)
 static int enqueue_rescue(demod_t *st, const int16_t *d_pcm, size_t n_windows, uint8_t *d_sym,
                           float *d_mag, float *d_spec, hipStream_t s)
 {
-    if (!st->rescue || n_windows == 0) return DEMOD_OK;
+    if (!st->rescue || !st->rescue_launch || n_windows == 0) return DEMOD_OK;
     RescueParams r;
     std::memset(&r, 0, sizeof(r));
     r.pcm = d_pcm;

@@ -97,11 +97,27 @@ __global__ __launch_bounds__(64) void rescue_kernel(RescueParams p)
         for (int g0 = 0; g0 < T; g0 += wpw) {
             const int cnt = min(wpw, T - g0);
             const int chunks = n / 8;  // 16-byte chunks per window
-            for (int c = lane; c < cnt * chunks; c += 64) {
-                const int ff = c / chunks, q = c - ff * chunks;
-                const long long w = base + idx[g0 + ff];
-                const u32x4q v = reinterpret_cast<const u32x4q *>(p.pcm + w * p.hop)[q];
-                *reinterpret_cast<u32x4q *>(smp + ff * stride + 16 * q) = v;
+            // 16-byte chunks, eight loads per lane in flight at a time (a
+            // plain loop left one L2 round trip per chunk on the critical path)
+            for (int c0 = 0; c0 < cnt * chunks; c0 += 8 * 64) {
+                u32x4q v[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int c = c0 + 64 * u + lane;
+                    if (c < cnt * chunks) {
+                        const int ff = c / chunks, q = c - ff * chunks;
+                        const long long w = base + idx[g0 + ff];
+                        v[u] = reinterpret_cast<const u32x4q *>(p.pcm + w * p.hop)[q];
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int c = c0 + 64 * u + lane;
+                    if (c < cnt * chunks) {
+                        const int ff = c / chunks, q = c - ff * chunks;
+                        *reinterpret_cast<u32x4q *>(smp + ff * stride + 16 * q) = v[u];
+                    }
+                }
             }
             __syncthreads();
             const bool act = f < cnt;
@@ -110,6 +126,7 @@ __global__ __launch_bounds__(64) void rescue_kernel(RescueParams p)
                 const double c = p.coef[t];
                 double s1 = 0.0, s2 = 0.0;
                 const u32x4q *xs = reinterpret_cast<const u32x4q *>(smp + f * stride);
+#pragma unroll 4
                 for (int q = 0; q < chunks; ++q) {
                     const u32x4q d = xs[q];
                     const unsigned d4[4] = {d.x, d.y, d.z, d.w};
@@ -155,10 +172,15 @@ __global__ __launch_bounds__(64) void rescue_kernel(RescueParams p)
         for (int i = lane; i < 1023; i += 64) tw[i] = gtw[i];
         for (int g0 = 0; g0 < T; ++g0) {
             const long long w = base + idx[g0];
-            const int16_t *x = p.pcm + w * p.hop;
-            for (int i = lane; i < 1024; i += 64) {
-                const unsigned r = bitrev10((unsigned)i);
-                re[r] = (double)x[i];
+            // lane l loads samples 16 l .. 16 l + 15 (two 16-byte loads, the
+            // window start is 16-byte aligned) and scatters them bit-reversed
+            const u32x4q *x = reinterpret_cast<const u32x4q *>(p.pcm + w * p.hop) + 2 * lane;
+            const u32x4q x0 = x[0], x1 = x[1];
+            const unsigned xs[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const unsigned r = bitrev10((unsigned)(16 * lane + e));
+                re[r] = (double)(short)((xs[e >> 1] >> (16 * (e & 1))) & 0xFFFFu);
                 im[r] = 0.0;
             }
             __syncthreads();

@@ -530,8 +530,23 @@ def run_config(A, D, torch, dist, args, config, rank, world, local, use_dist, st
             t_off.append(time_steps(torch, step0, steps, warm))
             t_on.append(time_steps(torch, lambda: step(), steps, warm))
         on, off = float(np.median(t_on)), float(np.median(t_off))
+        # how many windows the detector flagged: a handle that flags but
+        # skips the rescue launch leaves bit 7 on those symbols
+        os.environ["FSKD_NO_RESCUE"] = "flags"
+        try:
+            df = A.Demodulator(cfg)
+        finally:
+            del os.environ["FSKD_NO_RESCUE"]
+        if d_spec is not None:
+            df.batch_spectrum_async(d_pcm, n_eval, sl, d_mag, d_spec, stream=comp.cuda_stream)
+        else:
+            df.batch_async(d_pcm, n_eval, sl, d_mag, stream=comp.cuda_stream)
+        torch.cuda.synchronize()
+        flagged = int((sl >= 128).sum().item())
+        df.close()
         r["rescue"] = {"ms_per_step": round(on, 4), "ms_per_step_without_rescue": round(off, 4),
                        "cost_frac": round((on - off) / off, 4),
+                       "flagged_windows": flagged, "flagged_frac": flagged / float(n_eval),
                        "launches_without": d0.batch_launches(n_eval, not no_mags),
                        "how": "interleaved medians of 3 x %d steps each way" % steps}
         d0.close()
