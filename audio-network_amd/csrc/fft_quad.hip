@@ -721,8 +721,13 @@ constexpr int kFmtWord3 = 0xFAC | (3 << 12) | (5 << 15);
 // and reads follow, and column 0's DFT-16 runs while they are in flight (the
 // waits land on the first use of round 1's data, not before column 0's
 // math); the next group's round-0 writes are ordered behind them.
+// TW3R: the post-pass twiddles W1024^kP / 2 from registers instead of the
+// LDS table tw3: kP = te + 32 j, so the twiddle is a per-lane base
+// W1024^te / 2 (te = t, or 16 for lane 0's pairs j < 8) times the
+// compile-time W32^j — one packed complex product (29 VALU per group) in
+// place of 8 ds_read2_b64.
 template <int WPB = 4, int MINW = 4, int PF = 0, bool SPEC = true, bool FMT = false, int AUX = 2,
-          int FUSED = 0, int RD = 0, int SPL = 0, int OVL = 0>
+          int FUSED = 0, int RD = 0, int SPL = 0, int OVL = 0, int TW3R = 0>
 __device__ __attribute__((always_inline)) inline void fft1024_quad_body(const FftParams &p)
 {
     static_assert(!OVL || (FUSED >= 4 && PF != 1), "OVL: the FUSED 4 column DFT-16");
@@ -765,6 +770,12 @@ __device__ __attribute__((always_inline)) inline void fft1024_quad_body(const Ff
     const int mybin = t < p.k ? p.bins[t] : 0;
     const int myslot = SPL ? q * 513 + mybin : quad_slot(mybin);
     float *pw = reinterpret_cast<float *>(slab[wave]);
+    // TW3R: this lane's post-pass twiddle bases (pairs j < 8 and j >= 8)
+    f2 tb_lo = (f2){0.f, 0.f}, tb_hi = (f2){0.f, 0.f};
+    if constexpr (TW3R) {
+        tb_lo = 0.5f * t1024[t == 0 ? 16 : t];
+        tb_hi = 0.5f * t1024[t];
+    }
     __syncthreads();
 
     const long long n_groups = (p.n_windows + 3) >> 2;
@@ -985,6 +996,18 @@ __device__ __attribute__((always_inline)) inline void fft1024_quad_body(const Ff
                 const f4 x = *reinterpret_cast<const f4 *>(&tw3[tw3_at(j0, t)]);
                 w0 = (f2){x.x, x.y};
                 w1 = (f2){x.z, x.w};
+            } else if constexpr (TW3R) {
+                // W1024^kP / 2 = base x W32^j (j0 = 0 and j0 + 1 = 8 ... cheap cases)
+                const f2 b0 = j0 < 8 ? tb_lo : tb_hi, b1 = j1 < 8 ? tb_lo : tb_hi;
+                if constexpr (j0 == 0) {
+                    w0 = b0;
+                    w1 = cmulk(b1, w32c<j1>());
+                } else if constexpr (j0 == 8) {
+                    w0 = mj(b0);
+                    w1 = cmulk(b1, w32c<j1>());
+                } else {
+                    cmulk2(w0, b0, w32c<j0>(), w1, b1, w32c<j1>());
+                }
             } else {
                 w0 = tw3[tw3_at(j0, t)];
                 w1 = tw3[tw3_at(j1, t)];
@@ -1112,11 +1135,11 @@ __device__ __attribute__((always_inline)) inline void fft1024_quad_body(const Ff
 }
 
 template <int WPB = 4, int MINW = 4, int PF = 0, bool SPEC = true, bool FMT = false, int AUX = 2,
-          int FUSED = 0, int SPL = 0, int OVL = 0>
+          int FUSED = 0, int SPL = 0, int OVL = 0, int TW3R = 0>
 __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MINW > 0 ? MINW : 1)))
 void fft1024_quad_kernel(FftParams p)
 {
-    fft1024_quad_body<WPB, MINW, PF, SPEC, FMT, AUX, FUSED, 0, SPL, OVL>(p);
+    fft1024_quad_body<WPB, MINW, PF, SPEC, FMT, AUX, FUSED, 0, SPL, OVL, TW3R>(p);
 }
 
 // (a device-code attribute: the host pass of hipcc does not know the feature)
@@ -1141,15 +1164,15 @@ FSKD_NO_LDS_PAIRING void fft1024_quad_kernel_r64(FftParams p)
 // Persistent grid: as many blocks as fit the chip, each wave strides over
 // groups of 4 windows (the LDS twiddle tables are built once per block).
 template <int WPB, int MINW, int PF, bool SPEC, bool FMT = false, int AUX = 2, int FUSED = 0, int RD = 0,
-          int SPL = 0, int OVL = 0>
+          int SPL = 0, int OVL = 0, int TW3R = 0>
 hipError_t launch_fft_quad_t(const FftParams &p, hipStream_t s)
 {
     void (*kern)(FftParams);
-    static_assert(!(RD > 0 && (SPL > 0 || OVL > 0)), "SPL / OVL: fft1024_quad_kernel only");
+    static_assert(!(RD > 0 && (SPL > 0 || OVL > 0 || TW3R > 0)), "SPL / OVL / TW3R: fft1024_quad_kernel only");
     if constexpr (RD > 0)
         kern = fft1024_quad_kernel_r64<WPB, MINW, PF, SPEC, FMT, AUX, FUSED, RD>;
     else
-        kern = fft1024_quad_kernel<WPB, MINW, PF, SPEC, FMT, AUX, FUSED, SPL, OVL>;
+        kern = fft1024_quad_kernel<WPB, MINW, PF, SPEC, FMT, AUX, FUSED, SPL, OVL, TW3R>;
     int dev = 0, cus = 256, per_cu = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);

@@ -123,6 +123,20 @@ int main(int argc, char **argv)
         if (!lin) return launch_fft_quad(p, s);
         return p.hop < 1024 ? launch_fft_quad_t<4, 4, 2, true, false, 0, 4, 0, 2>(p, s)
                             : launch_fft_quad_t<4, 4, 2, true, false, 2, 4, 0, 2>(p, s); }, {}});
+    // post-pass twiddles from registers (TW3R), tone-only and spectrum
+    vs.push_back({"tw3: shipped", [](const FftParams &p, hipStream_t s) { return launch_fft_quad(p, s); }, {}});
+    vs.push_back({"tw3: TW3R", [](const FftParams &p, hipStream_t s) {
+        const bool lin = p.spec && ((uintptr_t)p.spec & 15) == 0;
+        if (p.spec && !lin) return launch_fft_quad(p, s);
+        if (p.hop < 1024)
+            return lin ? launch_fft_quad_t<4, 4, 0, true, false, 0, 4, 0, 2, 0, 1>(p, s)
+                       : launch_fft_quad_t<4, 4, 0, false, false, 0, 4, 0, 0, 0, 1>(p, s);
+        return lin ? launch_fft_quad_t<4, 4, 0, true, false, 2, 4, 0, 2, 0, 1>(p, s)
+                   : launch_fft_quad_t<4, 4, 0, false, false, 2, 4, 0, 0, 0, 1>(p, s); }, {}});
+    vs.push_back({"tw3: TW3R OVL1", [](const FftParams &p, hipStream_t s) {
+        if (p.spec) return launch_fft_quad(p, s);
+        return p.hop < 1024 ? launch_fft_quad_t<4, 4, 0, false, false, 0, 4, 0, 0, 1, 1>(p, s)
+                            : launch_fft_quad_t<4, 4, 0, false, false, 2, 4, 0, 0, 1, 1>(p, s); }, {}});
     vs.push_back({"ovl: OVL1 FMT", [](const FftParams &p, hipStream_t s) {
         if (p.spec) return launch_fft_quad(p, s);  // tone-only variant
         return p.hop < 1024 ? launch_fft_quad_t<4, 4, 0, false, true, 0, 4, 0, 0, 1>(p, s)
