@@ -557,14 +557,16 @@ int demod_batch_launches(const demod_t *st, size_t n_windows, int with_mags)
     if (!st) return DEMOD_BAD_ARG;
     if (n_windows == 0) return 0;
     const size_t per = launch_slice(st, n_windows, with_mags != 0);
-    const size_t n = (n_windows + per - 1) / per + (st->rescue && st->rescue_launch ? 1 : 0);
+    // + the decision rescue's launch (the FFT detector rescues in the kernel)
+    const size_t n = (n_windows + per - 1) / per +
+                     (st->rescue && st->rescue_launch && st->detector != kDetFft ? 1 : 0);
     return n > 0x7FFFFFFF ? 0x7FFFFFFF : (int)n;
 }
 
 // The decision rescue over a batch's windows (rescue.hip), after its detector
 // launches on the same stream.
 static int enqueue_rescue(demod_t *st, const int16_t *d_pcm, size_t n_windows, uint8_t *d_sym,
-                          float *d_mag, float *d_spec, hipStream_t s)
+                          float *d_mag, hipStream_t s)
 {
     if (!st->rescue || !st->rescue_launch || n_windows == 0) return DEMOD_OK;
     RescueParams r;
@@ -574,16 +576,10 @@ static int enqueue_rescue(demod_t *st, const int16_t *d_pcm, size_t n_windows, u
     r.hop = st->cfg.hop;
     r.n = (int)st->cfg.n;
     r.k = (int)st->cfg.k;
-    r.fft = st->detector == kDetFft ? 1 : 0;
     r.sym = d_sym;
     r.sym_aligned4 = ((uintptr_t)d_sym & 3) == 0;
     r.mag = d_mag;
-    r.spec = d_spec;
-    r.tw = st->d_rtw;
-    for (uint32_t k = 0; k < st->cfg.k; ++k) {
-        r.bins[k] = st->fft_bins[k];
-        r.coef[k] = st->rcoef[k];
-    }
+    for (uint32_t k = 0; k < st->cfg.k; ++k) r.coef[k] = st->rcoef[k];
     HIP_TRY(launch_rescue(r, s));
     return DEMOD_OK;
 }
@@ -615,9 +611,12 @@ static int enqueue_fft(demod_t *st, const int16_t *d_pcm, size_t n_windows, uint
     p.spec = d_spec;
     p.amb_tq = st->amb_tq;
     p.amb_floor = st->amb_floor;
+    // the FFT detector re-decides its flagged windows itself (rescue_fft.h):
+    // one launch, no symbol scan
+    p.rescue = st->rescue && st->rescue_launch ? 1 : 0;
+    p.rtw = st->d_rtw;
     HIP_TRY(launch_fft_quad(p, s));
-    const int rc = enqueue_rescue(st, d_pcm, n_windows, d_sym, d_mag, d_spec, s);
-    return rc < 0 ? rc : (int)n_windows;
+    return (int)n_windows;
 }
 
 
@@ -665,7 +664,7 @@ static int enqueue_batch(demod_t *st, const int16_t *d_pcm, size_t n_windows, ui
         p.mag = d_mag ? d_mag + w0 * st->cfg.k : nullptr;
         HIP_TRY(launch_detector(st->detector, p, s));
     }
-    const int rc = enqueue_rescue(st, d_pcm, n_windows, d_sym, d_mag, nullptr, s);
+    const int rc = enqueue_rescue(st, d_pcm, n_windows, d_sym, d_mag, s);
     return rc < 0 ? rc : (int)n_windows;
 }
 

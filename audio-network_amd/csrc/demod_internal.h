@@ -137,6 +137,8 @@ struct FftParams {
     float *spec;             // [n_windows][513] or nullptr
     float amb_tq;            // decision rescue, as GoertzelParams
     float amb_floor;
+    int rescue;              // 1: flagged windows are re-decided in the kernel (rescue_fft.h)
+    const double *rtw;       // rescue: [1023] (cos, sin), stage len at len / 2 - 1 + j
 };
 
 // rescue.hip: re-decides every window whose symbol carries kSymAmbiguous.
@@ -146,13 +148,9 @@ struct RescueParams {
     long long hop;
     int n;
     int k;
-    int fft;                 // 0: Goertzel recurrence, 1: radix-2 FFT (n = 1024)
     uint8_t *sym;
     int sym_aligned4;        // sym is 4-byte aligned: dword scans
     float *mag;              // [n_windows][k] or nullptr
-    float *spec;             // [n_windows][n / 2 + 1] or nullptr (fft)
-    const double *tw;        // fft: [n - 1] (cos, sin), stage len at len / 2 - 1 + j
-    int bins[kMaxTones];     // fft: tone bins
     double coef[kMaxTones];  // Goertzel: 2 cos(2 pi f_k / fs), the caller's tone order
 };
 hipError_t launch_rescue(const RescueParams &p, hipStream_t s);

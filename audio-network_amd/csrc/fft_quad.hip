@@ -26,6 +26,7 @@
 #include <type_traits>
 
 #include "demod_internal.h"
+#include "rescue_fft.h"
 #include "window_sum.h"
 
 namespace fskd {
@@ -727,7 +728,7 @@ constexpr int kFmtWord3 = 0xFAC | (3 << 12) | (5 << 15);
 // compile-time W32^j — one packed complex product (29 VALU per group) in
 // place of 8 ds_read2_b64.
 template <int WPB = 4, int MINW = 4, int PF = 0, bool SPEC = true, bool FMT = false, int AUX = 2,
-          int FUSED = 0, int RD = 0, int SPL = 0, int OVL = 0, int TW3R = 0>
+          int FUSED = 0, int RD = 0, int SPL = 0, int OVL = 0, int TW3R = 0, int RSC = 1>
 __device__ __attribute__((always_inline)) inline void fft1024_quad_body(const FftParams &p)
 {
     static_assert(!OVL || (FUSED >= 4 && PF != 1), "OVL: the FUSED 4 column DFT-16");
@@ -781,6 +782,7 @@ __device__ __attribute__((always_inline)) inline void fft1024_quad_body(const Ff
     const long long n_groups = (p.n_windows + 3) >> 2;
     const long long stride = (long long)gridDim.x * WPB;
     long long g = tile_block(p.xcd_swizzle) * WPB + wave;
+    const long long g_first = g;
     static_assert(!FMT || PF == 0, "FMT loads straight into a[]");
     uint32_t nx[FMT ? 1 : 32];
     f2 nxf[FMT ? 32 : 1];
@@ -1132,14 +1134,88 @@ __device__ __attribute__((always_inline)) inline void fft1024_quad_body(const Ff
             __builtin_amdgcn_wave_barrier();
         }
     }
+
+    // 6. decision rescue (rescue_fft.h), after the group loop
+    //    (no code inside it, whose registers stay as they were): the symbol
+    //    bytes of the groups are read back (one byte per window) and every
+    //    flagged window is decided again in double, one window per wave at a
+    //    time through the wave's slab.
+    //    RSC 1: each wave its own groups' windows.
+    //    RSC 2: the block's flagged windows dealt round-robin to its waves, 64
+    //    groups per wave at a time; every wave reads a chunk's bytes before
+    //    any rescue rewrites them (the barrier), so all deal the same list.
+    //    RSC 0: no rescue code (probe A/B).
+    auto rescue_one = [&](long long ww, lds_double *xs) {
+        rescue_fft_window(p.pcm + ww * p.hop, xs, reinterpret_cast<const double2 *>(p.rtw), p.bins, p.k,
+                          p.sym + ww, p.mag ? p.mag + ww * p.k : nullptr, p.spec ? p.spec + ww * 513 : nullptr);
+    };
+    auto flags4 = [&](long long gl) {  // bit q: window 4 gl + q is flagged
+        unsigned f = 0;
+        if (gl < n_groups) {
+#pragma unroll
+            for (int q0 = 0; q0 < 4; ++q0) {
+                const long long ww = 4 * gl + q0;
+                if (ww < p.n_windows &&
+                    (__hip_atomic_load(p.sym + ww, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & kSymAmbiguous))
+                    f |= 1u << q0;
+            }
+        }
+        return f;
+    };
+    if constexpr (RSC == 1) {
+        if (p.rescue) {
+            __builtin_amdgcn_s_waitcnt(0);  // this wave's symbol stores have landed
+            lds_double *xs = (lds_double *)(slab[wave]);
+            for (long long gb = g_first; gb < n_groups; gb += 64 * stride) {
+                const unsigned f = flags4(gb + (long long)lane * stride);
+                unsigned long long m = __ballot(f != 0);
+                while (m) {
+                    const int src = __builtin_ctzll(m);
+                    m &= m - 1;
+                    const unsigned fs = (unsigned)__builtin_amdgcn_readlane((int)f, src);
+                    const long long gs = gb + (long long)src * stride;
+                    for (int q0 = 0; q0 < 4; ++q0)
+                        if ((fs >> q0) & 1u) rescue_one(4 * gs + q0, xs);
+                }
+            }
+        }
+    } else if constexpr (RSC == 2) {
+        if (p.rescue) {
+            __builtin_amdgcn_s_waitcnt(0);  // this wave's symbol stores have landed
+            __syncthreads();                // ... and every wave's of the block
+            lds_double *xs = (lds_double *)(slab[wave]);
+            int seen = 0;                   // flagged windows dealt so far (wave-uniform)
+            for (long long gb0 = g_first - wave; gb0 < n_groups; gb0 += 64 * stride) {
+                unsigned f[WPB];
+#pragma unroll
+                for (int wv = 0; wv < WPB; ++wv) f[wv] = flags4(gb0 + wv + (long long)lane * stride);
+                __syncthreads();
+#pragma unroll
+                for (int wv = 0; wv < WPB; ++wv) {
+                    unsigned long long m = __ballot(f[wv] != 0);
+                    while (m) {
+                        const int src = __builtin_ctzll(m);
+                        m &= m - 1;
+                        const unsigned fs = (unsigned)__builtin_amdgcn_readlane((int)f[wv], src);
+                        const long long gs = gb0 + wv + (long long)src * stride;
+                        for (int q0 = 0; q0 < 4; ++q0)
+                            if ((fs >> q0) & 1u) {
+                                if (seen++ % WPB != wave) continue;
+                                rescue_one(4 * gs + q0, xs);
+                            }
+                    }
+                }
+            }
+        }
+    }
 }
 
 template <int WPB = 4, int MINW = 4, int PF = 0, bool SPEC = true, bool FMT = false, int AUX = 2,
-          int FUSED = 0, int SPL = 0, int OVL = 0, int TW3R = 0>
+          int FUSED = 0, int SPL = 0, int OVL = 0, int TW3R = 0, int RSC = 1>
 __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MINW > 0 ? MINW : 1)))
 void fft1024_quad_kernel(FftParams p)
 {
-    fft1024_quad_body<WPB, MINW, PF, SPEC, FMT, AUX, FUSED, 0, SPL, OVL, TW3R>(p);
+    fft1024_quad_body<WPB, MINW, PF, SPEC, FMT, AUX, FUSED, 0, SPL, OVL, TW3R, RSC>(p);
 }
 
 // (a device-code attribute: the host pass of hipcc does not know the feature)
@@ -1164,7 +1240,7 @@ FSKD_NO_LDS_PAIRING void fft1024_quad_kernel_r64(FftParams p)
 // Persistent grid: as many blocks as fit the chip, each wave strides over
 // groups of 4 windows (the LDS twiddle tables are built once per block).
 template <int WPB, int MINW, int PF, bool SPEC, bool FMT = false, int AUX = 2, int FUSED = 0, int RD = 0,
-          int SPL = 0, int OVL = 0, int TW3R = 0>
+          int SPL = 0, int OVL = 0, int TW3R = 0, int RSC = 1>
 hipError_t launch_fft_quad_t(const FftParams &p, hipStream_t s)
 {
     void (*kern)(FftParams);
@@ -1172,7 +1248,7 @@ hipError_t launch_fft_quad_t(const FftParams &p, hipStream_t s)
     if constexpr (RD > 0)
         kern = fft1024_quad_kernel_r64<WPB, MINW, PF, SPEC, FMT, AUX, FUSED, RD>;
     else
-        kern = fft1024_quad_kernel<WPB, MINW, PF, SPEC, FMT, AUX, FUSED, SPL, OVL, TW3R>;
+        kern = fft1024_quad_kernel<WPB, MINW, PF, SPEC, FMT, AUX, FUSED, SPL, OVL, TW3R, RSC>;
     int dev = 0, cus = 256, per_cu = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);

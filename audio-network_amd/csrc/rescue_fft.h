@@ -1,0 +1,165 @@
+// rescue_fft.h — the FFT detector's decision rescue, run inside the detector
+// (DESIGN.md §2a).
+//
+// A window whose fp32 top-2 tone margin is within the powers' error bound is
+// decided again with the definition's arithmetic in double precision: the
+// iterative radix-2 DIT FFT of oracle/fsk_oracle.c:oracle_fft_power
+// (bit-reversed input, stages len = 2 .. 1024, w = (cos, sin)(-2 pi j / len)
+// from the host's table, t = w b, b' = a - t, a' = a + t, every product and
+// sum rounded on its own), P[b] = re^2 + im^2, argmax over the tone bins with
+// ties to the lowest tone. Every butterfly runs on the same operands in the
+// same order as the oracle's, so the rescued powers and symbol are the
+// oracle's bit for bit; only where the values wait between stages differs.
+//
+// The wave that decided the group runs it at once, in a wave-uniform branch,
+// with all 64 lanes on one window: the ten stages in three register passes of
+// 16 points per lane — positions 16 l + e of the bit-reversed array (stages
+// len 2 .. 16 inside the lane), then (l & 15) + 16 m + 256 (l >> 4) (len 32 ..
+// 256), then l + 64 q + 256 m (len 512, 1024) — with two exchanges through
+// the wave's own 1088-double LDS slab (re, then im). Flagged windows are rare
+// (0.04 % of the hop-256 bench stream), so the cost spreads over the
+// detector's grid: no second launch and no scan of the symbol bytes.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace fskd {
+
+typedef __attribute__((address_space(3))) double lds_double;
+
+// LDS slot of FFT position q: one pad double per 16 (1088 slots)
+__device__ __forceinline__ int rfslot(int q) { return q + (q >> 4); }
+
+__device__ __forceinline__ void rf_wave_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// the definition's radix-2 butterfly on (a, b) with twiddle (wr, wi)
+__device__ __forceinline__ void rf_bfly(double &ar, double &ai, double &br, double &bi, double wr, double wi)
+{
+#pragma clang fp contract(off)
+    const double tr = br * wr - bi * wi;
+    const double ti = br * wi + bi * wr;
+    const double xr = ar, xi = ai;
+    br = xr - tr;
+    bi = xi - ti;
+    ar = xr + tr;
+    ai = xi + ti;
+}
+
+// One window (n = 1024) at x, the whole wave. xs: the wave's LDS slab (>= 1088
+// doubles, free on entry, free on return). rtw: [1023] (cos, sin), stage len
+// at len / 2 - 1 + j. bins: the k tone bins. Writes the symbol, and the tone
+// powers / full spectrum (rounded to fp32) where the rows are given.
+__device__ __attribute__((always_inline)) inline void rescue_fft_window(const int16_t *__restrict__ x, lds_double *xs,
+                                                            const double2 *__restrict__ rtw,
+                                                            const int *__restrict__ bins, int k,
+                                                            uint8_t *sym, float *mag, float *spec)
+{
+#pragma clang fp contract(off)
+    const int lane = (int)__lane_id();
+    const int lo = lane & 15, hi = lane >> 4;
+    const int brl = (int)(__builtin_bitreverse32((unsigned)lane) >> 26);  // bitrev6(lane)
+    double ar[16], ai[16];
+    // pass A: position 16 l + e holds sample bitrev10(16 l + e) = 64 bitrev4(e) + bitrev6(l)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+        const int b4 = (int)(__builtin_bitreverse32((unsigned)e) >> 28);
+        ar[e] = (double)x[64 * b4 + brl];
+        ai[e] = 0.0;
+    }
+#pragma unroll
+    for (int h = 1; h <= 8; h <<= 1)
+#pragma unroll
+        for (int e = 0; e < 16; ++e)
+            if (!(e & h)) {
+                const double2 t = rtw[h - 1 + (e & (h - 1))];
+                rf_bfly(ar[e], ai[e], ar[e + h], ai[e + h], t.x, t.y);
+            }
+    // exchange A -> B: lane l takes positions lo + 16 m + 256 hi
+#pragma unroll
+    for (int e = 0; e < 16; ++e) xs[rfslot(16 * lane + e)] = ar[e];
+    rf_wave_sync();
+#pragma unroll
+    for (int m = 0; m < 16; ++m) ar[m] = xs[rfslot(lo + 16 * m + 256 * hi)];
+    rf_wave_sync();
+#pragma unroll
+    for (int e = 0; e < 16; ++e) xs[rfslot(16 * lane + e)] = ai[e];
+    rf_wave_sync();
+#pragma unroll
+    for (int m = 0; m < 16; ++m) ai[m] = xs[rfslot(lo + 16 * m + 256 * hi)];
+    // pass B: stages len 32 .. 256 (half 16 h), j = lo + 16 (m & (h - 1))
+#pragma unroll
+    for (int h = 1; h <= 8; h <<= 1)
+#pragma unroll
+        for (int m = 0; m < 16; ++m)
+            if (!(m & h)) {
+                const double2 t = rtw[16 * h - 1 + lo + 16 * (m & (h - 1))];
+                rf_bfly(ar[m], ai[m], ar[m + h], ai[m + h], t.x, t.y);
+            }
+    // exchange B -> C: lane l takes positions l + 64 q + 256 m (slot 4 q + m)
+    rf_wave_sync();
+#pragma unroll
+    for (int m = 0; m < 16; ++m) xs[rfslot(lo + 16 * m + 256 * hi)] = ar[m];
+    rf_wave_sync();
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int m = 0; m < 4; ++m) ar[4 * q + m] = xs[rfslot(lane + 64 * q + 256 * m)];
+    rf_wave_sync();
+#pragma unroll
+    for (int m = 0; m < 16; ++m) xs[rfslot(lo + 16 * m + 256 * hi)] = ai[m];
+    rf_wave_sync();
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int m = 0; m < 4; ++m) ai[4 * q + m] = xs[rfslot(lane + 64 * q + 256 * m)];
+    // pass C: stage len 512 (pairs m, m + 1; j = g) and 1024 (pairs m, m + 2; j = g + 256 m)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int g = lane + 64 * q;
+        const double2 t1 = rtw[255 + g];
+        rf_bfly(ar[4 * q], ai[4 * q], ar[4 * q + 1], ai[4 * q + 1], t1.x, t1.y);
+        rf_bfly(ar[4 * q + 2], ai[4 * q + 2], ar[4 * q + 3], ai[4 * q + 3], t1.x, t1.y);
+        const double2 t2 = rtw[511 + g], t3 = rtw[767 + g];
+        rf_bfly(ar[4 * q], ai[4 * q], ar[4 * q + 2], ai[4 * q + 2], t2.x, t2.y);
+        rf_bfly(ar[4 * q + 1], ai[4 * q + 1], ar[4 * q + 3], ai[4 * q + 3], t3.x, t3.y);
+    }
+    // natural order now: slot 4 q + m holds bin g + 256 m. P = re^2 + im^2 for
+    // bins 0 .. 512 into the slab (reads done above), the spectrum row as fp32
+    rf_wave_sync();
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+            const int b = lane + 64 * q + 256 * m;
+            const double P = ar[4 * q + m] * ar[4 * q + m] + ai[4 * q + m] * ai[4 * q + m];
+            xs[b] = P;
+            if (spec) spec[b] = (float)P;
+        }
+    if (lane == 0) {
+        const double P = ar[2] * ar[2] + ai[2] * ai[2];
+        xs[512] = P;
+        if (spec) spec[512] = (float)P;
+    }
+    rf_wave_sync();
+    // argmax over the tones (ties to the lowest), as the oracle's loop
+    double best = -1.0;
+    int arg = 0;
+    for (int i = 0; i < k; ++i) {
+        const double P = xs[bins[i]];
+        if (mag && lane == i) mag[i] = (float)P;
+        if (P > best) {
+            best = P;
+            arg = i;
+        }
+    }
+    if (lane == 0) *sym = (uint8_t)arg;
+    rf_wave_sync();
+}
+
+}  // namespace fskd

@@ -25,12 +25,13 @@
  * Decisions: every symbol is the argmax of the tone powers as the double-
  * precision definition computes them (ties to the lowest tone). The kernels
  * decide in fp32; a window whose fp32 top-2 margin lies within the powers'
- * error bound leaves its detector flagged, and a second launch on the same
- * stream (the decision rescue) decides it again in double with
- * the definition's own arithmetic and rewrites its symbol and powers. A batch
- * is complete when its stream has passed that second launch; there is no
- * state shared between batches, so batches of one handle may run on
- * different streams.
+ * error bound is flagged, and the decision rescue decides it
+ * again in double with the definition's own arithmetic and rewrites its
+ * symbol and powers: a second launch on the same stream for the Goertzel-
+ * family detectors, the tail of its own launch for the FFT detector. A batch
+ * is complete when its stream has passed those launches; there is no state
+ * shared between batches, so batches of one handle may run on different
+ * streams.
  *
  * Every compute entry point runs on the GPU (HIP, gfx950). There is no CPU
  * fallback: without a visible MI355X, demod_create() fails with
@@ -143,7 +144,8 @@ int demod_max_symbols(const demod_t *st, size_t n_frames);
 
 /* Kernel launches one device-pointer demod_batch / demod_batch_async of
  * n_windows makes (with_mags: magnitudes requested): the detector's, plus one
- * for the decision rescue (K >= 2). Goertzel-family batches whose symbol +
+ * for the decision rescue (K >= 2, Goertzel-family detectors; the FFT
+ * detector rescues inside its own launch). Goertzel-family batches whose symbol +
  * magnitude output exceeds ~10 MiB run as equal detector slices, so each
  * launch's output is written back from L2 in a burst instead of interleaved
  * with the input stream; profilers see that many

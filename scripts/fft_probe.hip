@@ -33,6 +33,20 @@ using namespace fskd;
         }                                                                       \
     } while (0)
 
+// the shipped kernel with decision-rescue strategy R (fft_quad.hip step 6)
+template <int R>
+hipError_t launch_rsc(const FftParams &p, hipStream_t s)
+{
+    const bool lin = p.spec && ((uintptr_t)p.spec & 15) == 0;
+    if (p.hop < 1024)
+        return lin ? launch_fft_quad_t<4, 4, 0, true, false, 0, 4, 0, 2, 0, 0, R>(p, s)
+             : p.spec ? launch_fft_quad_t<4, 4, 0, true, false, 0, 4, 0, 0, 0, 0, R>(p, s)
+                      : launch_fft_quad_t<4, 4, 0, false, false, 0, 4, 0, 0, 0, 0, R>(p, s);
+    return lin ? launch_fft_quad_t<4, 4, 0, true, false, 2, 4, 0, 2, 0, 0, R>(p, s)
+         : p.spec ? launch_fft_quad_t<4, 4, 0, true, false, 2, 4, 0, 0, 0, 0, R>(p, s)
+                  : launch_fft_quad_t<4, 4, 0, false, false, 2, 4, 0, 0, 0, 0, R>(p, s);
+}
+
 struct Var {
     std::string name;
     std::function<hipError_t(const FftParams &, hipStream_t)> launch;
@@ -85,6 +99,24 @@ int main(int argc, char **argv)
     CK(hipMemcpy(d_t1, t1.data(), 4096, hipMemcpyHostToDevice));
     CK(hipMemcpy(d_t2, t2.data(), 4096, hipMemcpyHostToDevice));
     CK(hipMemcpy(d_bins, bins, 8, hipMemcpyHostToDevice));
+
+    // the decision rescue's double radix-2 twiddles and thresholds, as
+    // demod_api.cpp sets them for the FFT detector
+    std::vector<double> rtw(2 * 1023);
+    for (int len = 2; len <= 1024; len <<= 1) {
+        const double ang = -(2.0 * M_PI) / (double)len;
+        for (int j = 0; j < len / 2; ++j) {
+            double sn, cs;
+            sincos(ang * (double)j, &sn, &cs);
+            rtw[2 * (len / 2 - 1 + j)] = cs;
+            rtw[2 * (len / 2 - 1 + j) + 1] = sn;
+        }
+    }
+    double *d_rtw;
+    CK(hipMalloc(&d_rtw, rtw.size() * 8));
+    CK(hipMemcpy(d_rtw, rtw.data(), rtw.size() * 8, hipMemcpyHostToDevice));
+    const float amb_tq = (float)(12.0 * 2.64e-7 * 1024.0 * 32768.0);
+    const float amb_floor = amb_tq * amb_tq / 16.0f;
 
     std::vector<Var> vs;
     // variant 0 is the reference every other variant is checked against
@@ -141,6 +173,18 @@ int main(int argc, char **argv)
         if (p.spec) return launch_fft_quad(p, s);  // tone-only variant
         return p.hop < 1024 ? launch_fft_quad_t<4, 4, 0, false, true, 0, 4, 0, 0, 1>(p, s)
                             : launch_fft_quad_t<4, 4, 0, false, true, 2, 4, 0, 0, 1>(p, s); }, {}});
+    // round 3: the decision rescue inside the detector (step 6): compiled out,
+    // compiled in and off, flags only, per-wave and per-block rescue
+    vs.push_back({"rsc0 no rescue code", [](const FftParams &p, hipStream_t s) { return launch_rsc<0>(p, s); }, {}});
+    vs.push_back({"rsc1 compiled, off", [](const FftParams &p, hipStream_t s) { return launch_rsc<1>(p, s); }, {}});
+    vs.push_back({"rsc1 flags only", [=](const FftParams &p, hipStream_t s) {
+        FftParams q = p; q.amb_tq = amb_tq; q.amb_floor = amb_floor; return launch_rsc<1>(q, s); }, {}});
+    vs.push_back({"rsc1 per-wave rescue", [=](const FftParams &p, hipStream_t s) {
+        FftParams q = p; q.amb_tq = amb_tq; q.amb_floor = amb_floor; q.rescue = 1; q.rtw = d_rtw;
+        return launch_rsc<1>(q, s); }, {}});
+    vs.push_back({"rsc2 per-block rescue", [=](const FftParams &p, hipStream_t s) {
+        FftParams q = p; q.amb_tq = amb_tq; q.amb_floor = amb_floor; q.rescue = 1; q.rtw = d_rtw;
+        return launch_rsc<2>(q, s); }, {}});
     if (filter) {
         std::vector<Var> keep;
         for (size_t i = 0; i < vs.size(); ++i)

@@ -10,7 +10,7 @@ Signals: the bench level (A 8000, sigma 400), a quiet signal (A 20,
 sigma 10), pure noise (sigma 2000), two tones of equal amplitude in every
 window (every window a near tie), digital silence.
 
-    python scripts/rescue_cost.py [--windows 262144] [--reps 20]
+    python scripts/rescue_cost.py [--windows 262144] [--reps 20] [--only fft]
 """
 import argparse
 import json
@@ -40,6 +40,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--windows", type=int, default=1 << 18)
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--only", default="", help="run the detectors whose name contains this")
     args = ap.parse_args()
     import torch
     import bench
@@ -54,6 +55,7 @@ def main():
             ("fold F16 K=8", f8, A.METHOD_FOLDED, n),
             ("residue K=8", odd8, A.METHOD_RESIDUE, n),
             ("fft hop 256", A.FSK2_FREQS, A.METHOD_FFT, 256)]
+    dets = [d for d in dets if args.only in d[0]]
     for name, freqs, method, hop in dets:
         cfg = A.make_cfg(freqs=freqs, method=method, hop=hop)
         sigs = {}

@@ -159,3 +159,32 @@ def test_decision_margins_at_bench_levels(A, O, torch, sigma, plan):
           f"{int((sym != d_true.cpu().numpy()).sum())} transmitted-symbol errors")
     if sigma == 400:
         assert in_band == 0 and (sym == d_true.cpu().numpy()).all()
+
+
+@pytest.mark.parametrize("hop", [1024, 256, 200])
+def test_fft_rescue_spectrum_is_the_oracles(A, O, torch, hop):
+    """The FFT rescue (rescue_fft_kernel: the ten radix-2 stages in three
+    register passes) re-runs the definition's butterflies on the same
+    operands, so a rescued window's whole stored spectrum is the oracle's
+    double spectrum rounded to fp32, bit for bit — on aligned near-tie
+    windows and on the straddling windows of a sliding stream over them."""
+    freqs = A.FSK8_FREQS
+    x, _ = near_tie_windows(freqs, 800, seed=4242 + hop)
+    flat = x.reshape(-1)
+    W = (flat.size - 1024) // hop + 1
+    with A.Demodulator(freqs=freqs, hop=hop, method=FFT) as d:
+        d_pcm = torch.from_numpy(flat.copy()).cuda()
+        d_sym = torch.empty(W, dtype=torch.uint8, device="cuda")
+        d_mag = torch.empty((W, len(freqs)), dtype=torch.float32, device="cuda")
+        d_spec = torch.empty((W, 513), dtype=torch.float32, device="cuda")
+        d.batch_spectrum_async(d_pcm, W, d_sym, d_mag, d_spec)
+        torch.cuda.synchronize()
+    sym, mag, spec = d_sym.cpu().numpy(), d_mag.cpu().numpy(), d_spec.cpu().numpy()
+    ref_sym, ref_P = O.fft_demod(flat, freqs, 1024, hop)
+    check_decisions(sym, mag, ref_sym, ref_P)
+    Ps = np.sort(ref_P, axis=1)
+    sure = np.flatnonzero((Ps[:, -1] - Ps[:, -2]) < 1e-5 * Ps[:, -1])
+    assert sure.size >= (20 if hop == 1024 else 5), sure.size
+    full = np.stack([O.fft_power(flat[i * hop:i * hop + 1024]) for i in sure]).astype(np.float32)
+    assert np.array_equal(spec[sure].view(np.uint32), full.view(np.uint32))
+    assert np.array_equal(mag[sure].view(np.uint32), ref_P[sure].astype(np.float32).view(np.uint32))
