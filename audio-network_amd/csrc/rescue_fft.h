@@ -51,6 +51,19 @@ __device__ __forceinline__ void rf_bfly(double &ar, double &ai, double &br, doub
     ai = xi + ti;
 }
 
+// The same butterfly with w = (cos 0, sin 0) = (1, -0): t = b exactly (up to
+// the sign of a zero), so the products are skipped. Zeros of either sign add
+// and square alike, so every power stays bit-identical to the oracle's.
+__device__ __forceinline__ void rf_bfly0(double &ar, double &ai, double &br, double &bi)
+{
+#pragma clang fp contract(off)
+    const double xr = ar, xi = ai;
+    ar = xr + br;
+    ai = xi + bi;
+    br = xr - br;
+    bi = xi - bi;
+}
+
 // One window (n = 1024) at x, the whole wave. xs: the wave's LDS slab (>= 1088
 // doubles, free on entry, free on return). rtw: [1023] (cos, sin), stage len
 // at len / 2 - 1 + j. bins: the k tone bins. Writes the symbol, and the tone
@@ -77,8 +90,12 @@ __device__ __attribute__((always_inline)) inline void rescue_fft_window(const in
 #pragma unroll
         for (int e = 0; e < 16; ++e)
             if (!(e & h)) {
-                const double2 t = rtw[h - 1 + (e & (h - 1))];
-                rf_bfly(ar[e], ai[e], ar[e + h], ai[e + h], t.x, t.y);
+                if ((e & (h - 1)) == 0) {
+                    rf_bfly0(ar[e], ai[e], ar[e + h], ai[e + h]);
+                } else {
+                    const double2 t = rtw[h - 1 + (e & (h - 1))];
+                    rf_bfly(ar[e], ai[e], ar[e + h], ai[e + h], t.x, t.y);
+                }
             }
     // exchange A -> B: lane l takes positions lo + 16 m + 256 hi
 #pragma unroll
@@ -122,10 +139,9 @@ __device__ __attribute__((always_inline)) inline void rescue_fft_window(const in
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         const int g = lane + 64 * q;
-        const double2 t1 = rtw[255 + g];
+        const double2 t1 = rtw[255 + g], t2 = rtw[511 + g], t3 = rtw[767 + g];
         rf_bfly(ar[4 * q], ai[4 * q], ar[4 * q + 1], ai[4 * q + 1], t1.x, t1.y);
         rf_bfly(ar[4 * q + 2], ai[4 * q + 2], ar[4 * q + 3], ai[4 * q + 3], t1.x, t1.y);
-        const double2 t2 = rtw[511 + g], t3 = rtw[767 + g];
         rf_bfly(ar[4 * q], ai[4 * q], ar[4 * q + 2], ai[4 * q + 2], t2.x, t2.y);
         rf_bfly(ar[4 * q + 1], ai[4 * q + 1], ar[4 * q + 3], ai[4 * q + 3], t3.x, t3.y);
     }

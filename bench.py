@@ -42,7 +42,9 @@ Extra entries of the default run:
 
 Defaults: 200 timed steps after 20 warmup steps (the warmup is at least 64
 launches, MIN_WARMUP), so each config keeps the GPU busy for 0.1-0.5 s
-rather than a few ms, long enough for an outside utilisation sampler to see.
+rather than a few ms. "sustained" (N = 1 headline, --sustain 6): the same
+step back to back for ~6 s, the steady rate over seconds, during which an
+outside utilisation sampler sees the GPU busy.
 """
 import argparse
 import importlib.util
@@ -234,7 +236,7 @@ def free_port() -> int:
 
 def run_config(A, D, torch, dist, args, config, rank, world, local, use_dist, steps, warmup,
                plan="survey", method_name="auto", hop_fft=256, no_mags=False, spectrum=False,
-               rescue_ab=False, parity_windows=0, n_streams_total=1024):
+               rescue_ab=False, parity_windows=0, n_streams_total=1024, sustain_s=0.0):
     """Allocate, synthesise, warm up and time one workload; returns a dict."""
     freqs = A.FSK8_FREQS if config == "fsk8" else A.FSK2_FREQS
     if config == "fsk8" and plan == "odd":
@@ -511,6 +513,25 @@ def run_config(A, D, torch, dist, args, config, rank, world, local, use_dist, st
                               "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
                               "frac": round(tf / VALU_PEAK_TFLOPS, 4),
                               "flop_per_window": fpw}
+    if sustain_s > 0 and not use_dist:
+        # the same step back to back for sustain_s seconds (synchronised every
+        # 256 steps): the steady rate over seconds rather than milliseconds,
+        # long enough for an outside utilisation sampler to see the GPU busy
+        torch.cuda.synchronize()
+        t0, n_sus = time.perf_counter(), 0
+        while True:
+            for _ in range(256):
+                step()
+            n_sus += 256
+            torch.cuda.synchronize()
+            if time.perf_counter() - t0 >= sustain_s:
+                break
+        el = time.perf_counter() - t0
+        r["sustained"] = {"seconds": round(el, 3), "steps": n_sus,
+                          "ms_per_step": round(el / n_sus * 1e3, 4),
+                          "value": round(total_windows * n / (el / n_sus) / 1e6, 1),
+                          "unit": "Msamples/s",
+                          "how": "the timed step back to back, synchronised every 256 steps"}
     if rescue_ab and not use_dist:
         # the same step with the decision rescue switched off: its cost
         os.environ["FSKD_NO_RESCUE"] = "1"
@@ -737,6 +758,9 @@ def main():
     ap.add_argument("--no-extras", action="store_true",
                     help="skip the extra entries (fsk8, fft_hop256*, streams, host_e2e at N = 1; "
                          "streams at N > 1)")
+    ap.add_argument("--sustain", type=float, default=6.0,
+                    help="N = 1 headline: also run the step back to back for this many seconds "
+                         "and report the rate as 'sustained' (0: off)")
     ap.add_argument("--force-dist", action="store_true",
                     help="initialise torch.distributed and run the gather even at N = 1 "
                          "(exercises the RCCL path on one GPU)")
@@ -778,7 +802,8 @@ def main():
     r = run_config(A, D, torch, dist, args, args.config, rank, world, local, use_dist,
                    args.steps, args.warmup, plan=args.plan, method_name=args.method,
                    hop_fft=args.hop, no_mags=args.no_mags, spectrum=args.spectrum,
-                   rescue_ab=plain and args.config in ("fsk2", "fsk8", "fft"))
+                   rescue_ab=plain and args.config in ("fsk2", "fsk8", "fft"),
+                   sustain_s=args.sustain if plain and args.config == "fsk2" and not args.no_extras else 0.0)
 
     extras = {}
     if plain and args.config == "fsk2" and not args.no_extras:
@@ -799,34 +824,39 @@ def main():
         torch.cuda.empty_cache()
         extras["streams"] = streams_child(args)
     elif world > 1 and args.config == "fsk2" and not args.no_extras:
-        # configs[4] over the N ranks (strong scaling), and the same workload on
-        # rank 0's GPU alone for scaling_vs_n1 (the other ranks wait)
-        for k in ("d_pcm", "d_sym", "d_mag", "d_true"):
-            r.pop(k, None)
-        torch.cuda.empty_cache()
-        args.graph = args.dist_backend == "nccl"
-        rs = run_config(A, D, torch, dist, args, "streams", rank, world, local, True,
-                        args.steps, args.warmup)
-        ent = {"workload": f"configs[4]: 1024 streams x 2048 windows sharded over {world} GPUs",
-               "scaling": "strong", "value": round(rs["total_windows"] * 1024 /
-                                                   (rs["ms_per_step"] / 1e3) / 1e6, 1),
-               "unit": "Msamples/s", "ms_per_step": round(rs["ms_per_step"], 4),
-               "kernel_ms": round(rs["kernel_ms"], 4), "symbol_errors": rs["sym_err"],
-               "framing": rs["framed"], "overhead": rs.get("overhead")}
-        del rs
-        torch.cuda.empty_cache()
-        dist.barrier()
-        if rank == 0:
-            r1 = run_config(A, D, torch, None, args, "streams", 0, 1, local, False,
-                            args.steps, args.warmup)
-            ent["n1_ms_per_step"] = round(r1["ms_per_step"], 4)
-            ent["n1_how"] = ("the same 1024 streams on rank 0's GPU alone in this job (eager: "
-                             "detector + framing, no gather)")
-            ent["scaling_vs_n1"] = round(r1["ms_per_step"] / ent["ms_per_step"], 3)
-            del r1
+        # the headline is already measured: a failure here (every rank runs the
+        # same code, so every rank raises alike) costs the entry, not the line
+        try:
+            # configs[4] over the N ranks (strong scaling), and the same workload on
+            # rank 0's GPU alone for scaling_vs_n1 (the other ranks wait)
+            for k in ("d_pcm", "d_sym", "d_mag", "d_true"):
+                r.pop(k, None)
             torch.cuda.empty_cache()
-        dist.barrier()
-        extras["streams"] = ent
+            args.graph = args.dist_backend == "nccl"
+            rs = run_config(A, D, torch, dist, args, "streams", rank, world, local, True,
+                            args.steps, args.warmup)
+            ent = {"workload": f"configs[4]: 1024 streams x 2048 windows sharded over {world} GPUs",
+                   "scaling": "strong", "value": round(rs["total_windows"] * 1024 /
+                                                       (rs["ms_per_step"] / 1e3) / 1e6, 1),
+                   "unit": "Msamples/s", "ms_per_step": round(rs["ms_per_step"], 4),
+                   "kernel_ms": round(rs["kernel_ms"], 4), "symbol_errors": rs["sym_err"],
+                   "framing": rs["framed"], "overhead": rs.get("overhead")}
+            del rs
+            torch.cuda.empty_cache()
+            dist.barrier()
+            if rank == 0:
+                r1 = run_config(A, D, torch, None, args, "streams", 0, 1, local, False,
+                                args.steps, args.warmup)
+                ent["n1_ms_per_step"] = round(r1["ms_per_step"], 4)
+                ent["n1_how"] = ("the same 1024 streams on rank 0's GPU alone in this job (eager: "
+                                 "detector + framing, no gather)")
+                ent["scaling_vs_n1"] = round(r1["ms_per_step"] / ent["ms_per_step"], 3)
+                del r1
+                torch.cuda.empty_cache()
+            dist.barrier()
+            extras["streams"] = ent
+        except Exception as e:  # noqa: BLE001 - reported in the line
+            extras["streams"] = {"error": f"{type(e).__name__}: {e}"[:800]}
 
     if rank == 0:
         samples = r["total_windows"] * r["n"]  # stream samples demodulated (each counted once)
@@ -882,6 +912,8 @@ def main():
             out["overhead"] = r["overhead"]
         if "rescue" in r:
             out["rescue"] = r["rescue"]
+        if "sustained" in r:
+            out["sustained"] = r["sustained"]
         if r["framed"]:
             out["framing"] = r["framed"]
         out.update(extras)
