@@ -236,7 +236,8 @@ def free_port() -> int:
 
 def run_config(A, D, torch, dist, args, config, rank, world, local, use_dist, steps, warmup,
                plan="survey", method_name="auto", hop_fft=256, no_mags=False, spectrum=False,
-               rescue_ab=False, parity_windows=0, n_streams_total=1024, sustain_s=0.0):
+               rescue_ab=False, parity_windows=0, n_streams_total=1024, sustain_s=0.0,
+               parity_every=0):
     """Allocate, synthesise, warm up and time one workload; returns a dict."""
     freqs = A.FSK8_FREQS if config == "fsk8" else A.FSK2_FREQS
     if config == "fsk8" and plan == "odd":
@@ -532,6 +533,14 @@ def run_config(A, D, torch, dist, args, config, rank, world, local, use_dist, st
                           "value": round(total_windows * n / (el / n_sus) / 1e6, 1),
                           "unit": "Msamples/s",
                           "how": "the timed step back to back, synchronised every 256 steps"}
+    # parity of the timed output itself, before the rescue A/B below reuses
+    # the magnitude buffer
+    if parity_every and rank == 0:
+        r["parity_all"] = parity_all(d_pcm, slots[(st["i"] - 1) % len(slots)], d_mag, freqs, n, hop,
+                                     config == "fft", every=parity_every)
+    if parity_windows and rank == 0:
+        r["parity_sample"] = parity_consecutive(A, d_pcm, slots[(st["i"] - 1) % len(slots)], d_mag,
+                                                freqs, n, hop, parity_windows, config == "fft")
     if rescue_ab and not use_dist:
         # the same step with the decision rescue switched off: its cost
         os.environ["FSKD_NO_RESCUE"] = "1"
@@ -572,9 +581,6 @@ def run_config(A, D, torch, dist, args, config, rank, world, local, use_dist, st
                        "how": "interleaved medians of 3 x %d steps each way" % steps}
         d0.close()
         del sl
-    if parity_windows and rank == 0:
-        r["parity_sample"] = parity_consecutive(A, d_pcm, slots[(st["i"] - 1) % len(slots)], d_mag,
-                                                freqs, n, hop, parity_windows, config == "fft")
     demod.close()
     return r
 
@@ -610,7 +616,7 @@ def parity_consecutive(A, d_pcm, d_sym, d_mag, freqs, n, hop, count, fft):
     out = {"windows_checked": int(W), "consecutive": True, "hop": hop,
            "oracle": "oracle_fft_demod (double radix-2)" if fft else "oracle_goertzel (double)",
            "symbol_mismatches": int((gs != sym).sum()),
-           "flag_bits_left": int((gs & 0x80).sum()),
+           "flag_bits_left": int(((gs & 0x80) != 0).sum()),
            "margin": margin_stats(P)}
     if d_mag is not None:
         gm = d_mag[:W].cpu().numpy().astype(np.float64)
@@ -625,6 +631,67 @@ def parity_consecutive(A, d_pcm, d_sym, d_mag, freqs, n, hop, count, fft):
     return out
 
 
+def parity_all(d_pcm, d_sym, d_mag, freqs, n, hop, fft, every=1, chunk=65536):
+    """GPU vs the oracle on every `every`-th window of the whole timed output
+    (every = 1: all of them), in chunks of `chunk` windows: symbol
+    mismatches, flag bits left, magnitude error relative to max_k P and the
+    count of windows above 1e-5 of max_k P."""
+    sys.path.insert(0, ROOT)
+    from oracle import oracle as O
+    _, _, _, threads, _ = cpu_share()
+    W = d_sym.numel()
+    flat = d_pcm.reshape(-1)
+    idx_all = np.arange(0, W, every)
+    mism = flags = above = 0
+    worst = 0.0
+    t0 = time.perf_counter()
+    for c0 in range(0, idx_all.size, chunk):
+        idx = idx_all[c0:c0 + chunk]
+        if every == 1:
+            a, b = int(idx[0]), int(idx[-1])
+            x = flat[a * hop:b * hop + n].cpu().numpy()
+            oh = hop
+        else:
+            # the sampled windows side by side, each its own n samples
+            starts = torch_index(flat, idx, hop, n)
+            x, oh = starts, n
+        if fft:
+            sym, P = O.fft_demod(x, freqs, n, oh, threads=threads)
+        else:
+            sym, P = O.goertzel(x, freqs, n, oh, threads=threads)
+        ii = torch_like(d_sym, idx)
+        gs = d_sym[ii].cpu().numpy()
+        mism += int((gs != sym).sum())
+        flags += int(((gs & 0x80) != 0).sum())
+        if d_mag is not None:
+            gm = d_mag[ii].cpu().numpy().astype(np.float64)
+            rel = np.abs(gm - P).max(1) / np.maximum(P.max(1), 1e-300)
+            worst = max(worst, float(rel.max()))
+            above += int((rel > 1e-5).sum())
+    out = {"windows_checked": int(idx_all.size), "of_windows": int(W),
+           "sample": "every window" if every == 1 else f"every {every}th window",
+           "oracle": "oracle_fft_demod (double radix-2)" if fft else "oracle_goertzel (double)",
+           "symbol_mismatches": mism, "flag_bits_left": flags,
+           "oracle_seconds": round(time.perf_counter() - t0, 2), "threads": threads}
+    if d_mag is not None:
+        out["max_rel_mag_err"] = worst
+        out["windows_above_1e-5_of_max_P"] = above
+    return out
+
+
+def torch_like(t, idx):
+    import torch
+    return torch.as_tensor(idx, device=t.device)
+
+
+def torch_index(flat, idx, hop, n):
+    """The n samples of each window in idx, gathered on the device, as one
+    contiguous host array (window after window)."""
+    import torch
+    off = torch.as_tensor(idx, device=flat.device)[:, None] * hop + torch.arange(n, device=flat.device)
+    return flat[off.reshape(-1)].cpu().numpy()
+
+
 def summary(r) -> dict:
     """The extra-config entry of the bench line."""
     out = {"workload": (f"configs[2]: 8-FSK Goertzel, {r['W']} x 1024 windows" if r["config"] == "fsk8"
@@ -637,7 +704,7 @@ def summary(r) -> dict:
            "value": round(r["W"] * 1024 / (r["ms_per_step"] / 1e3) / 1e6, 1), "unit": "Msamples/s",
            "symbol_errors": r["sym_err"],
            "launches_per_step": r["roofline"]["launches_per_step"]}
-    for key in ("rescue", "parity_sample"):
+    for key in ("rescue", "parity_sample", "parity_all"):
         if key in r:
             out[key] = r[key]
     if r["config"] == "fft":
@@ -803,7 +870,9 @@ def main():
                    args.steps, args.warmup, plan=args.plan, method_name=args.method,
                    hop_fft=args.hop, no_mags=args.no_mags, spectrum=args.spectrum,
                    rescue_ab=plain and args.config in ("fsk2", "fsk8", "fft"),
-                   sustain_s=args.sustain if plain and args.config == "fsk2" and not args.no_extras else 0.0)
+                   sustain_s=args.sustain if plain and args.config == "fsk2" and not args.no_extras else 0.0,
+                   parity_every=(1 if args.config in ("fsk2", "fsk8") else 64)
+                   if plain and not args.no_cpu_baseline else 0)
 
     extras = {}
     if plain and args.config == "fsk2" and not args.no_extras:
@@ -815,7 +884,8 @@ def main():
             rr = run_config(A, D, torch, dist, args, cfgname, rank, world, local, False,
                             args.steps, args.warmup, hop_fft=256, spectrum=spec,
                             rescue_ab=not spec,
-                            parity_windows=16384 if (cfgname == "fft" and not spec) else 0)
+                            parity_windows=16384 if (cfgname == "fft" and not spec) else 0,
+                            parity_every=0 if spec or args.no_cpu_baseline else (1 if cfgname == "fsk8" else 64))
             extras[key] = summary(rr)
             del rr
             torch.cuda.empty_cache()
@@ -914,6 +984,8 @@ def main():
             out["rescue"] = r["rescue"]
         if "sustained" in r:
             out["sustained"] = r["sustained"]
+        if "parity_all" in r:
+            out["parity_all"] = r["parity_all"]
         if r["framed"]:
             out["framing"] = r["framed"]
         out.update(extras)

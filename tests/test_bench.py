@@ -118,3 +118,32 @@ def test_gpus_n_self_launches_torchrun(monkeypatch):
     assert cmd[1:3] == ["-m", "torch.distributed.run"]
     assert "--nproc-per-node=2" in cmd and "--master-addr=127.0.0.1" in cmd
     assert cmd[-4:] == ["--gpus", "2", "--steps", "3"]
+
+
+def test_parity_all_counts_against_the_oracle():
+    """bench.parity_all (CPU tensors standing in for device ones): the oracle's
+    own output checks clean, a changed symbol, a leftover flag bit and a
+    perturbed power are each counted; the strided sample reads the right
+    windows."""
+    import torch
+    from oracle import oracle as O
+    f = (1500.0, 3000.0)
+    pcm, _ = O.synth_fsk(f, 1024, 96, 11, 8000, 400)
+    sym, P = O.goertzel(pcm, f, 1024)
+    d_pcm = torch.from_numpy(pcm.copy())
+    mag = torch.from_numpy(P.astype(np.float32))
+    out = bench.parity_all(d_pcm, torch.from_numpy(sym.copy()), mag, f, 1024, 1024, False, chunk=40)
+    assert out["windows_checked"] == 96 and out["symbol_mismatches"] == 0
+    assert out["flag_bits_left"] == 0 and out["windows_above_1e-5_of_max_P"] == 0
+    bad = sym.copy()
+    bad[5] ^= 1
+    bad[70] |= 0x80
+    mag[33, int(np.argmax(P[33]))] *= 1.001
+    out = bench.parity_all(d_pcm, torch.from_numpy(bad), mag, f, 1024, 1024, False, chunk=40)
+    assert out["symbol_mismatches"] == 2 and out["flag_bits_left"] == 1
+    assert out["windows_above_1e-5_of_max_P"] == 1
+    flat = pcm.reshape(-1)
+    s2, P2 = O.fft_demod(flat, f, 1024, 256)
+    out = bench.parity_all(torch.from_numpy(flat.copy()), torch.from_numpy(s2.copy()),
+                           torch.from_numpy(P2.astype(np.float32)), f, 1024, 256, True, every=9, chunk=7)
+    assert out["windows_checked"] == len(range(0, s2.size, 9)) and out["symbol_mismatches"] == 0
