@@ -42,8 +42,9 @@ __device__ __forceinline__ long long tile_block_swz()
 
 // R: read the group's input; W: 0 no writes, 1 nt stores, 2 plain stores,
 // 3 buffer stores with cache-policy bits AUX; RUN: each wave takes a
-// contiguous run of groups instead of every stride-th
-template <bool R, int W, int AUX = 0, bool RUN = false>
+// contiguous run of groups instead of every stride-th; RAUX: the loads'
+// cache-policy bits
+template <bool R, int W, int AUX = 0, bool RUN = false, int RAUX = 0>
 __global__ __launch_bounds__(256) void mem_kernel(const short *pcm, long long n_windows, long long hop,
                                                   float *spec, unsigned *sink)
 {
@@ -69,7 +70,7 @@ __global__ __launch_bounds__(256) void mem_kernel(const short *pcm, long long n_
             const int voff = (int)(wq * hop * 2) + 4 * t;
             unsigned nx[32];
 #pragma unroll
-            for (int n1 = 0; n1 < 32; ++n1) nx[n1] = __builtin_amdgcn_raw_buffer_load_b32(rs, voff + 64 * n1, 0, 0);
+            for (int n1 = 0; n1 < 32; ++n1) nx[n1] = __builtin_amdgcn_raw_buffer_load_b32(rs, voff + 64 * n1, 0, RAUX);
 #pragma unroll
             for (int n1 = 0; n1 < 32; ++n1) acc += nx[n1] * (unsigned)(2 * n1 + 1);
         }
@@ -142,6 +143,12 @@ int main(int argc, char **argv)
         {"w only nt, runs per wave", mem_kernel<false, 1, 0, true>, {}},
         {"w only plain, runs per wave", mem_kernel<false, 2, 0, true>, {}},
         {"r+w plain, runs per wave", mem_kernel<true, 2, 0, true>, {}},
+        {"r(nt)+w nt", mem_kernel<true, 1, 0, false, 2>, {}},
+        {"r(nt)+w plain", mem_kernel<true, 2, 0, false, 2>, {}},
+        {"r(sc0)+w nt", mem_kernel<true, 1, 0, false, 1>, {}},
+        {"r(nt)+w nt, runs per wave", mem_kernel<true, 1, 0, true, 2>, {}},
+        {"r(nt)+w plain, runs per wave", mem_kernel<true, 2, 0, true, 2>, {}},
+        {"r(sc0 nt)+w nt", mem_kernel<true, 1, 0, false, 3>, {}},
     };
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
