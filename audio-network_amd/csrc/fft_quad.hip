@@ -1137,7 +1137,8 @@ __device__ __attribute__((always_inline)) inline void fft1024_quad_body(const Ff
 
     // 6. decision rescue (rescue_fft.h), after the group loop
     //    (no code inside it, whose registers stay as they were): the symbol
-    //    bytes of the groups are read back (one byte per window) and every
+    //    bytes of the groups are read back (one byte per window, plain loads:
+    //    the bytes were written by this wave or its block) and every
     //    flagged window is decided again in double, one window per wave at a
     //    time through the wave's slab.
     //    RSC 1: each wave its own groups' windows.
@@ -1155,16 +1156,17 @@ __device__ __attribute__((always_inline)) inline void fft1024_quad_body(const Ff
 #pragma unroll
             for (int q0 = 0; q0 < 4; ++q0) {
                 const long long ww = 4 * gl + q0;
-                if (ww < p.n_windows &&
-                    (__hip_atomic_load(p.sym + ww, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & kSymAmbiguous))
-                    f |= 1u << q0;
+                if (ww < p.n_windows && (p.sym[ww] & kSymAmbiguous)) f |= 1u << q0;
             }
         }
         return f;
     };
     if constexpr (RSC == 1) {
         if (p.rescue) {
-            __builtin_amdgcn_s_waitcnt(0);  // this wave's symbol stores have landed
+            // this wave's symbol stores have landed (in this XCD's L2, where
+            // the plain loads below find them) and are ordered before the loads
+            __builtin_amdgcn_s_waitcnt(0);
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
             lds_double *xs = (lds_double *)(slab[wave]);
             for (long long gb = g_first; gb < n_groups; gb += 64 * stride) {
                 const unsigned f = flags4(gb + (long long)lane * stride);
@@ -1182,7 +1184,7 @@ __device__ __attribute__((always_inline)) inline void fft1024_quad_body(const Ff
     } else if constexpr (RSC == 2) {
         if (p.rescue) {
             __builtin_amdgcn_s_waitcnt(0);  // this wave's symbol stores have landed
-            __syncthreads();                // ... and every wave's of the block
+            __syncthreads();                // ... and every wave's of the block (a workgroup fence)
             lds_double *xs = (lds_double *)(slab[wave]);
             int seen = 0;                   // flagged windows dealt so far (wave-uniform)
             for (long long gb0 = g_first - wave; gb0 < n_groups; gb0 += 64 * stride) {

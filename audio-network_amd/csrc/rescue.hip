@@ -40,7 +40,9 @@ __global__ __launch_bounds__(64) void rescue_kernel(RescueParams p)
     __shared__ __attribute__((aligned(16))) unsigned char smp[kRescueLdsBytes];
     __shared__ double pd[64];
     const int lane = threadIdx.x;
-    const long long base = (long long)blockIdx.x * kRescueChunk;
+    // the chunk the detector's XCD-swizzled tiles wrote from this block's XCD
+    // (tile_block): its symbol lines are still in this XCD's L2
+    const long long base = tile_block(1) * kRescueChunk;
     const int span = (int)min((long long)kRescueChunk, p.n_windows - base);
 
     // 1. any flagged window in the chunk? (buffer loads bounded by the

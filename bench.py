@@ -825,6 +825,8 @@ def main():
     ap.add_argument("--no-extras", action="store_true",
                     help="skip the extra entries (fsk8, fft_hop256*, streams, host_e2e at N = 1; "
                          "streams at N > 1)")
+    ap.add_argument("--no-rescue-ab", action="store_true",
+                    help="skip the rescue-off A/B runs (profiling: only the shipped path launches)")
     ap.add_argument("--sustain", type=float, default=6.0,
                     help="N = 1 headline: also run the step back to back for this many seconds "
                          "and report the rate as 'sustained' (0: off)")
@@ -869,7 +871,7 @@ def main():
     r = run_config(A, D, torch, dist, args, args.config, rank, world, local, use_dist,
                    args.steps, args.warmup, plan=args.plan, method_name=args.method,
                    hop_fft=args.hop, no_mags=args.no_mags, spectrum=args.spectrum,
-                   rescue_ab=plain and args.config in ("fsk2", "fsk8", "fft"),
+                   rescue_ab=plain and args.config in ("fsk2", "fsk8", "fft") and not args.no_rescue_ab,
                    sustain_s=args.sustain if plain and args.config == "fsk2" and not args.no_extras else 0.0,
                    parity_every=(1 if args.config in ("fsk2", "fsk8") else 64)
                    if plain and not args.no_cpu_baseline else 0)
@@ -883,7 +885,7 @@ def main():
                                    ("fft_hop256_spectrum", "fft", True)):
             rr = run_config(A, D, torch, dist, args, cfgname, rank, world, local, False,
                             args.steps, args.warmup, hop_fft=256, spectrum=spec,
-                            rescue_ab=not spec,
+                            rescue_ab=not spec and not args.no_rescue_ab,
                             parity_windows=16384 if (cfgname == "fft" and not spec) else 0,
                             parity_every=0 if spec or args.no_cpu_baseline else (1 if cfgname == "fsk8" else 64))
             extras[key] = summary(rr)
