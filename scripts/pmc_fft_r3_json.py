@@ -41,6 +41,8 @@ def main(tag="r3close"):
     W, hop, n = 1 << 20, 256, 1024
     Wev = (W * n - n) // hop + 1
     for cfg, spec in (("fft", False), ("fftspec", True)):
+        if not os.path.exists(os.path.join(src, f"pmc_{cfg}_FETCH_SIZE")):
+            continue
         got = {}
         for c in ("FETCH_SIZE", "WRITE_SIZE"):
             path = os.path.join(src, f"pmc_{cfg}_{c}", "run_counter_collection.csv")
@@ -59,7 +61,7 @@ def main(tag="r3close"):
                "method": ("rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate runs of "
                           "bench.py --config fft" + (" --spectrum" if spec else "") +
                           " --no-cpu-baseline --no-rescue-ab --warmup 2 --steps 5 "
-                          "(scripts/gpu_r3_close.sh); bytes = KB*1024, FETCH doubled per "
+                          "(scripts/gpu_r3_close.sh, gpu_r3_o.sh); bytes = KB*1024, FETCH doubled per "
                           "MI355X_MICROARCH.md §HBM; round 3: the decision rescue inside the kernel"),
                "source": f"profiles/round3/{tag}/pmc_{cfg}_FETCH_SIZE.csv, pmc_{cfg}_WRITE_SIZE.csv"}
         with open(os.path.join(ROOT, "profiles", f"pmc_{cfg}.json"), "w") as fh:
