@@ -1,5 +1,6 @@
 """configs[0]: the native host C test (tests/native/config1.c) — one 1024-sample
 2-FSK buffer through the oracle, the C ABI and the frame codec."""
+import fcntl
 import os
 import subprocess
 
@@ -9,8 +10,15 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 NATIVE = os.path.join(HERE, "native")
 
 
+def _make(*targets):
+    """make under an exclusive lock: xdist workers share tests/native/."""
+    with open(os.path.join(NATIVE, ".make.lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        subprocess.run(["make", "-C", NATIVE, "-s", *targets], check=True, capture_output=True)
+
+
 def _build_and_run():
-    subprocess.run(["make", "-C", NATIVE, "-s"], check=True, capture_output=True)
+    _make()
     return subprocess.run([os.path.join(NATIVE, "config1")], capture_output=True, text=True,
                           timeout=120)
 
@@ -36,7 +44,7 @@ def test_wire_codecs_under_sanitizers(seed):
     fuzzed on exact-size buffers (tests/native/fuzz_wire.c): round trips at
     every payload size, truncations, mutations, random bytes; any read past
     an input or undefined behaviour aborts the run."""
-    subprocess.run(["make", "-C", NATIVE, "-s", "fuzz_wire"], check=True, capture_output=True)
+    _make("fuzz_wire")
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1",
                UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1")
     r = subprocess.run([os.path.join(NATIVE, "fuzz_wire"), "200000", str(seed)],
