@@ -50,7 +50,7 @@ __device__ __forceinline__ float group_sum_f(float v, int log2g)
 // epilogue. F16: c16 / r hold this lane's four slots (fold_tile_kernel F16).
 // fold_tile_kernel and fold_slide_kernel both end here, so a window's result
 // does not depend on which of them formed its sums.
-template <int K, bool F16>
+template <int K, bool F16, int MST = -1>
 __device__ __forceinline__ void fold_decide(const int (&acc)[8], const float4 *r,
                                             const float (&c16)[4], int lane, long long w,
                                             bool live, const GoertzelParams &p)
@@ -87,7 +87,7 @@ __device__ __forceinline__ void fold_decide(const int (&acc)[8], const float4 *r
             xr[2 * h + 1] = X1.x;
             xi[2 * h + 1] = X1.y;
         }
-        window_sum_decide_split8<true>(xr, xi, lane, w, live, p.sym, p.mag, p.perm, p.amb_tq,
+        window_sum_decide_split8<true, MST>(xr, xi, lane, w, live, p.sym, p.mag, p.perm, p.amb_tq,
                                        p.amb_floor);
     } else {
         float xr[K], xi[K];
@@ -118,7 +118,7 @@ __device__ __forceinline__ void fold_decide(const int (&acc)[8], const float4 *r
             xr[K - 1] = r[K - 1].x * s1 - r[K - 1].z * s2;
             xi[K - 1] = r[K - 1].y * s1 - r[K - 1].w * s2;
         }
-        window_sum_decide<K>(xr, xi, lane, w, live, p.sym, p.mag, 0, p.amb_tq, p.amb_floor);
+        window_sum_decide<K, false, MST>(xr, xi, lane, w, live, p.sym, p.mag, 0, p.amb_tq, p.amb_floor);
     }
 }
 
@@ -144,7 +144,7 @@ __device__ __forceinline__ void fold_decide(const int (&acc)[8], const float4 *r
 //       rotations per lane, and the first reduce-scatter stage is already done
 //       (window_sum_decide_split8; perm maps slots back to the caller's tones).
 template <int K, int LOG2G, bool NT = true, int WPB = 4, bool ROTLDS = false, bool NTS = false,
-          bool WS = false, bool PK = false, bool LDST = false, bool F16 = false>
+          bool WS = false, bool PK = false, bool LDST = false, bool F16 = false, int MST = -1>
 __global__ __launch_bounds__(64 * WPB) void fold_tile_kernel(GoertzelParams p)
 {
     const int lane = threadIdx.x & 63;
@@ -227,7 +227,7 @@ __global__ __launch_bounds__(64 * WPB) void fold_tile_kernel(GoertzelParams p)
         }
         if constexpr (F16 || (WS && LOG2G == 4 && !PK && !ROTLDS)) {
             const long long w = wbase + win_in_tile;
-            fold_decide<K, F16>(acc, r, c16, lane, w, w < p.n_windows, p);
+            fold_decide<K, F16, MST>(acc, r, c16, lane, w, w < p.n_windows, p);
             continue;
         }
         float xf[8];
@@ -272,7 +272,7 @@ __global__ __launch_bounds__(64 * WPB) void fold_tile_kernel(GoertzelParams p)
                 xi[k] = rk.y * t1[k] - rk.w * t2[k];
             }
             const long long w = wbase + win_in_tile;
-            window_sum_decide<K>(xr, xi, lane, w, w < p.n_windows, p.sym, p.mag, 0, p.amb_tq,
+            window_sum_decide<K, false, MST>(xr, xi, lane, w, w < p.n_windows, p.sym, p.mag, 0, p.amb_tq,
                                  p.amb_floor);
             continue;
         }

@@ -28,6 +28,30 @@
 
 namespace fskd {
 
+// Magnitude store policy. 0 plain, 1 non-temporal, 2 + a: raw buffer store
+// with cache-policy bits a (probe only, 32-bit offsets). The default (-1,
+// kMagStore<K>) is plain for every K. Non-temporal stores at K = 8 (a wave's
+// 4 windows fill one whole 128-byte line) measured box-dependent against the
+// shipped plain stores in 4 launch slices (demod_api.cpp launch_slice): one
+// launch 310 vs 327 us on one box, 331 vs 324 us on the next, the
+// no-magnitude floor 307 / 298 us (scripts/mag_probe.hip,
+// profiles/round3/r3q/, r3r/); no policy was better on both.
+template <int K>
+constexpr int kMagStore = 0;
+
+template <int MST>
+__device__ __forceinline__ void mag_store(float *mag, long long idx, float v)
+{
+    if constexpr (MST == 0) {
+        mag[idx] = v;
+    } else if constexpr (MST == 1) {
+        __builtin_nontemporal_store(v, mag + idx);
+    } else {
+        __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(mag, (short)0, 0x7FFFFFF0, 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rs, (int)(4 * idx), 0, MST - 2);
+    }
+}
+
 template <int CTRL>
 __device__ __forceinline__ float ws_dpp(float v)
 {
@@ -154,7 +178,7 @@ __device__ __forceinline__ bool ws_ambiguous(float mx, float a0, bool ok0, float
 // (residue.hip DCLS); magnitudes, the tie rule and the symbol use that index.
 // tq / fl: the decision rescue's ambiguity test (tq = 0: off); an ambiguous
 // window's symbol carries kSymAmbiguous for rescue_kernel.
-template <int K, bool PERM = false>
+template <int K, bool PERM = false, int MST = -1>
 __device__ __forceinline__ void window_sum_decide(const float (&re)[K], const float (&im)[K],
                                                   int lane, long long w, bool live,
                                                   uint8_t *sym, float *mag,
@@ -190,9 +214,10 @@ __device__ __forceinline__ void window_sum_decide(const float (&re)[K], const fl
     const bool ok1 = V > 16 && re_lane && t0 + 8 < K;
     const int o0 = PERM ? (int)((perm >> (4 * t0)) & 15u) : t0;
     const int o1 = PERM ? (int)((perm >> (4 * ((t0 + 8) & 15))) & 15u) : t0 + 8;
+    constexpr int MS = MST >= 0 ? MST : kMagStore<K>;
     if (live && mag) {
-        if (ok0) mag[w * K + o0] = P0;
-        if (ok1) mag[w * K + o1] = P1;
+        if (ok0) mag_store<MS>(mag, w * K + o0, P0);
+        if (ok1) mag_store<MS>(mag, w * K + o1, P1);
     }
     float mx;
     const unsigned arg = ws_argmax_m<(V > 16)>(__float_as_uint(P0), ok0, o0, __float_as_uint(P1),
@@ -206,7 +231,7 @@ __device__ __forceinline__ void window_sum_decide(const float (&re)[K], const fl
 // tones 4-7, each over the whole window): that is the state after the first
 // reduce-scatter stage, so only stages 2, 1, 0 run (21 instead of 45
 // instructions). re/im = this lane's 4 tones (slots 4 * bit3 + s).
-template <bool PERM = false>
+template <bool PERM = false, int MST = -1>
 __device__ __forceinline__ void window_sum_decide_split8(const float (&re)[4], const float (&im)[4],
                                                          int lane, long long w, bool live,
                                                          uint8_t *sym, float *mag,
@@ -229,7 +254,8 @@ __device__ __forceinline__ void window_sum_decide_split8(const float (&re)[4], c
     const float sq = v[0] * v[0];
     const float P0 = sq + ws_dpp<0xB1>(sq);
     const int o0 = PERM ? (int)((perm >> (4 * t0)) & 15u) : t0;
-    if (live && mag && re_lane) mag[w * K + o0] = P0;
+    constexpr int MS = MST >= 0 ? MST : kMagStore<K>;
+    if (live && mag && re_lane) mag_store<MS>(mag, w * K + o0, P0);
     float mx;
     const unsigned arg = ws_argmax_m<false>(__float_as_uint(P0), re_lane, o0, 0u, false, 0, mx);
     const bool amb = ws_ambiguous(mx, P0, re_lane, 0.f, false, tq, fl);
