@@ -700,6 +700,11 @@ constexpr int kFmtWord3 = 0xFAC | (3 << 12) | (5 << 15);
 // from the registers of the lanes that hold them (p.slot, a wave-uniform
 // index: s_set_gpr_idx) instead of going through the 2 KiB per-window power
 // slab in LDS; true = the slab, for the full-spectrum store.
+// PICK (SPEC false): 0 = each lane keeps the best and second tone it owns
+// (per tone: a compare chain, selects and an exec-masked magnitude store),
+// then the row argmax; 1 = tone i's power is gathered into lane i of its row
+// by one ds_bpermute, so lanes t < K hold tone t like the slab pick leaves
+// them (4 VALU per tone instead of ~27, one coalesced magnitude store).
 // AUX: the loads' cache-policy bits (2 = nt, 1 = sc0, 0 = plain; launch_fft_quad).
 // FUSED: 1 = each DFT-4's two butterfly stages as one asm block
 // (dft4_fused_v / _k), 2 = also the post-pass pairs (postpair2), 3 = also
@@ -728,7 +733,7 @@ constexpr int kFmtWord3 = 0xFAC | (3 << 12) | (5 << 15);
 // compile-time W32^j — one packed complex product (29 VALU per group) in
 // place of 8 ds_read2_b64.
 template <int WPB = 4, int MINW = 4, int PF = 0, bool SPEC = true, bool FMT = false, int AUX = 2,
-          int FUSED = 0, int RD = 0, int SPL = 0, int OVL = 0, int TW3R = 0, int RSC = 1>
+          int FUSED = 0, int RD = 0, int SPL = 0, int OVL = 0, int TW3R = 0, int RSC = 1, int PICK = 0>
 __device__ __attribute__((always_inline)) inline void fft1024_quad_body(const FftParams &p)
 {
     static_assert(!OVL || (FUSED >= 4 && PF != 1), "OVL: the FUSED 4 column DFT-16");
@@ -777,6 +782,7 @@ __device__ __attribute__((always_inline)) inline void fft1024_quad_body(const Ff
         tb_lo = 0.5f * t1024[t == 0 ? 16 : t];
         tb_hi = 0.5f * t1024[t];
     }
+    const int rowaddr = (lane & 48) * 4;  // byte address of this window row's lane 0 (ds_bpermute)
     __syncthreads();
 
     const long long n_groups = (p.n_windows + 3) >> 2;
@@ -1066,6 +1072,24 @@ __device__ __attribute__((always_inline)) inline void fft1024_quad_body(const Ff
             // SPL: the fenced lane id again, so the store address is formed
             // here rather than held across the loop
             if (live && t < p.k && p.mag) p.mag[w * p.k + (SPL ? tt : t)] = pk;
+        } else if constexpr (PICK == 1) {
+            // 5. tone pick, gathered: tone i's power (register slot and lane
+            //    from its uniform slot, as below) is read across the row with
+            //    one ds_bpermute into lane t = i, so lanes t < K end holding
+            //    tone t's power, as the slab pick of the spectrum path leaves
+            //    them: one coalesced magnitude store and the same row argmax
+            float mine = -1.f;
+#pragma nounroll
+            for (int i = 0; i < p.k; ++i) {
+                const int f = p.slot[i];
+                const float v = f >= 512 ? (f == 512 ? px.x : px.y) : pv[((f >> 5) << 1) | (f & 1)];
+                const int src = f >= 512 ? 0 : ((f >> 1) & 15);
+                const float got = __int_as_float(
+                    __builtin_amdgcn_ds_bpermute(rowaddr + 4 * src, __float_as_int(v)));
+                mine = t == i ? got : mine;
+            }
+            pk = mine;
+            if (live && t < p.k && p.mag) p.mag[w * p.k + t] = pk;
         } else {
             // 5. tone pick from registers: tone i's power sits in lane
             //    (slot >> 1) & 15 of each window row at pv[slot >> 5 | half]
@@ -1213,11 +1237,11 @@ __device__ __attribute__((always_inline)) inline void fft1024_quad_body(const Ff
 }
 
 template <int WPB = 4, int MINW = 4, int PF = 0, bool SPEC = true, bool FMT = false, int AUX = 2,
-          int FUSED = 0, int SPL = 0, int OVL = 0, int TW3R = 0, int RSC = 1>
+          int FUSED = 0, int SPL = 0, int OVL = 0, int TW3R = 0, int RSC = 1, int PICK = 0>
 __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MINW > 0 ? MINW : 1)))
 void fft1024_quad_kernel(FftParams p)
 {
-    fft1024_quad_body<WPB, MINW, PF, SPEC, FMT, AUX, FUSED, 0, SPL, OVL, TW3R, RSC>(p);
+    fft1024_quad_body<WPB, MINW, PF, SPEC, FMT, AUX, FUSED, 0, SPL, OVL, TW3R, RSC, PICK>(p);
 }
 
 // (a device-code attribute: the host pass of hipcc does not know the feature)
@@ -1242,7 +1266,7 @@ FSKD_NO_LDS_PAIRING void fft1024_quad_kernel_r64(FftParams p)
 // Persistent grid: as many blocks as fit the chip, each wave strides over
 // groups of 4 windows (the LDS twiddle tables are built once per block).
 template <int WPB, int MINW, int PF, bool SPEC, bool FMT = false, int AUX = 2, int FUSED = 0, int RD = 0,
-          int SPL = 0, int OVL = 0, int TW3R = 0, int RSC = 1>
+          int SPL = 0, int OVL = 0, int TW3R = 0, int RSC = 1, int PICK = 0>
 hipError_t launch_fft_quad_t(const FftParams &p, hipStream_t s)
 {
     void (*kern)(FftParams);
@@ -1250,7 +1274,7 @@ hipError_t launch_fft_quad_t(const FftParams &p, hipStream_t s)
     if constexpr (RD > 0)
         kern = fft1024_quad_kernel_r64<WPB, MINW, PF, SPEC, FMT, AUX, FUSED, RD>;
     else
-        kern = fft1024_quad_kernel<WPB, MINW, PF, SPEC, FMT, AUX, FUSED, SPL, OVL, TW3R, RSC>;
+        kern = fft1024_quad_kernel<WPB, MINW, PF, SPEC, FMT, AUX, FUSED, SPL, OVL, TW3R, RSC, PICK>;
     int dev = 0, cus = 256, per_cu = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
@@ -1282,16 +1306,19 @@ hipError_t launch_fft_quad_t(const FftParams &p, hipStream_t s)
 // 2.73 ms; a write-only fill of the same buffer 1.45 ms, the detector
 // without the spectrum 1.71-1.80 ms (scripts/spectrum_probe.py,
 // profiles/round2/spec_lin/).
+// Tones only: the gathered tone pick (PICK 1), -1.8 % at hop 256 and -1.7 %
+// at hop 1024 against the per-lane register pick, identical outputs
+// (profiles/round3/r3s/).
 hipError_t launch_fft_quad(const FftParams &p, hipStream_t s)
 {
     const bool lin = p.spec && ((uintptr_t)p.spec & 15) == 0;
     if (p.hop < 1024)
         return lin ? launch_fft_quad_t<4, 4, 0, true, false, 0, 4, 0, 2>(p, s)
              : p.spec ? launch_fft_quad_t<4, 4, 0, true, false, 0, 4>(p, s)
-                      : launch_fft_quad_t<4, 4, 0, false, false, 0, 4>(p, s);
+                      : launch_fft_quad_t<4, 4, 0, false, false, 0, 4, 0, 0, 0, 0, 1, 1>(p, s);
     return lin ? launch_fft_quad_t<4, 4, 0, true, false, 2, 4, 0, 2>(p, s)
          : p.spec ? launch_fft_quad_t<4, 4, 0, true, false, 2, 4>(p, s)
-                  : launch_fft_quad_t<4, 4, 0, false, false, 2, 4>(p, s);
+                  : launch_fft_quad_t<4, 4, 0, false, false, 2, 4, 0, 0, 0, 0, 1, 1>(p, s);
 }
 
 int fft_quad_slot(int bin) { return quad_slot(bin); }

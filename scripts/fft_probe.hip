@@ -185,6 +185,16 @@ int main(int argc, char **argv)
     vs.push_back({"rsc2 per-block rescue", [=](const FftParams &p, hipStream_t s) {
         FftParams q = p; q.amb_tq = amb_tq; q.amb_floor = amb_floor; q.rescue = 1; q.rtw = d_rtw;
         return launch_rsc<2>(q, s); }, {}});
+    // round 3, late: the tone pick gathered by ds_bpermute (PICK 1) instead of
+    // the per-tone register pick with per-lane best tracking
+    vs.push_back({"pick: shipped", [](const FftParams &p, hipStream_t s) { return launch_fft_quad(p, s); }, {}});
+    vs.push_back({"pick: PICK1", [](const FftParams &p, hipStream_t s) {
+        if (p.spec) return launch_fft_quad(p, s);
+        return p.hop < 1024 ? launch_fft_quad_t<4, 4, 0, false, false, 0, 4, 0, 0, 0, 0, 1, 1>(p, s)
+                            : launch_fft_quad_t<4, 4, 0, false, false, 2, 4, 0, 0, 0, 0, 1, 1>(p, s); }, {}});
+    // (round 3, late: lane 0's post-pass pairing through 32 exec-masked LDS
+    // instructions instead of 32 v_cndmask, "l0: L0": -32 VALU per group but
+    // +2.2 % at hop 256, +1.1 % at hop 1024, profiles/round3/r3t/; removed)
     if (filter) {
         std::vector<Var> keep;
         for (size_t i = 0; i < vs.size(); ++i)
