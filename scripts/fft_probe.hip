@@ -195,6 +195,10 @@ int main(int argc, char **argv)
     // (round 3, late: lane 0's post-pass pairing through 32 exec-masked LDS
     // instructions instead of 32 v_cndmask, "l0: L0": -32 VALU per group but
     // +2.2 % at hop 256, +1.1 % at hop 1024, profiles/round3/r3t/; removed)
+    // (round 3, late: the input as one wide read of the group's span staged
+    // through the slab with a bank skew, "wl: WL": identical outputs but +4 %
+    // at hop 256 with the spectrum, +4 % tones only, +2.7 % at hop 512 with
+    // the spectrum, profiles/round3/r3w/; removed)
     if (filter) {
         std::vector<Var> keep;
         for (size_t i = 0; i < vs.size(); ++i)

@@ -31,6 +31,7 @@
     } while (0)
 
 typedef float f4 __attribute__((ext_vector_type(4)));
+typedef unsigned u4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ long long tile_block_swz()
 {
@@ -44,7 +45,7 @@ __device__ __forceinline__ long long tile_block_swz()
 // 3 buffer stores with cache-policy bits AUX; RUN: each wave takes a
 // contiguous run of groups instead of every stride-th; RAUX: the loads'
 // cache-policy bits
-template <bool R, int W, int AUX = 0, bool RUN = false, int RAUX = 0>
+template <bool R, int W, int AUX = 0, bool RUN = false, int RAUX = 0, bool WIDE = false>
 __global__ __launch_bounds__(256) void mem_kernel(const short *pcm, long long n_windows, long long hop,
                                                   float *spec, unsigned *sink)
 {
@@ -59,7 +60,21 @@ __global__ __launch_bounds__(256) void mem_kernel(const short *pcm, long long n_
     const long long g_end = RUN ? (g_begin + per < n_groups ? g_begin + per : n_groups) : n_groups;
     unsigned acc = 0;
     for (long long g = g_begin; g < g_end; g += stride) {
-        if constexpr (R) {
+        if constexpr (R && WIDE) {
+            // the group's 4 windows as one contiguous span (3 hops + 1024
+            // samples), 16 B per lane: 4 wide loads per lane instead of 32 dwords
+            const long long w0 = 4 * g;
+            const long long left = n_windows - w0;
+            long long bytes = (((left < 4 ? left : 4) - 1) * hop + 1024) * 2;
+            __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                (void *)(pcm + w0 * hop), (short)0, (int)bytes, 0x00020000);
+            u4 v[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * (64 * i + lane), 0, RAUX);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) acc += (v[i].x ^ v[i].y ^ v[i].z ^ v[i].w) * (unsigned)(2 * i + 1);
+        }
+        if constexpr (R && !WIDE) {
             const long long w0 = 4 * g;
             const long long left = n_windows - w0;
             const long long wq = q < left ? q : left - 1;
@@ -149,6 +164,12 @@ int main(int argc, char **argv)
         {"r(nt)+w nt, runs per wave", mem_kernel<true, 1, 0, true, 2>, {}},
         {"r(nt)+w plain, runs per wave", mem_kernel<true, 2, 0, true, 2>, {}},
         {"r(sc0 nt)+w nt", mem_kernel<true, 1, 0, false, 3>, {}},
+        // round 3, late: the group's span in 4 x 16 B per lane (each byte once per group)
+        {"read only wide", mem_kernel<true, 0, 0, false, 0, true>, {}},
+        {"r wide + w nt", mem_kernel<true, 1, 0, false, 0, true>, {}},
+        {"r wide + w plain", mem_kernel<true, 2, 0, false, 0, true>, {}},
+        {"r wide(nt) + w nt", mem_kernel<true, 1, 0, false, 2, true>, {}},
+        {"r wide + w nt, runs per wave", mem_kernel<true, 1, 0, true, 0, true>, {}},
     };
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
@@ -174,7 +195,7 @@ int main(int argc, char **argv)
         std::sort(m.begin(), m.end());
         const double med = m[m.size() / 2];
         const bool R = v.name[0] == 'r';
-        const bool Wr = v.kern != mem_kernel<true, 0>;
+        const bool Wr = v.kern != mem_kernel<true, 0> && v.kern != mem_kernel<true, 0, 0, false, 0, true>;
         const double bytes = (R ? rd : 0) + (Wr ? wr : 0);
         std::printf("%-28s W %lld: min %.4f ms median %.4f ms  %.2f TB/s (unique bytes %.2f GB)\n", v.name, W,
                     m[0], med, bytes / (med * 1e-3) / 1e12, bytes / 1e9);
