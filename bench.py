@@ -835,6 +835,9 @@ def main():
                          "(exercises the RCCL path on one GPU)")
     ap.add_argument("--no-graph", dest="graph", action="store_false",
                     help="streams config: time eager steps instead of one HIP graph per step")
+    ap.add_argument("--extras-timeout", type=float, default=240.0,
+                    help="N > 1: seconds the configs[4] extra may take before a watchdog prints "
+                         "the headline line without it and ends every rank")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="nccl (= RCCL over xGMI) on the real node; gloo only to rehearse the "
                          "multi-rank path with several ranks sharing one GPU")
@@ -877,6 +880,7 @@ def main():
                    if plain and not args.no_cpu_baseline else 0)
 
     extras = {}
+    guard = None
     if plain and args.config == "fsk2" and not args.no_extras:
         # configs[2] and configs[3], same steps / warmup, in their own buffers
         # (the main run's stay alive for the CPU baseline's parity sample)
@@ -897,7 +901,13 @@ def main():
         extras["streams"] = streams_child(args)
     elif world > 1 and args.config == "fsk2" and not args.no_extras:
         # the headline is already measured: a failure here (every rank runs the
-        # same code, so every rank raises alike) costs the entry, not the line
+        # same code, so every rank raises alike) costs the entry, not the line;
+        # a hang (the step's HIP graph holds an RCCL collective) ends at the
+        # watchdog's deadline with the headline line printed and every rank
+        # exiting 0
+        guard = extras_watchdog(lambda: headline_line(args, r, world, {"streams": {
+            "error": f"timed out after {args.extras_timeout:.0f} s (watchdog)"}}),
+            rank, args.extras_timeout)
         try:
             # configs[4] over the N ranks (strong scaling), and the same workload on
             # rank 0's GPU alone for scaling_vs_n1 (the other ranks wait)
@@ -931,76 +941,17 @@ def main():
             extras["streams"] = {"error": f"{type(e).__name__}: {e}"[:800]}
 
     if rank == 0:
-        samples = r["total_windows"] * r["n"]  # stream samples demodulated (each counted once)
-        value = samples / (r["ms_per_step"] / 1e3) / 1e6
-        config, K, hop, W, n_eval = r["config"], r["K"], r["hop"], r["W"], r["n_eval"]
-        dev_framing = config == "streams"
-        out = {
-            "metric": METRIC,
-            "value": round(value, 1),
-            "unit": "Msamples/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "warmup_effective": r["warm"],
-            "ms_per_step": round(r["ms_per_step"], 4),
-            "higher_is_better": True,
-            "scaling": "strong" if config == "streams" else "weak",
-            "vs_baseline": None,
-            "dtype": "fp32",
-            "data": "synthetic (seeded splitmix64 FSK, A=8000, Irwin-Hall noise sigma=400)",
-            "config": {
-                "workload": ("configs[4]: 1024 streams x 2048 windows (2^21 samples each), "
-                             f"sharded by stream over {world} GPU(s), 2-FSK"
-                             if config == "streams" else
-                             f"configs[3]: sliding 1024-pt full-spectrum FFT, hop {hop}, "
-                             f"{n_eval} windows over a {W * 1024}-sample int16 stream per GPU"
-                             if config == "fft" else
-                             ("configs[1]: 2-FSK" if K == 2 else
-                              "configs[2]: 8-FSK" + (" (integer bins 32 + 9 i)" if args.plan == "odd"
-                                                     else ""))
-                             + f" Goertzel, {W} x 1024-sample int16 windows per GPU, HBM-resident"),
-                "tones_hz": list(r["freqs"]),
-                "windows_per_gpu": n_eval,
-                "hop": hop,
-                "n": r["n"],
-                "outputs": "symbols" + ("" if args.no_mags else " + |X_k|^2"),
-                "parallelism": (f"dp{world} (stream shards; per-rank device framing, RCCL "
-                                "all-gather of ToReceiver frames)" if dev_framing else
-                                f"dp{world} (independent window shards, RCCL symbol all-gather)"),
-            },
-            "detector": r["detector"],
-            "kernel_ms_p10_p50_p90": [round(float(np.percentile(r["kts"], q)), 4)
-                                      for q in (10, 50, 90)],
-            "symbol_errors": r["sym_err"],
-            "symbol_error_rate": r["sym_err"] / float(r["total_windows"]),
-            "kernel_ms": round(r["kernel_ms"], 4),
-            "kernel_ms_steps": f"HIP events on every {EV_EVERY}th timed step ({len(r['kts'])})",
-            "roofline": r["roofline"],
-        }
-        if "roofline_valu" in r:
-            out["roofline_valu"] = r["roofline_valu"]
-        if "overhead" in r:
-            out["overhead"] = r["overhead"]
-        if "rescue" in r:
-            out["rescue"] = r["rescue"]
-        if "sustained" in r:
-            out["sustained"] = r["sustained"]
-        if "parity_all" in r:
-            out["parity_all"] = r["parity_all"]
-        if r["framed"]:
-            out["framing"] = r["framed"]
-        out.update(extras)
+        out = headline_line(args, r, world, extras)
         if world == 1 and not args.no_cpu_baseline:
             visible, affinity, quota, threads, why = cpu_share()
             if args.cpu_threads:
                 threads, why = args.cpu_threads, "--cpu-threads"
             base, parity = cpu_baseline(r["d_pcm"], r["d_sym"], r["d_mag"], r["freqs"],
-                                        args.cpu_seconds, threads, config == "fft", hop)
+                                        args.cpu_seconds, threads, r["config"] == "fft", r["hop"])
             base.update({"host_cpus_visible": visible, "cpus_in_affinity": affinity,
                          "cgroup_quota_cores": quota, "threads_why": why})
             out["cpu_baseline"] = base
-            if config in ("fsk2", "fsk8"):
+            if r["config"] in ("fsk2", "fsk8"):
                 sys.path.insert(0, ROOT)
                 from oracle import oracle as O
                 parity = {"sigma400": parity,
@@ -1008,9 +959,103 @@ def main():
                                                      r["d_pcm"].device, torch, threads)}
             out["parity_sample"] = parity
         out["extra_keys"] = sorted(extras)
+        if guard is not None:
+            guard.printed = True
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+    if guard is not None:
+        guard.set()
+
+
+def extras_watchdog(line_fn, rank, seconds):
+    """N > 1: if the extra measurement (and the teardown after it) has not
+    finished after `seconds`, rank 0 prints the headline line (line_fn) unless
+    it already printed its line, and every rank exits 0. Returns the event
+    that disarms it (its `printed` attribute marks the line as out)."""
+    import threading
+
+    done = threading.Event()
+    done.printed = False
+
+    def fire():
+        if done.wait(seconds):
+            return
+        if rank == 0 and not done.printed:
+            out = line_fn()
+            out["extra_keys"] = sorted(k for k in out if k == "streams")
+            print(json.dumps(out), flush=True)
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(0)
+
+    threading.Thread(target=fire, daemon=True).start()
+    return done
+
+
+def headline_line(args, r, world, extras) -> dict:
+    """The JSON line (without the CPU baseline and extra_keys) for rank 0."""
+    samples = r["total_windows"] * r["n"]  # stream samples demodulated (each counted once)
+    value = samples / (r["ms_per_step"] / 1e3) / 1e6
+    config, K, hop, W, n_eval = r["config"], r["K"], r["hop"], r["W"], r["n_eval"]
+    dev_framing = config == "streams"
+    out = {
+        "metric": METRIC,
+        "value": round(value, 1),
+        "unit": "Msamples/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "warmup_effective": r["warm"],
+        "ms_per_step": round(r["ms_per_step"], 4),
+        "higher_is_better": True,
+        "scaling": "strong" if config == "streams" else "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic (seeded splitmix64 FSK, A=8000, Irwin-Hall noise sigma=400)",
+        "config": {
+            "workload": ("configs[4]: 1024 streams x 2048 windows (2^21 samples each), "
+                         f"sharded by stream over {world} GPU(s), 2-FSK"
+                         if config == "streams" else
+                         f"configs[3]: sliding 1024-pt full-spectrum FFT, hop {hop}, "
+                         f"{n_eval} windows over a {W * 1024}-sample int16 stream per GPU"
+                         if config == "fft" else
+                         ("configs[1]: 2-FSK" if K == 2 else
+                          "configs[2]: 8-FSK" + (" (integer bins 32 + 9 i)" if args.plan == "odd"
+                                                 else ""))
+                         + f" Goertzel, {W} x 1024-sample int16 windows per GPU, HBM-resident"),
+            "tones_hz": list(r["freqs"]),
+            "windows_per_gpu": n_eval,
+            "hop": hop,
+            "n": r["n"],
+            "outputs": "symbols" + ("" if args.no_mags else " + |X_k|^2"),
+            "parallelism": (f"dp{world} (stream shards; per-rank device framing, RCCL "
+                            "all-gather of ToReceiver frames)" if dev_framing else
+                            f"dp{world} (independent window shards, RCCL symbol all-gather)"),
+        },
+        "detector": r["detector"],
+        "kernel_ms_p10_p50_p90": [round(float(np.percentile(r["kts"], q)), 4)
+                                  for q in (10, 50, 90)],
+        "symbol_errors": r["sym_err"],
+        "symbol_error_rate": r["sym_err"] / float(r["total_windows"]),
+        "kernel_ms": round(r["kernel_ms"], 4),
+        "kernel_ms_steps": f"HIP events on every {EV_EVERY}th timed step ({len(r['kts'])})",
+        "roofline": r["roofline"],
+    }
+    if "roofline_valu" in r:
+        out["roofline_valu"] = r["roofline_valu"]
+    if "overhead" in r:
+        out["overhead"] = r["overhead"]
+    if "rescue" in r:
+        out["rescue"] = r["rescue"]
+    if "sustained" in r:
+        out["sustained"] = r["sustained"]
+    if "parity_all" in r:
+        out["parity_all"] = r["parity_all"]
+    if r["framed"]:
+        out["framing"] = r["framed"]
+    out.update(extras)
+    return out
 
 
 if __name__ == "__main__":

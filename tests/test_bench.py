@@ -147,3 +147,36 @@ def test_parity_all_counts_against_the_oracle():
     out = bench.parity_all(torch.from_numpy(flat.copy()), torch.from_numpy(s2.copy()),
                            torch.from_numpy(P2.astype(np.float32)), f, 1024, 256, True, every=9, chunk=7)
     assert out["windows_checked"] == len(range(0, s2.size, 9)) and out["symbol_mismatches"] == 0
+
+
+def _watchdog_run(code):
+    return subprocess.run([sys.executable, "-c", f"import sys; sys.path.insert(0, {ROOT!r}); "
+                           "import bench, time; " + code],
+                          capture_output=True, text=True, timeout=60)
+
+
+def test_extras_watchdog_prints_headline_and_exits_zero():
+    """N > 1: a hung extra measurement ends at the watchdog's deadline with rank
+    0's headline line printed (the extra marked) and the process exiting 0."""
+    r = _watchdog_run("bench.extras_watchdog(lambda: {'value': 1.5, 'streams': {'error': 't'}}, 0, 0.3); "
+                      "time.sleep(30)")
+    assert r.returncode == 0
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["value"] == 1.5 and line["extra_keys"] == ["streams"]
+    # other ranks exit without printing
+    r = _watchdog_run("bench.extras_watchdog(lambda: {'value': 1.5}, 1, 0.3); time.sleep(30)")
+    assert r.returncode == 0 and r.stdout.strip() == ""
+
+
+def test_extras_watchdog_disarmed_stays_silent():
+    r = _watchdog_run("e = bench.extras_watchdog(lambda: {'value': 1.5}, 0, 0.5); e.set(); "
+                      "time.sleep(1.0); print('main done')")
+    assert r.returncode == 0 and r.stdout.strip() == "main done"
+
+
+def test_extras_watchdog_after_the_line_only_exits():
+    """A teardown that hangs after rank 0 printed its line: the watchdog ends
+    the process without a second line."""
+    r = _watchdog_run("e = bench.extras_watchdog(lambda: {'value': 1.5}, 0, 0.5); e.printed = True; "
+                      "print('{\"value\": 2.0}', flush=True); time.sleep(30)")
+    assert r.returncode == 0 and r.stdout.strip().splitlines() == ['{"value": 2.0}']
