@@ -909,6 +909,8 @@ def main():
             "error": f"timed out after {args.extras_timeout:.0f} s (watchdog)"}}),
             rank, args.extras_timeout)
         try:
+            if os.environ.get("BENCH_TEST_HANG_EXTRA"):
+                time.sleep(3600)  # tests: a hung extra (test_self_launch_watchdog_keeps_the_headline)
             # configs[4] over the N ranks (strong scaling), and the same workload on
             # rank 0's GPU alone for scaling_vs_n1 (the other ranks wait)
             for k in ("d_pcm", "d_sym", "d_mag", "d_true"):

@@ -125,19 +125,20 @@ def test_self_launch_two_ranks_prints_n_gpus_2():
 
 
 def test_self_launch_watchdog_keeps_the_headline():
-    """The N > 1 watchdog with a deadline shorter than the configs[4] extra:
-    the job still ends 0 with exactly one line, the headline measured and
-    the extra marked as timed out (a hung RCCL step on a real node ends the
-    same way instead of losing the line)."""
+    """The N > 1 watchdog with a hung configs[4] extra (BENCH_TEST_HANG_EXTRA
+    makes every rank sleep inside it): the job still ends 0 with exactly one
+    line, the headline measured and the extra marked as timed out (a hung
+    RCCL step on a real node ends the same way instead of losing the line)."""
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no GPU visible")
     env = dict(os.environ)
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT", "MASTER_ADDR"):
         env.pop(k, None)
+    env["BENCH_TEST_HANG_EXTRA"] = "1"
     r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--gpus", "2",
                         "--dist-backend", "gloo", "--windows", "65536", "--steps", "3",
-                        "--warmup", "1", "--extras-timeout", "0.5"],
+                        "--warmup", "1", "--extras-timeout", "5"],
                        capture_output=True, timeout=600, cwd=ROOT, env=env)
     out = r.stdout.decode()
     assert r.returncode == 0, (out[-2000:], r.stderr.decode()[-4000:])
