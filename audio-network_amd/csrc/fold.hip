@@ -125,6 +125,7 @@ __device__ __forceinline__ void fold_decide(const int (&acc)[8], const float4 *r
 //   ROTLDS: keep the per-lane rotation constants in a block LDS table instead
 //           of 4K VGPRs (raises occupancy for large K).
 //   NTS: non-temporal output stores.
+//   LAUX: (probe) the input loads' cache-policy bits; -1: nt when NT, else plain.
 //   WS: window_sum.h epilogue (reduce-scatter, packed-key argmax) at n = 1024.
 //   PK: (with WS) tone pairs in packed fp32, one v_pk_add_f32 + v_pk_fma_f32
 //       per pair per folded sample instead of 2 scalar instructions per tone.
@@ -144,7 +145,8 @@ __device__ __forceinline__ void fold_decide(const int (&acc)[8], const float4 *r
 //       rotations per lane, and the first reduce-scatter stage is already done
 //       (window_sum_decide_split8; perm maps slots back to the caller's tones).
 template <int K, int LOG2G, bool NT = true, int WPB = 4, bool ROTLDS = false, bool NTS = false,
-          bool WS = false, bool PK = false, bool LDST = false, bool F16 = false, int MST = -1>
+          bool WS = false, bool PK = false, bool LDST = false, bool F16 = false, int MST = -1,
+          int LAUX = -1>
 __global__ __launch_bounds__(64 * WPB) void fold_tile_kernel(GoertzelParams p)
 {
     const int lane = threadIdx.x & 63;
@@ -200,7 +202,7 @@ __global__ __launch_bounds__(64 * WPB) void fold_tile_kernel(GoertzelParams p)
         u32x4f v[8];
 #pragma unroll
         for (int m = 0; m < 8; ++m)
-            v[m] = __builtin_amdgcn_raw_buffer_load_b128(rs, goff[m], 0, NT ? 2 : 0);
+            v[m] = __builtin_amdgcn_raw_buffer_load_b128(rs, goff[m], 0, LAUX >= 0 ? LAUX : NT ? 2 : 0);
         if (LDST) {
 #pragma unroll
             for (int m = 0; m < 8; ++m) wl[64 * m + lane] = v[m];

@@ -3,7 +3,7 @@
 // policy and launch slicing.
 //
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -Iinclude scripts/mag_probe.hip -o scripts/bin/mag_probe
-//   scripts/bin/mag_probe [rounds=6] [reps=5]
+//   scripts/bin/mag_probe [rounds=6] [reps=5] [loads]
 //
 // Same kernel, grid and input as the shipped configs[2] path
 // (fold_tile_kernel F16, 2-wave blocks, one tile per wave, XCD-swizzled);
@@ -37,11 +37,11 @@ using namespace fskd;
         }                                                                       \
     } while (0)
 
-template <int MST>
+template <int MST, int LAUX = -1>
 static const void *f16k()
 {
     return reinterpret_cast<const void *>(
-        &fold_tile_kernel<8, 4, true, kPlainWPB, false, false, true, false, true, true, MST>);
+        &fold_tile_kernel<8, 4, true, kPlainWPB, false, false, true, false, true, true, MST, LAUX>);
 }
 
 struct Var {
@@ -110,9 +110,19 @@ int main(int argc, char **argv)
     CK(hipMalloc(&mag_ref, W * 8 * 4));
 
     std::vector<Var> vs;
+    const bool loads = argc > 3 && std::strcmp(argv[3], "loads") == 0;
     for (int sl : {1, 2, 4}) {
         vs.push_back({"no mags", f16k<-1>(), sl, false, {}});
         vs.push_back({"plain (shipped)", f16k<-1>(), sl, true, {}});
+        if (loads) {
+            // input load policy with plain magnitude stores (round 3, late)
+            vs.push_back({"loads sc0 nt", f16k<-1, 3>(), sl, true, {}});
+            vs.push_back({"loads sc1 nt", f16k<-1, 18>(), sl, true, {}});
+            vs.push_back({"loads sc0 sc1", f16k<-1, 17>(), sl, true, {}});
+            vs.push_back({"loads sc0 sc1 nt", f16k<-1, 19>(), sl, true, {}});
+            vs.push_back({"loads plain", f16k<-1, 0>(), sl, true, {}});
+            continue;
+        }
         vs.push_back({"nontemporal", f16k<1>(), sl, true, {}});
         vs.push_back({"buffer nt", f16k<2 + 2>(), sl, true, {}});
         vs.push_back({"buffer sc1", f16k<2 + 16>(), sl, true, {}});
