@@ -5,6 +5,8 @@ profiles/pmc_<cfg>.json (read by bench.py for roofline.traffic) and copies the
 counter CSVs to profiles/<round>/.
 
     python scripts/pmc_traffic_json.py [round2]
+    python scripts/pmc_traffic_json.py round3/r3z r3z   # round 3 closing check:
+        # passes under gpurun_out/r3z/ (scripts/gpu_r3_z.sh), CSVs to profiles/round3/r3z/
 
 Round 2 (scripts/gpu_profile_r2.sh, scripts/gpu_r2_fft.sh) adds the FFT
 detector at hop 256 (configs[3]) and hop 1024.
@@ -24,13 +26,17 @@ CFGS = {"fsk2": (2, "goertzel_tile_kernel", 1024), "fsk8": (8, "fold_tile_kernel
         "fft1024": (2, "fft1024_quad_kernel", 1024)}
 
 
-def main(rnd="round1"):
+def main(rnd="round1", sub=""):
+    base = os.path.join(ROOT, "gpurun_out", sub)
+    os.makedirs(os.path.join(ROOT, "profiles", rnd), exist_ok=True)
     for tag, (k, kname, hop) in CFGS.items():
-        if not os.path.exists(os.path.join(ROOT, "gpurun_out", f"pmc_{tag}_FETCH_SIZE")):
+        if sub and tag.startswith("fft"):
+            continue  # round 3: the FFT passes go through scripts/pmc_fft_r3_json.py
+        if not os.path.exists(os.path.join(base, f"pmc_{tag}_FETCH_SIZE")):
             continue
         vals, name = {}, None
         for c in ("FETCH_SIZE", "WRITE_SIZE"):
-            src = os.path.join(ROOT, "gpurun_out", f"pmc_{tag}_{c}", "run_counter_collection.csv")
+            src = os.path.join(base, f"pmc_{tag}_{c}", "run_counter_collection.csv")
             rows = [r for r in csv.DictReader(open(src))
                     if kname in r["Kernel_Name"] and r["Counter_Name"] == c]
             name = rows[0]["Kernel_Name"]
@@ -50,7 +56,9 @@ def main(rnd="round1"):
             "hbm_bytes_per_launch": rd + wr, "alg_bytes_per_launch": alg,
             "traffic_over_alg": (rd + wr) / alg,
             "method": ("rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate runs of "
-                       "bench.py (scripts/gpu_pmc_traffic.sh, round 2: gpu_profile_r2.sh / gpu_r2_fft.sh); bytes = KB*1024, FETCH doubled "
+                       "bench.py (" + ("scripts/gpu_r3_z.sh, round 3 closing check" if sub else
+                                       "scripts/gpu_pmc_traffic.sh, round 2: gpu_profile_r2.sh / gpu_r2_fft.sh")
+                       + "); bytes = KB*1024, FETCH doubled "
                        "per MI355X_MICROARCH.md §HBM (gfx950 counts 1/2 of 16 B/lane streaming "
                        "reads); calibration: the 16 B/lane synth_kernel write of 2 GiB reads "
                        "WRITE_SIZE 2105344 KB = 2.0078 GiB"),
