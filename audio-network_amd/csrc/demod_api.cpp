@@ -41,6 +41,9 @@ struct demod {
     // decision rescue (rescue.hip)
     bool rescue = false;        // K >= 2 and not switched off (FSKD_NO_RESCUE=1)
     bool rescue_launch = true;  // FSKD_NO_RESCUE=flags: flag only, no rescue launch (diagnostics)
+    // large-output batches: one launch with L2 write-back bursts (default), or
+    // the round-2 launch slices (FSKD_WB_BURSTS=0, measurement switch)
+    bool wb_bursts = true;
     float amb_tq = 0.f;         // detectors' ambiguity threshold: amb_tq sqrt(P_max)
     float amb_floor = 0.f;
     double rcoef[kMaxTones] = {};  // 2 cos(2 pi f_k / fs) in double, the caller's tone order
@@ -415,6 +418,8 @@ static int init_device_state(demod_t *st)
     const char *no_rescue = std::getenv("FSKD_NO_RESCUE");
     st->rescue = c.k >= 2 && !(no_rescue && no_rescue[0] == '1');
     st->rescue_launch = !(no_rescue && std::strcmp(no_rescue, "flags") == 0);
+    const char *wb_env = std::getenv("FSKD_WB_BURSTS");
+    st->wb_bursts = !(wb_env && std::strcmp(wb_env, "0") == 0);
     if (st->rescue) {
         const double sq = (double)c.n * 32768.0;  // sqrt(Q)
         const double tau = amb_tau(st->detector, st->log2g);
@@ -529,6 +534,7 @@ static size_t windows_for(const demod_t *st, size_t total)
 }
 
 constexpr size_t kOutChunkBytes = 10u << 20;  // symbol + magnitude bytes per detector launch
+constexpr size_t kBurstBytes = 5u << 20;      // output bytes per L2 write-back burst
 
 // Windows per launch of a Goertzel-family batch (enqueue_batch): outputs
 // beyond ~1 MiB per XCD L2 are written back to HBM while the input still
@@ -541,15 +547,31 @@ constexpr size_t kOutChunkBytes = 10u << 20;  // symbol + magnitude bytes per de
 // (hop < n) are bound by the recurrences and L2, not by HBM turnarounds, and
 // only pay the extra launches there (2-FSK hop 128: 0.466 -> 0.494 ms), so
 // they stay one launch, as does the VALU-bound FFT detector.
+// Round 3: such a batch runs as ONE launch that writes each XCD's L2 back in
+// bursts of ~kBurstBytes of output (wb_burst, demod_internal.h): no drain and
+// ramp per slice (8-FSK 315-316 us against 331 us for the 4 slices and 337 us
+// for one plain launch on one box, 309-310 / 324 / 316 us on another;
+// scripts/mag_probe.hip wb). FSKD_WB_BURSTS=0 keeps the slices.
+static size_t out_bytes(const demod_t *st, size_t n_windows, bool mags)
+{
+    return n_windows * (1 + (mags ? 4 * (size_t)st->cfg.k : 0));
+}
+static bool large_output(const demod_t *st, size_t n_windows, bool mags)
+{
+    return st->detector != kDetFft && st->cfg.hop >= st->cfg.n && n_windows &&
+           out_bytes(st, n_windows, mags) > kOutChunkBytes;
+}
 static size_t launch_slice(const demod_t *st, size_t n_windows, bool mags)
 {
-    if (st->detector == kDetFft || st->cfg.hop < st->cfg.n || n_windows == 0) return n_windows;
-    const size_t out_per_window = 1 + (mags ? 4 * (size_t)st->cfg.k : 0);
-    const size_t parts = std::min<size_t>(
-        (n_windows * out_per_window + kOutChunkBytes - 1) / kOutChunkBytes, 16);
-    if (parts <= 1) return n_windows;
+    if (!large_output(st, n_windows, mags) || st->wb_bursts) return n_windows;
+    const size_t parts = std::min<size_t>((out_bytes(st, n_windows, mags) + kOutChunkBytes - 1) / kOutChunkBytes, 16);
     const size_t per = (n_windows + parts - 1) / parts;
     return (per + 63) / 64 * 64;
+}
+static int burst_count(const demod_t *st, size_t n_windows, bool mags)
+{
+    if (!large_output(st, n_windows, mags) || !st->wb_bursts) return 0;
+    return (int)std::min<size_t>((out_bytes(st, n_windows, mags) + kBurstBytes - 1) / kBurstBytes, 64);
 }
 
 int demod_batch_launches(const demod_t *st, size_t n_windows, int with_mags)
@@ -656,6 +678,7 @@ static int enqueue_batch(demod_t *st, const int16_t *d_pcm, size_t n_windows, ui
     p.amb_tq = st->amb_tq;
     p.amb_floor = st->amb_floor;
     const size_t per = launch_slice(st, n_windows, d_mag != nullptr);
+    p.wb_bursts = burst_count(st, n_windows, d_mag != nullptr);
     for (size_t w0 = 0; w0 < n_windows; w0 += per) {
         const size_t cnt = std::min(per, n_windows - w0);
         p.pcm = d_pcm + w0 * st->cfg.hop;

@@ -44,6 +44,9 @@ struct GoertzelParams {
     // 1: overlapping windows (hop < n) share lines between tiles, so the loads
     // keep them in L2 (plain policy); 0: each byte is read once (nt)
     int cached;
+    // write-back bursts (wb_burst): 0 = none, else the number of bursts per
+    // XCD in this launch
+    int wb_bursts;
     // decision rescue (rescue.hip): ambiguity test constants
     float amb_tq;            // threshold = amb_tq * sqrt(P_max); 0: no flagging
     float amb_floor;         // 0 < P_max < amb_floor: always ambiguous
@@ -119,6 +122,21 @@ __device__ __forceinline__ long long tile_block(int swz)
     const long long per = nb / 8, full = per * 8;
     if (b >= full) return b;
     return (b % 8) * per + b / 8;
+}
+
+// Write-back bursts (round 3), at the end of a Goertzel-family
+// tile kernel. A batch whose outputs are more than the XCDs' L2s hold dirty
+// (8-FSK: 33 MiB) runs as one launch in which the last block of every
+// 1/wb_bursts of an XCD's swizzled blocks (its wave 0, after its stores)
+// writes that XCD's L2 back with an agent-scope release, so the output lines
+// leave in a few bursts instead of trickling out between the input's reads;
+// the launch slices this replaces paid a drain and a ramp per slice.
+__device__ __forceinline__ void wb_burst(int wb_bursts)
+{
+    if (wb_bursts <= 0 || threadIdx.x >= 64) return;
+    const long long b = blockIdx.x, per = gridDim.x / 8, seg = per / wb_bursts;
+    if (seg > 0 && b < per * 8 && (b / 8) % seg == seg - 1)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
 }
 
 // Full-spectrum detector (fft.hip), n = 1024.

@@ -306,6 +306,7 @@ __global__ __launch_bounds__(64 * WPB) void fold_tile_kernel(GoertzelParams p)
             }
         }
     }
+    wb_burst(p.wb_bursts);
 }
 
 // acc (lo, hi) += the sign-extended int16 halves of n, minus those of o: four

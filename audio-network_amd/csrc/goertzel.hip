@@ -365,6 +365,7 @@ __global__ __launch_bounds__(64 * WPB) void goertzel_tile_kernel(GoertzelParams 
             do_tile(t + stride, vb, t + 3 * stride);
         }
     }
+    wb_burst(p.wb_bursts);
 }
 
 // Shipped configuration: packed tone pairs for K >= 3 (K = 4: 407 -> 336 us,

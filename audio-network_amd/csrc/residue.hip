@@ -374,6 +374,7 @@ void residue_tile_kernel(GoertzelParams p)
             }
         }
     }
+    wb_burst(p.wb_bursts);
 }
 
 size_t residue_lds_bytes(int k, int log2g, int qp)

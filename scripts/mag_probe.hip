@@ -3,7 +3,7 @@
 // policy and launch slicing.
 //
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -Iinclude scripts/mag_probe.hip -o scripts/bin/mag_probe
-//   scripts/bin/mag_probe [rounds=6] [reps=5] [loads]
+//   scripts/bin/mag_probe [rounds=6] [reps=5] [loads|wb]
 //
 // Same kernel, grid and input as the shipped configs[2] path
 // (fold_tile_kernel F16, 2-wave blocks, one tile per wave, XCD-swizzled);
@@ -50,6 +50,7 @@ struct Var {
     int slices;
     bool mags;
     std::vector<float> ms;
+    int bursts = 0;  // GoertzelParams::wb_bursts (round 3, late)
 };
 
 int main(int argc, char **argv)
@@ -111,7 +112,25 @@ int main(int argc, char **argv)
 
     std::vector<Var> vs;
     const bool loads = argc > 3 && std::strcmp(argv[3], "loads") == 0;
+    const bool wb = argc > 3 && std::strcmp(argv[3], "wb") == 0;
+    if (wb) {
+        // round 3, late: L2 write-back bursts inside one launch (GoertzelParams::wb_bursts)
+        // against the shipped 4 slices and no magnitudes
+        for (int sl : {1, 4}) {
+            vs.push_back({"no mags", f16k<-1>(), sl, false, {}});
+            vs.push_back({"plain (shipped)", f16k<-1>(), sl, true, {}});
+        }
+        vs.push_back({"plain wbl2 x7", f16k<-1>(), 1, true, {}, 7});
+        vs.push_back({"plain wbl2 x4", f16k<-1>(), 1, true, {}, 4});
+        vs.push_back({"plain wbl2 x8", f16k<-1>(), 1, true, {}, 8});
+        vs.push_back({"plain wbl2 x16", f16k<-1>(), 1, true, {}, 16});
+        vs.push_back({"plain wbl2 x64", f16k<-1>(), 1, true, {}, 64});
+        vs.push_back({"plain wbl2 x256", f16k<-1>(), 1, true, {}, 256});
+        vs.push_back({"plain wbl2 x8", f16k<-1>(), 2, true, {}, 8});
+        vs.push_back({"nontemporal wbl2 x8", f16k<1>(), 1, true, {}, 8});
+    }
     for (int sl : {1, 2, 4}) {
+        if (wb) break;
         vs.push_back({"no mags", f16k<-1>(), sl, false, {}});
         vs.push_back({"plain (shipped)", f16k<-1>(), sl, true, {}});
         if (loads) {
@@ -138,6 +157,7 @@ int main(int argc, char **argv)
             q.n_windows = cnt;
             q.sym = s_out + w0;
             q.mag = v.mags ? m_out + w0 * 8 : nullptr;
+            q.wb_bursts = v.bursts;
             const long long tiles = (cnt + 3) / 4;
             const unsigned blocks = (unsigned)((tiles + kPlainWPB - 1) / kPlainWPB);
             void *args[] = {&q};

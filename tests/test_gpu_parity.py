@@ -671,21 +671,31 @@ def test_device_framing_matches_host_codec(A, torch, n_streams, n, bits, max_pay
             assert np.array_equal(np.concatenate(back), sym[s] & mask)
 
 
-def test_batch_launch_slices(A, O, torch):
-    """Batches whose symbol + magnitude output exceeds ~10 MiB run as several
-    launches (demod_batch_launches); the slices must give the same symbols and
-    powers as one launch over the same windows (smaller batches below the
-    threshold), including a window count that is not a multiple of the slice."""
+@pytest.mark.parametrize("plan", ["fold", "odd"])
+@pytest.mark.parametrize("mode", ["bursts", "slices"])
+def test_batch_launch_slices(A, O, torch, monkeypatch, mode, plan):
+    """Batches whose symbol + magnitude output exceeds ~10 MiB run as one
+    launch that writes each XCD's L2 back in bursts (round 3, the default) or,
+    with FSKD_WB_BURSTS=0 (read at create), as several launch slices
+    (demod_batch_launches); either must give the same symbols and powers as one
+    launch over the same windows (smaller batches below the threshold),
+    including a window count that is not a multiple of the slice. Plans: the
+    configs[2] tones (fold detector) and integer bins 32 + 9 i (residue
+    detector)."""
+    if mode == "slices":
+        monkeypatch.setenv("FSKD_WB_BURSTS", "0")
+    else:
+        monkeypatch.delenv("FSKD_WB_BURSTS", raising=False)
     n, W = 1024, (1 << 20) + 77
-    f = A.FSK8_FREQS
+    f = A.FSK8_FREQS if plan == "fold" else tuple(48000.0 * (32 + 9 * i) / n for i in range(8))
     cfg = A.make_cfg(n=n, freqs=f)
     d_pcm = torch.empty((W, n), dtype=torch.int16, device="cuda")
     A.synth_fsk(cfg, 99, W, 8000, 400, d_pcm)
     sym = torch.empty(W, dtype=torch.uint8, device="cuda")
     mag = torch.empty((W, 8), dtype=torch.float32, device="cuda")
     with A.Demodulator(cfg) as d:
-        # detector slices + the decision rescue's launch (DESIGN.md §2a)
-        assert d.batch_launches(W, mags=True) == 4 + 1
+        # detector launches + the decision rescue's launch (DESIGN.md §2a)
+        assert d.batch_launches(W, mags=True) == (4 if mode == "slices" else 1) + 1
         assert d.batch_launches(W, mags=False) == 1 + 1
         assert d.batch_launches(1 << 18, mags=True) == 1 + 1
         d.batch_device(d_pcm, W, sym, mag)
