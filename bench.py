@@ -459,8 +459,9 @@ def run_config(A, D, torch, dist, args, config, rank, world, local, use_dist, st
             framed = {"frames_bytes": len(stream_bytes), "bits_per_symbol": A.bits_per_symbol(K),
                       "roundtrip_ok": bool((back == all_sym.cpu().numpy()).all())}
 
-    # dispatches per step: batches with > ~10 MiB of output run as slices
-    # (demod_batch_launches); kernel_ms brackets the whole batch
+    # dispatches per step (demod_batch_launches): the detector launch (or
+    # launch slices under FSKD_WB_BURSTS=0) + the rescue's; kernel_ms
+    # brackets the whole batch
     launches = demod.batch_launches(n_eval, not no_mags)
     alg_bytes = W * 2 * n + n_eval * (1 + (0 if no_mags else 4 * K) +
                                       (513 * 4 if d_spec is not None else 0))
