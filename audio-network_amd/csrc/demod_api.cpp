@@ -44,6 +44,7 @@ struct demod {
     // large-output batches: one launch with L2 write-back bursts (default), or
     // the round-2 launch slices (FSKD_WB_BURSTS=0, measurement switch)
     bool wb_bursts = true;
+    int wb_force = 0;  // FSKD_WB_BURSTS=<n >= 1>: n bursts on every hop = n batch (measurement)
     float amb_tq = 0.f;         // detectors' ambiguity threshold: amb_tq sqrt(P_max)
     float amb_floor = 0.f;
     double rcoef[kMaxTones] = {};  // 2 cos(2 pi f_k / fs) in double, the caller's tone order
@@ -420,6 +421,7 @@ static int init_device_state(demod_t *st)
     st->rescue_launch = !(no_rescue && std::strcmp(no_rescue, "flags") == 0);
     const char *wb_env = std::getenv("FSKD_WB_BURSTS");
     st->wb_bursts = !(wb_env && std::strcmp(wb_env, "0") == 0);
+    if (wb_env && std::atoi(wb_env) > 0) st->wb_force = std::min(std::atoi(wb_env), 64);
     if (st->rescue) {
         const double sq = (double)c.n * 32768.0;  // sqrt(Q)
         const double tau = amb_tau(st->detector, st->log2g);
@@ -535,6 +537,7 @@ static size_t windows_for(const demod_t *st, size_t total)
 
 constexpr size_t kOutChunkBytes = 10u << 20;  // symbol + magnitude bytes per detector launch
 constexpr size_t kBurstBytes = 5u << 20;      // output bytes per L2 write-back burst
+constexpr size_t kBurstMinBytes = 4u << 20;   // smaller outputs: no bursts
 
 // Windows per launch of a Goertzel-family batch (enqueue_batch): outputs
 // beyond ~1 MiB per XCD L2 are written back to HBM while the input still
@@ -551,7 +554,10 @@ constexpr size_t kBurstBytes = 5u << 20;      // output bytes per L2 write-back 
 // bursts of ~kBurstBytes of output (wb_burst, demod_internal.h): no drain and
 // ramp per slice (8-FSK 315-316 us against 331 us for the 4 slices and 337 us
 // for one plain launch on one box, 309-310 / 324 / 316 us on another;
-// scripts/mag_probe.hip wb). FSKD_WB_BURSTS=0 keeps the slices.
+// scripts/mag_probe.hip wb). Batches from kBurstMinBytes up
+// also take at least 4 bursts (2-FSK's 9 MiB: 0.3006 ms against 0.3058 ms
+// with one write-back at the kernel's end, scripts/gpu_r3_wb2.sh).
+// FSKD_WB_BURSTS=0 keeps the round-2 behaviour (slices, no bursts).
 static size_t out_bytes(const demod_t *st, size_t n_windows, bool mags)
 {
     return n_windows * (1 + (mags ? 4 * (size_t)st->cfg.k : 0));
@@ -570,8 +576,11 @@ static size_t launch_slice(const demod_t *st, size_t n_windows, bool mags)
 }
 static int burst_count(const demod_t *st, size_t n_windows, bool mags)
 {
-    if (!large_output(st, n_windows, mags) || !st->wb_bursts) return 0;
-    return (int)std::min<size_t>((out_bytes(st, n_windows, mags) + kBurstBytes - 1) / kBurstBytes, 64);
+    if (st->wb_force && st->detector != kDetFft && st->cfg.hop >= st->cfg.n) return st->wb_force;
+    if (!st->wb_bursts || st->detector == kDetFft || st->cfg.hop < st->cfg.n) return 0;
+    const size_t out = out_bytes(st, n_windows, mags);
+    if (out < kBurstMinBytes) return 0;
+    return (int)std::min<size_t>(std::max<size_t>((out + kBurstBytes - 1) / kBurstBytes, 4), 64);
 }
 
 int demod_batch_launches(const demod_t *st, size_t n_windows, int with_mags)
