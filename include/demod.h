@@ -145,12 +145,14 @@ int demod_max_symbols(const demod_t *st, size_t n_frames);
 /* Kernel launches one device-pointer demod_batch / demod_batch_async of
  * n_windows makes (with_mags: magnitudes requested): the detector's, plus one
  * for the decision rescue (K >= 2, Goertzel-family detectors; the FFT
- * detector rescues inside its own launch). Goertzel-family batches whose symbol +
- * magnitude output exceeds ~10 MiB run as equal detector slices, so each
- * launch's output is written back from L2 in a burst instead of interleaved
- * with the input stream; profilers see that many
- * dispatches. A host-pointer demod_batch over 4 MiB of samples runs in
- * chunks of 65 536 windows, each chunk counted as a batch of its own. */
+ * detector rescues inside its own launch). A Goertzel-family batch is one
+ * detector launch; from 4 MiB of symbol + magnitude output it writes each
+ * XCD's L2 back in a few bursts inside that launch instead of interleaving the
+ * write-back with the input stream. With the environment
+ * variable FSKD_WB_BURSTS=0 at demod_create (a measurement switch), batches
+ * over ~10 MiB of output run as equal detector slices instead, and profilers
+ * see that many dispatches. A host-pointer demod_batch over 4 MiB of samples
+ * runs in chunks of 65 536 windows, each chunk counted as a batch of its own. */
 int demod_batch_launches(const demod_t *st, size_t n_windows, int with_mags);
 
 /*
