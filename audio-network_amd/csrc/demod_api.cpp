@@ -44,6 +44,7 @@ struct demod {
     // large-output batches: one launch with L2 write-back bursts (default), or
     // the round-2 launch slices (FSKD_WB_BURSTS=0, measurement switch)
     bool wb_bursts = true;
+    bool rescue_kernel_forced = false;  // FSKD_RESCUE_LAUNCH=1: the rescue launch everywhere (measurement)
     int wb_force = 0;  // FSKD_WB_BURSTS=<n >= 1>: n bursts on every hop = n batch (measurement)
     float amb_tq = 0.f;         // detectors' ambiguity threshold: amb_tq sqrt(P_max)
     float amb_floor = 0.f;
@@ -419,6 +420,8 @@ static int init_device_state(demod_t *st)
     const char *no_rescue = std::getenv("FSKD_NO_RESCUE");
     st->rescue = c.k >= 2 && !(no_rescue && no_rescue[0] == '1');
     st->rescue_launch = !(no_rescue && std::strcmp(no_rescue, "flags") == 0);
+    const char *rl_env = std::getenv("FSKD_RESCUE_LAUNCH");
+    st->rescue_kernel_forced = rl_env && std::strcmp(rl_env, "1") == 0;
     const char *wb_env = std::getenv("FSKD_WB_BURSTS");
     st->wb_bursts = !(wb_env && std::strcmp(wb_env, "0") == 0);
     if (wb_env && std::atoi(wb_env) > 0) st->wb_force = std::min(std::atoi(wb_env), 64);
@@ -583,6 +586,15 @@ static int burst_count(const demod_t *st, size_t n_windows, bool mags)
     return (int)std::min<size_t>(std::max<size_t>((out + kBurstBytes - 1) / kBurstBytes, 4), 64);
 }
 
+// The plain bank's K = 2 chain path at n = 1024 (no segment sharing) re-decides
+// its flagged windows inside the detector kernel (rescue_row,
+// demod_internal.h): no rescue launch. Other Goertzel-family kernels keep it.
+static bool rescue_in_kernel(const demod_t *st)
+{
+    return st->detector == kDetGoertzel && st->log2g == 4 && st->cfg.k == 2 && st->slide_wt == 0 &&
+           !st->rescue_kernel_forced;
+}
+
 int demod_batch_launches(const demod_t *st, size_t n_windows, int with_mags)
 {
     if (!st) return DEMOD_BAD_ARG;
@@ -590,7 +602,8 @@ int demod_batch_launches(const demod_t *st, size_t n_windows, int with_mags)
     const size_t per = launch_slice(st, n_windows, with_mags != 0);
     // + the decision rescue's launch (the FFT detector rescues in the kernel)
     const size_t n = (n_windows + per - 1) / per +
-                     (st->rescue && st->rescue_launch && st->detector != kDetFft ? 1 : 0);
+                     (st->rescue && st->rescue_launch && st->detector != kDetFft &&
+                              !rescue_in_kernel(st) ? 1 : 0);
     return n > 0x7FFFFFFF ? 0x7FFFFFFF : (int)n;
 }
 
@@ -599,7 +612,7 @@ int demod_batch_launches(const demod_t *st, size_t n_windows, int with_mags)
 static int enqueue_rescue(demod_t *st, const int16_t *d_pcm, size_t n_windows, uint8_t *d_sym,
                           float *d_mag, hipStream_t s)
 {
-    if (!st->rescue || !st->rescue_launch || n_windows == 0) return DEMOD_OK;
+    if (!st->rescue || !st->rescue_launch || n_windows == 0 || rescue_in_kernel(st)) return DEMOD_OK;
     RescueParams r;
     std::memset(&r, 0, sizeof(r));
     r.pcm = d_pcm;
@@ -688,6 +701,8 @@ static int enqueue_batch(demod_t *st, const int16_t *d_pcm, size_t n_windows, ui
     p.amb_floor = st->amb_floor;
     const size_t per = launch_slice(st, n_windows, d_mag != nullptr);
     p.wb_bursts = burst_count(st, n_windows, d_mag != nullptr);
+    p.rescue_inline = st->rescue && st->rescue_launch && rescue_in_kernel(st) ? 1 : 0;
+    for (uint32_t k = 0; k < st->cfg.k; ++k) p.rcoef[k] = st->rcoef[k];
     for (size_t w0 = 0; w0 < n_windows; w0 += per) {
         const size_t cnt = std::min(per, n_windows - w0);
         p.pcm = d_pcm + w0 * st->cfg.hop;

@@ -47,6 +47,11 @@ struct GoertzelParams {
     // write-back bursts (wb_burst): 0 = none, else the number of bursts per
     // XCD in this launch
     int wb_bursts;
+    // in-kernel decision rescue (goertzel.hip, n = 1024, K <= 2 chain path):
+    // flagged windows are re-decided by their own row instead of a rescue
+    // launch; rcoef = 2 cos(2 pi f_k / fs) in double, the caller's tone order
+    int rescue_inline;
+    double rcoef[kMaxTones];
     // decision rescue (rescue.hip): ambiguity test constants
     float amb_tq;            // threshold = amb_tq * sqrt(P_max); 0: no flagging
     float amb_floor;         // 0 < P_max < amb_floor: always ambiguous
@@ -131,6 +136,56 @@ __device__ __forceinline__ long long tile_block(int swz)
 // writes that XCD's L2 back with an agent-scope release, so the output lines
 // leave in a few bursts instead of trickling out between the input's reads;
 // the launch slices this replaces paid a drain and a ramp per slice.
+// In-kernel decision rescue of one window by its 16-lane row (round 3, late;
+// goertzel.hip K <= 2 at n = 1024): lane seg < K runs tone seg's recurrence
+// in double over the window's n samples with exactly rescue_kernel's
+// operations and order (so exactly oracle/fsk_oracle.c's), the row's argmax
+// (ties to the lowest tone) replaces the flagged symbol, and the powers
+// (rounded to fp32) the magnitudes. Every lane of the wave calls it (the
+// shuffles); rows with amb_row false change nothing.
+template <int K>
+__device__ __forceinline__ void rescue_row(const GoertzelParams &p, long long w, int seg, int lane,
+                                           bool amb_row, int n)
+{
+#pragma clang fp contract(off)
+    typedef unsigned int u32x4r __attribute__((ext_vector_type(4)));
+    double P = 0.0;
+    if (amb_row && seg < K) {
+        const double c = p.rcoef[seg];
+        double s1 = 0.0, s2 = 0.0;
+        const u32x4r *xs = reinterpret_cast<const u32x4r *>(p.pcm + w * p.hop);
+        for (int q = 0; q < n / 8; ++q) {
+            const u32x4r d = xs[q];
+            const unsigned d4[4] = {d.x, d.y, d.z, d.w};
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const double x = (double)(short)((d4[e >> 1] >> (16 * (e & 1))) & 0xFFFFu);
+                double s = x + c * s1;
+                s = s - s2;
+                s2 = s1;
+                s1 = s;
+            }
+        }
+        const double a = s1 * s1 + s2 * s2;
+        const double b = c * s1;
+        P = a - b * s2;
+    }
+    double best = -1.0;
+    int arg = 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const double pk = __shfl(P, (lane & 48) + k);
+        if (pk > best) {
+            best = pk;
+            arg = k;
+        }
+    }
+    if (amb_row) {
+        if (seg == 0) p.sym[w] = (uint8_t)arg;
+        if (p.mag && seg < K) p.mag[w * K + seg] = (float)P;
+    }
+}
+
 __device__ __forceinline__ void wb_burst(int wb_bursts)
 {
     if (wb_bursts <= 0 || threadIdx.x >= 64) return;

@@ -287,8 +287,10 @@ __global__ __launch_bounds__(64 * WPB) void goertzel_tile_kernel(GoertzelParams 
                         xr[k] = X.x;
                         xi[k] = X.y;
                     } else {  // as the direct K <= 2 path below
-                        xr[k] = r[k].x * z.x - r[k].z * z.y;
-                        xi[k] = r[k].y * z.x - r[k].w * z.y;
+                        // explicit fma (as the direct path): the SLIDE and direct
+                        // kernels must round alike whatever the contraction
+                        xr[k] = fmaf(r[k].x, z.x, -(r[k].z * z.y));
+                        xi[k] = fmaf(r[k].y, z.x, -(r[k].w * z.y));
                     }
                 }
                 if constexpr (WS) {
@@ -334,19 +336,29 @@ __global__ __launch_bounds__(64 * WPB) void goertzel_tile_kernel(GoertzelParams 
         float P[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-            float re = r[k].x * s1[k] - r[k].z * s2[k];
-            float im = r[k].y * s1[k] - r[k].w * s2[k];
+            float re = fmaf(r[k].x, s1[k], -(r[k].z * s2[k]));  // explicit: SLIDE rounds alike
+            float im = fmaf(r[k].y, s1[k], -(r[k].w * s2[k]));
             re = group_sum(re, log2g);
             im = group_sum(im, log2g);
             P[k] = fmaf(re, re, im * im);
         }
 
+        const uint8_t sv = chain_symbol<K>(P, p.amb_tq, p.amb_floor);
         if (w < p.n_windows) {
-            if (seg == 0) out_store<NTS>(p.sym + w, chain_symbol<K>(P, p.amb_tq, p.amb_floor));
+            if (seg == 0) out_store<NTS>(p.sym + w, sv);
             if (p.mag) {
 #pragma unroll
                 for (int k = 0; k < K; ++k)
                     if ((k & (g - 1)) == seg) out_store<NTS>(p.mag + w * K + k, P[k]);
+            }
+        }
+        if constexpr (LOG2G == 4 && K >= 2 && K <= 16) {
+            // decision rescue in the kernel (demod_internal.h rescue_row): the
+            // row's verdict is its lane 0's (the all-reduced powers may round
+            // differently in other lanes)
+            if (p.rescue_inline) {
+                const bool amb_row = w < p.n_windows && (__shfl((int)sv, lane & 48) & kSymAmbiguous);
+                if (__ballot(amb_row) != 0) rescue_row<K>(p, w, seg, lane, amb_row, n);
             }
         }
     };
