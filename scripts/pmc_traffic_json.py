@@ -41,19 +41,20 @@ def main(rnd="round1", sub=""):
             rows = sorted((r for r in csv.DictReader(open(src)) if r["Counter_Name"] == c),
                           key=lambda r: int(r["Dispatch_Id"]))
             name = next(r["Kernel_Name"] for r in rows if kname in r["Kernel_Name"])
-            # one batch = a run of consecutive detector launches (the 8-FSK
-            # batch is launch-sliced; the rescue launch separates batches);
-            # round 3 keeps the first MAX_BATCHES (warmup + timed steps): the
-            # bench's sustained phase re-reads the same input back to back
-            v, run = [], None
-            for r in rows:
-                if kname in r["Kernel_Name"]:
-                    run = (run or 0.0) + float(r["Counter_Value"])
-                elif run is not None:
-                    v.append(run)
-                    run = None
-            if run is not None:
-                v.append(run)
+            # one batch = `per` consecutive detector launches: the bench line of
+            # the pass gives launches_per_step, less the rescue's launch when
+            # the trace has one (round-2 launch slices: 4 + 1; round 3: 1 + 1,
+            # or 1 where the detector rescues in its own kernel); round 3
+            # keeps the first MAX_BATCHES (warmup + timed steps): the bench's
+            # sustained phase re-reads the same input back to back
+            det = [float(r["Counter_Value"]) for r in rows if kname in r["Kernel_Name"]]
+            per = 1
+            if sub:
+                line = [ln for ln in open(os.path.join(base, f"pmc_{tag}_{c}.log"))
+                        if ln.startswith("{")][-1]
+                lps = int(json.loads(line)["roofline"]["launches_per_step"])
+                per = max(1, lps - (1 if any("rescue_kernel" in r["Kernel_Name"] for r in rows) else 0))
+            v = [sum(det[i:i + per]) for i in range(0, len(det) - per + 1, per)]
             if sub:
                 v = v[:MAX_BATCHES]
             vals[c] = (sum(v) / len(v), len(v))
