@@ -25,6 +25,9 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libfskdemod.so")
+# FSKD_LIB: another build of the same ABI (measurement A/B of two builds in
+# one GPU call, scripts/gpu_run.sh); the product default is the in-tree build
+_LIB_ENV = os.environ.get("FSKD_LIB")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "demod.h")
 
 DEMOD_OK = 0
@@ -122,6 +125,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     global _lib
     if _lib is not None:
         return _lib
+    if _LIB_ENV and path == LIB_PATH:
+        path = _LIB_ENV
     if not os.path.exists(path):
         raise FileNotFoundError(
             f"{path} not built: run `make -C audio-network_amd/csrc` "
@@ -143,6 +148,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "demod_method": (ctypes.c_int, [_P]),
         "demod_max_symbols": (ctypes.c_int, [_P, _SZ]),
         "demod_batch_launches": (ctypes.c_int, [_P, _SZ, ctypes.c_int]),
+        "demod_rescue_tau": (ctypes.c_double, [_P]),
         "demodulate": (ctypes.c_int, [_P, _P, _SZ, _P, _SZ]),
         "demodulate_mags": (ctypes.c_int, [_P, _P, _SZ, _P, _P, _SZ]),
         "demod_batch": (ctypes.c_int, [_P, _P, _SZ, _P, _P]),
@@ -184,6 +190,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "demod_version_string": (ctypes.c_char_p, []),
     }
     for name, (res, args) in sig.items():
+        if _LIB_ENV and not hasattr(lib, name):
+            continue  # an older build for an A/B: entry points it predates stay unbound
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
@@ -330,6 +338,11 @@ class Demodulator:
 
     def max_symbols(self, n_frames: int) -> int:
         return int(self._lib.demod_max_symbols(self._h, n_frames))
+
+    @property
+    def rescue_tau(self) -> float:
+        """The decision rescue's threshold factor tau (demod_rescue_tau; 0: off)."""
+        return float(self._lib.demod_rescue_tau(self._h))
 
     def batch_launches(self, n_windows: int, mags: bool = True) -> int:
         """Kernel launches one batch of n_windows makes (demod_batch_launches)."""

@@ -46,8 +46,10 @@ struct demod {
     bool wb_bursts = true;
     bool rescue_kernel_forced = false;  // FSKD_RESCUE_LAUNCH=1: the rescue launch everywhere (measurement)
     int wb_force = 0;  // FSKD_WB_BURSTS=<n >= 1>: n bursts on every hop = n batch (measurement)
-    float amb_tq = 0.f;         // detectors' ambiguity threshold: amb_tq sqrt(P_max)
+    double tau = 0.0;           // decision rescue threshold factor (amb_tau)
+    float amb_tq = 0.f;         // stage 1: amb_tq sqrt(P_max), the int16 worst-case energy
     float amb_floor = 0.f;
+    float amb_t2e = 0.f;        // stage 2: threshold^2 = amb_t2e E P_max
     double rcoef[kMaxTones] = {};  // 2 cos(2 pi f_k / fs) in double, the caller's tone order
     double *d_rtw = nullptr;    // FFT: radix-2 twiddles (cos, sin)(-2 pi j / len), [n - 1]
     float coef[kMaxTones] = {};
@@ -190,20 +192,40 @@ static int validate(const demod_cfg_t *c)
     return DEMOD_OK;
 }
 
-// Decision rescue threshold factor tau per detector. The
-// largest fp32 power error each detector showed against the double oracle,
-// as a fraction r of sqrt(P_max n sum x^2), over every signal family and
-// kernel path of scripts/precision_probe.py (profiles/round3/
-// precision_probe.log): plain bank (direct, SLIDE, Reinsch, any n) 2.67e-6,
-// fold / fold-slide / residue 1.19e-6, FFT 2.64e-7. A margin carries the
-// errors of two powers: tau = 2 r x 6 (safety).
-// The fold / residue figure was measured at n = 1024; other window lengths
-// keep the plain bank's.
-static double amb_tau(int detector, int log2g)
+// Decision rescue threshold factor tau per detector and tone plan (DESIGN.md
+// §2a). r = the largest fp32 power error a detector showed against the double
+// oracle, as a fraction of sqrt(P_max NE) (NE the energy of the window the
+// detector transforms: n sum x^2, or (n/8) sum xf^2 for the fold detector),
+// over every signal family and kernel path of scripts/precision_probe.py
+// (profiles/round3/precision_probe.log; round 4: tests/test_gpu_error_model.py
+// asserts the model on every window of an adversarial sweep): plain bank
+// (direct, SLIDE, Reinsch, any n) 2.67e-6 at the survey plans' lowest tone
+// (|sin w| = 0.195), fold / fold-slide / residue 1.19e-6 (n = 1024), FFT
+// 2.64e-7. A margin carries the errors of two powers: tau = 2 r x 6 (safety).
+// Plan-aware factors (Goertzel family):
+//  * the recurrence's conditioning: the fp32 coefficient 2cos(w) moves the
+//    chain's frequency by d(2cos w) / (2 sin w), and the chain state grows like
+//    1 / sin w, so the error grows like 1 / sin^2 w: r scales with
+//    (0.195 / s_min)^2 for the lowest |sin w| of the plan when that is below
+//    the measured plans' (down to the Reinsch switch at 0.1: x 3.8). Reinsch
+//    plans keep the plain figure (measured 3.0e-7 there: 9x headroom);
+//  * longer windows sum more segments: x sqrt(G / 16) for G = n / 64 > 16
+//    (measured flat from n = 256 to 4096, kept as margin);
+//  * fold and residue at n != 1024 (not probed there) take the plain bank's r.
+static double amb_tau(int detector, int log2g, const demod_cfg_t &c, bool reinsch)
 {
     if (detector == kDetFft) return 12.0 * 2.64e-7;
-    if ((detector == kDetFolded || detector == kDetResidue) && log2g == 4) return 12.0 * 1.19e-6;
-    return 12.0 * 2.67e-6;
+    double r = ((detector == kDetFolded || detector == kDetResidue) && log2g == 4) ? 1.19e-6 : 2.67e-6;
+    constexpr double kSinRef = 0.19509032201612825;  // sin(2 pi 1500 / 48000): bin 32 of 1024
+    if (!reinsch) {
+        double smin = 1.0;
+        for (uint32_t k = 0; k < c.k; ++k)
+            smin = std::min(smin, std::fabs(std::sin(2.0 * M_PI * c.freqs[k] / c.fs)));
+        if (smin < kSinRef) r *= (kSinRef / smin) * (kSinRef / smin);
+    }
+    const double G = (double)(1 << log2g);
+    if (G > 16.0) r *= std::sqrt(G / 16.0);
+    return 12.0 * r;
 }
 
 static int init_device_state(demod_t *st)
@@ -426,10 +448,19 @@ static int init_device_state(demod_t *st)
     st->wb_bursts = !(wb_env && std::strcmp(wb_env, "0") == 0);
     if (wb_env && std::atoi(wb_env) > 0) st->wb_force = std::min(std::atoi(wb_env), 64);
     if (st->rescue) {
-        const double sq = (double)c.n * 32768.0;  // sqrt(Q)
-        const double tau = amb_tau(st->detector, st->log2g);
-        st->amb_tq = (float)(tau * sq);
-        st->amb_floor = (float)(tau * tau * sq * sq / 16.0);
+        // stage 1 with Q (1 + 2e-4), so that it flags every window stage 2
+        // flags whatever the fp32 rounding of the energy sum (which the (1 +
+        // 1e-4) of amb_t2e covers); stage 2: amb_t2e E P_max, E the
+        // detector's energy sum (fold: of the N/8-sample folded window; FFT:
+        // Parseval's sum, already n sum x^2)
+        const double q = (double)c.n * (double)c.n * 1073741824.0 * (1.0 + 2e-4);
+        st->tau = amb_tau(st->detector, st->log2g, c, st->reinsch);
+        const double t2 = st->tau * st->tau;
+        st->amb_tq = (float)(st->tau * std::sqrt(q));
+        st->amb_floor = (float)(t2 * q / 16.0);
+        const double ne_per_e = st->detector == kDetFft ? 1.0
+                              : st->detector == kDetFolded ? (double)c.n / 8.0 : (double)c.n;
+        st->amb_t2e = (float)(t2 * ne_per_e * (1.0 + 1e-4));
     }
     st->slide_wt = 0;
     if (slide && st->detector == kDetGoertzel)
@@ -586,13 +617,21 @@ static int burst_count(const demod_t *st, size_t n_windows, bool mags)
     return (int)std::min<size_t>(std::max<size_t>((out + kBurstBytes - 1) / kBurstBytes, 4), 64);
 }
 
-// The plain bank's K = 2 chain path at n = 1024 (no segment sharing) re-decides
-// its flagged windows inside the detector kernel (rescue_row,
-// demod_internal.h): no rescue launch. Other Goertzel-family kernels keep it.
+// The direct Goertzel-family kernels at n = 1024 (plain bank, fold, residue;
+// any hop without segment sharing) re-decide their flagged windows inside the
+// detector kernel (rescue_row, demod_internal.h) from the tile they hold in
+// LDS: no rescue launch. Segment-shared windows (SLIDE, fold_slide_kernel)
+// and other window lengths keep rescue_kernel's launch; the FFT detector
+// always rescues in its own kernel (rescue_fft.h).
 static bool rescue_in_kernel(const demod_t *st)
 {
-    return st->detector == kDetGoertzel && st->log2g == 4 && st->cfg.k == 2 && st->slide_wt == 0 &&
-           !st->rescue_kernel_forced;
+    return st->detector != kDetFft && st->log2g == 4 && st->slide_wt == 0 && !st->rescue_kernel_forced;
+}
+
+double demod_rescue_tau(const demod_t *st)
+{
+    if (!st || !st->rescue) return 0.0;
+    return st->tau;
 }
 
 int demod_batch_launches(const demod_t *st, size_t n_windows, int with_mags)
@@ -655,6 +694,7 @@ static int enqueue_fft(demod_t *st, const int16_t *d_pcm, size_t n_windows, uint
     p.spec = d_spec;
     p.amb_tq = st->amb_tq;
     p.amb_floor = st->amb_floor;
+    p.amb_t2e = st->amb_t2e;
     // the FFT detector re-decides its flagged windows itself (rescue_fft.h):
     // one launch, no symbol scan
     p.rescue = st->rescue && st->rescue_launch ? 1 : 0;
@@ -699,6 +739,7 @@ static int enqueue_batch(demod_t *st, const int16_t *d_pcm, size_t n_windows, ui
     p.xcd_swizzle = 1;
     p.amb_tq = st->amb_tq;
     p.amb_floor = st->amb_floor;
+    p.amb_t2e = st->amb_t2e;
     const size_t per = launch_slice(st, n_windows, d_mag != nullptr);
     p.wb_bursts = burst_count(st, n_windows, d_mag != nullptr);
     p.rescue_inline = st->rescue && st->rescue_launch && rescue_in_kernel(st) ? 1 : 0;

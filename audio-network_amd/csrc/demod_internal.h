@@ -52,26 +52,60 @@ struct GoertzelParams {
     // launch; rcoef = 2 cos(2 pi f_k / fs) in double, the caller's tone order
     int rescue_inline;
     double rcoef[kMaxTones];
-    // decision rescue (rescue.hip): ambiguity test constants
-    float amb_tq;            // threshold = amb_tq * sqrt(P_max); 0: no flagging
-    float amb_floor;         // 0 < P_max < amb_floor: always ambiguous
+    // decision rescue (rescue.hip): ambiguity test constants.
+    // Stage 1 (every window, no per-sample work): the int16 worst case
+    // Q >= NE, threshold amb_tq sqrt(P_max), amb_tq = tau sqrt(Q); 0: no
+    // flagging. Stage 2 (only rows stage 1 flags): the window's own energy,
+    // threshold^2 = amb_t2e E P_max with E the detector's energy sum (plain
+    // bank / residue: sum x^2, amb_t2e = tau^2 n; fold: sum xf^2 of the folded
+    // window, tau^2 n / 8), floor amb_t2e E / 16.
+    float amb_tq;
+    float amb_floor;         // stage 1: 0 < P_max < amb_floor is ambiguous
+    float amb_t2e;
 };
 
 // Decision rescue. A detector's fp32 powers carry an error
-// |dP_k| <= r sqrt(P_max NE), NE = n sum x^2 <= Q = n^2 2^30 for int16 input
-// (r measured per detector, scripts/precision_probe.py). Where the fp32 top-2
-// margin is below amb_tq sqrt(P_max) (amb_tq = tau sqrt(Q), tau = 12 r), or
-// P_max is so small that the second-order term could dominate, the fp32
-// argmax may differ from the exact one: the detector sets kSymAmbiguous on
-// the window's symbol and rescue_kernel re-decides it with the definition's
-// double-precision arithmetic (bit-identical to oracle/fsk_oracle.c).
+// |dP_k| <= r sqrt(P_max NE), NE the window's energy scale (n sum x^2; for
+// the fold detector (n/8) sum xf^2 of the folded window it transforms; r per
+// detector and tone plan, demod_api.cpp amb_tau, checked by
+// tests/test_gpu_error_model.py). Where the fp32 top-2 margin is below
+// tau sqrt(NE P_max) (tau = 12 r: two powers' errors, x 6), or P_max is so
+// small that the second-order term could dominate, the fp32 argmax may
+// differ from the exact one: the detector marks the window ambiguous and the
+// rescue (rescue_row in the detector, or rescue_kernel) re-decides it with
+// the definition's double-precision arithmetic (bit-identical to
+// oracle/fsk_oracle.c). The test runs in two stages: NE <= Q = n^2 2^30 for
+// int16 input, so a window whose margin clears tau sqrt(Q P_max) clears the
+// exact test too and no per-sample work is spent on it (stage 1); only rows
+// stage 1 flags compute their energy (stage 2), so quiet input (dithered
+// silence, idle-channel noise) is not flagged wholesale.
 // P_max == 0 (every tone power exactly zero: silence) is decided as a tie
 // (tone 0) without a rescue.
 constexpr uint8_t kSymAmbiguous = 0x80;
 
+// stage 1: margin within tau sqrt(Q P_max) (amb_tq = tau sqrt(Q))
 __device__ __forceinline__ bool amb_margin(float p1, float p2, float tq, float fl)
 {
     return tq > 0.f && p1 > 0.f && (p1 - p2 < tq * __builtin_amdgcn_sqrtf(p1) || p1 < fl);
+}
+
+// stage 2: (p1 - p2)^2 < t2e E p1, or p1 below the floor t2e E / 16
+__device__ __forceinline__ bool amb_energy(float p1, float p2, float e, float t2e)
+{
+    const float c = t2e * e, d = p1 - p2;
+    return p1 > 0.f && (d * d < c * p1 || 16.f * p1 < c);
+}
+
+// The two stages over a wave: `amb1` is this lane's stage-1 verdict (false for
+// lanes without a real window); efn() returns the lane's row energy E and is
+// called by every lane (it may shuffle), only when some lane of the wave has
+// amb1 set (a wave-uniform branch: nothing is spent on unflagged waves).
+template <typename EFn>
+__device__ __forceinline__ bool amb_two_stage(bool amb1, float p1, float p2, float t2e, EFn efn)
+{
+    if (__ballot(amb1) == 0) return false;
+    const float e = efn();
+    return amb1 && amb_energy(p1, p2, e, t2e);
 }
 
 // Sequential argmax (ties to the lowest k) that also keeps the runner-up, for
@@ -96,14 +130,50 @@ __device__ __forceinline__ int chain_argmax(const float (&P)[K], float &p1, floa
     return arg;
 }
 
-// The symbol byte a chain decision stores (K >= 2: ambiguous windows flagged).
-template <int K>
-__device__ __forceinline__ uint8_t chain_symbol(const float (&P)[K], float tq, float fl)
+// A chain decision (K >= 2 flags ambiguous windows): the argmax, and the
+// two-stage ambiguity verdict (stage 2 via efn, see amb_two_stage; `live` =
+// the lane's window exists).
+template <int K, typename EFn>
+__device__ __forceinline__ int chain_decide(const float (&P)[K], bool live, float tq, float fl, float t2e,
+                                            EFn efn, bool &amb)
 {
     float p1, p2;
     const int arg = chain_argmax<K>(P, p1, p2);
-    const bool amb = K >= 2 && amb_margin(p1, p2, tq, fl);
-    return (uint8_t)(arg | (amb ? kSymAmbiguous : 0));
+    amb = K >= 2 && amb_two_stage(live && amb_margin(p1, p2, tq, fl), p1, p2, t2e, efn);
+    return arg;
+}
+
+// Sum of squares of the 64 int16 samples of one lane segment, 16-byte chunks
+// read by `chunk(i)` (i < 8), as fp32 (each square and partial sum rounded:
+// relative error < 1e-5, covered by the host's (1 + 1e-4) in amb_t2e).
+typedef unsigned int u32x4e __attribute__((ext_vector_type(4)));
+typedef float f32x2e __attribute__((ext_vector_type(2)));
+template <typename Chunk>
+__device__ __forceinline__ float seg_energy(Chunk chunk)
+{
+    f32x2e a = {0.f, 0.f}, b = {0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const u32x4e d = chunk(i);
+        const unsigned d4[4] = {d.x, d.y, d.z, d.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const f32x2e x = {(float)(int)(short)(d4[q] & 0xFFFFu), (float)((int)d4[q] >> 16)};
+            if (q & 1) b = __builtin_elementwise_fma(x, x, b);
+            else a = __builtin_elementwise_fma(x, x, a);
+        }
+    }
+    return (a.x + a.y) + (b.x + b.y);
+}
+
+// Sum over the 16 lanes of a row (n = 1024 windows), every lane the same total.
+__device__ __forceinline__ float row_sum16(float v)
+{
+    v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, true));
+    v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, true));
+    v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x141, 0xF, 0xF, true));
+    v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x140, 0xF, 0xF, true));
+    return v;
 }
 
 // Output store; NTS = non-temporal (streamed once, never re-read by the kernel).
@@ -136,35 +206,42 @@ __device__ __forceinline__ long long tile_block(int swz)
 // writes that XCD's L2 back with an agent-scope release, so the output lines
 // leave in a few bursts instead of trickling out between the input's reads;
 // the launch slices this replaces paid a drain and a ramp per slice.
-// In-kernel decision rescue of one window by its 16-lane row (round 3, late;
-// goertzel.hip K <= 2 at n = 1024): lane seg < K runs tone seg's recurrence
-// in double over the window's n samples with exactly rescue_kernel's
-// operations and order (so exactly oracle/fsk_oracle.c's), the row's argmax
-// (ties to the lowest tone) replaces the flagged symbol, and the powers
-// (rounded to fp32) the magnitudes. Every lane of the wave calls it (the
-// shuffles); rows with amb_row false change nothing.
-template <int K>
+// In-kernel decision rescue of one window by its 16-lane row (n = 1024; round
+// 3 for the 2-FSK plain bank, round 4 every direct Goertzel-family kernel at
+// n = 1024): lane seg < K runs tone seg's recurrence in double over the
+// window's 1024 samples with exactly rescue_kernel's operations and order (so
+// exactly oracle/fsk_oracle.c's), the row's argmax (ties to the lowest tone)
+// replaces the symbol, and the powers (rounded to fp32) the magnitudes.
+// chunk(q) returns the window's 16-byte chunk q (samples 8q .. 8q + 7) from
+// wherever the kernel holds the tile (its LDS slice: no global round trip per
+// chunk; the next chunk's read is issued before the current one's 24
+// dependent double operations). Every lane of the wave calls it (the
+// shuffles); rows with amb_row false change nothing. The detector leaves the
+// symbol and magnitudes of a flagged row to this function (no second store).
+template <int K, typename Chunk>
 __device__ __forceinline__ void rescue_row(const GoertzelParams &p, long long w, int seg, int lane,
-                                           bool amb_row, int n)
+                                           bool amb_row, Chunk chunk)
 {
 #pragma clang fp contract(off)
-    typedef unsigned int u32x4r __attribute__((ext_vector_type(4)));
     double P = 0.0;
     if (amb_row && seg < K) {
         const double c = p.rcoef[seg];
         double s1 = 0.0, s2 = 0.0;
-        const u32x4r *xs = reinterpret_cast<const u32x4r *>(p.pcm + w * p.hop);
-        for (int q = 0; q < n / 8; ++q) {
-            const u32x4r d = xs[q];
+        u32x4e d = chunk(0);
+        for (int q = 0; q < 128; ++q) {
+            const u32x4e nx = chunk(q < 127 ? q + 1 : q);
             const unsigned d4[4] = {d.x, d.y, d.z, d.w};
+            double xv[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) xv[e] = (double)(short)((d4[e >> 1] >> (16 * (e & 1))) & 0xFFFFu);
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
-                const double x = (double)(short)((d4[e >> 1] >> (16 * (e & 1))) & 0xFFFFu);
-                double s = x + c * s1;
+                double s = xv[e] + c * s1;
                 s = s - s2;
                 s2 = s1;
                 s1 = s;
             }
+            d = nx;
         }
         const double a = s1 * s1 + s2 * s2;
         const double b = c * s1;
@@ -208,9 +285,10 @@ struct FftParams {
     uint8_t *sym;
     float *mag;              // [n_windows][k] or nullptr
     float *spec;             // [n_windows][513] or nullptr
-    float amb_tq;            // decision rescue, as GoertzelParams
-    float amb_floor;
-    int rescue;              // 1: flagged windows are re-decided in the kernel (rescue_fft.h)
+    float amb_tq;            // decision rescue, as GoertzelParams (stage 2:
+    float amb_floor;         // E = 2 x the window's 513 bin powers >= n sum x^2,
+    float amb_t2e;           // Parseval, amb_t2e = tau^2)
+    int rescue;            // 1: flagged windows are re-decided in the kernel (rescue_fft.h)
     const double *rtw;       // rescue: [1023] (cos, sin), stage len at len / 2 - 1 + j
 };
 

@@ -1118,7 +1118,27 @@ __device__ __attribute__((always_inline)) inline void fft1024_quad_body(const Ff
         float mx;
         arg = (int)ws_argmax_m<false>(__float_as_uint(pk), owns, arg, 0u, false, 0, mx);
         // decision rescue: a runner-up within the threshold
-        const bool amb = p.k >= 2 && ws_ambiguous(mx, pk, owns, pk2, pk2 >= 0.f, p.amb_tq, p.amb_floor);
+        // decision rescue, two stages: the int16 worst case,
+        // then (only waves with a stage-1 flag) the window's energy by
+        // Parseval, E = 2 x the sum of its 513 bin powers >= n sum x^2 (the
+        // row's lanes hold every bin once, bin 256 twice in the register
+        // tuple: an upper bound either way)
+        auto efn = [&]() {
+            float e = 0.f;
+            if constexpr (SPEC && SPL) {
+                for (int i = tt; i < 513; i += 16) e += pw[rowb + i];
+            } else if constexpr (SPEC) {
+                for (int i = t; i < 513; i += 16) e += pq[quad_slot(i)];
+            } else {
+                f2 a = {0.f, 0.f};
+#pragma unroll
+                for (int i = 0; i < 32; i += 2) a = a + f2{pv[i], pv[i + 1]};
+                e = (a.x + a.y) + (l0 ? px.x + px.y : 0.f);
+            }
+            return 2.f * row_sum16(e);
+        };
+        const bool amb = p.k >= 2 && ws_amb_two_stage(mx, pk, owns, pk2, pk2 >= 0.f, live, p.amb_tq,
+                                                      p.amb_floor, p.amb_t2e, efn);
         if (live && t == 0) p.sym[w] = (uint8_t)(arg | (amb ? kSymAmbiguous : 0));
         if constexpr (SPEC && SPL) {
             if constexpr (PF == 2) {

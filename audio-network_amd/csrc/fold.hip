@@ -50,14 +50,27 @@ __device__ __forceinline__ float group_sum_f(float v, int log2g)
 // epilogue. F16: c16 / r hold this lane's four slots (fold_tile_kernel F16).
 // fold_tile_kernel and fold_slide_kernel both end here, so a window's result
 // does not depend on which of them formed its sums.
+// Stage 2 of the ambiguity test uses the energy of the folded window the
+// detector transforms, E = sum xf^2 over its N/8 positions (the lanes' acc;
+// amb_t2e = tau^2 N/8): the fold itself is exact, so the fp32 error scales with
+// the folded window, and E <= 8 sum x^2. defer: flagged rows are left to the
+// kernel's rescue_row. Returns the row's ambiguity verdict.
 template <int K, bool F16, int MST = -1>
-__device__ __forceinline__ void fold_decide(const int (&acc)[8], const float4 *r,
+__device__ __forceinline__ bool fold_decide(const int (&acc)[8], const float4 *r,
                                             const float (&c16)[4], int lane, long long w,
-                                            bool live, const GoertzelParams &p)
+                                            bool live, const GoertzelParams &p, bool defer)
 {
     float xf[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) xf[q] = (float)acc[q];
+    auto efn = [&]() {
+        f32x2f a = {0.f, 0.f};
+#pragma unroll
+        for (int q = 0; q < 8; q += 2)
+            a = __builtin_elementwise_fma(f32x2f{xf[q], xf[q + 1]}, f32x2f{xf[q], xf[q + 1]}, a);
+        return row_sum16(a.x + a.y);
+    };
+    const AmbTest at{p.amb_tq, p.amb_floor, p.amb_t2e, defer};
     if constexpr (F16) {
         const float sg = (lane & 8) ? -1.f : 1.f;
         float y[8];
@@ -87,8 +100,7 @@ __device__ __forceinline__ void fold_decide(const int (&acc)[8], const float4 *r
             xr[2 * h + 1] = X1.x;
             xi[2 * h + 1] = X1.y;
         }
-        window_sum_decide_split8<true, MST>(xr, xi, lane, w, live, p.sym, p.mag, p.perm, p.amb_tq,
-                                       p.amb_floor);
+        return window_sum_decide_split8<true, MST>(xr, xi, lane, w, live, p.sym, p.mag, p.perm, at, efn);
     } else {
         float xr[K], xi[K];
         constexpr int HP = K / 2;  // packed tone pairs; an odd last tone runs scalar
@@ -118,7 +130,7 @@ __device__ __forceinline__ void fold_decide(const int (&acc)[8], const float4 *r
             xr[K - 1] = r[K - 1].x * s1 - r[K - 1].z * s2;
             xi[K - 1] = r[K - 1].y * s1 - r[K - 1].w * s2;
         }
-        window_sum_decide<K, false, MST>(xr, xi, lane, w, live, p.sym, p.mag, 0, p.amb_tq, p.amb_floor);
+        return window_sum_decide<K, false, MST>(xr, xi, lane, w, live, p.sym, p.mag, 0, at, efn);
     }
 }
 
@@ -229,7 +241,16 @@ __global__ __launch_bounds__(64 * WPB) void fold_tile_kernel(GoertzelParams p)
         }
         if constexpr (F16 || (WS && LOG2G == 4 && !PK && !ROTLDS)) {
             const long long w = wbase + win_in_tile;
-            fold_decide<K, F16, MST>(acc, r, c16, lane, w, w < p.n_windows, p);
+            const bool live = w < p.n_windows;
+            // in-kernel decision rescue (LDST: the tile is still in the wave's
+            // LDS slice, window u's chunks at 128 u ..)
+            constexpr bool kInline = LDST && K >= 2;
+            const bool defer = kInline && p.rescue_inline;
+            const bool amb = fold_decide<K, F16, MST>(acc, r, c16, lane, w, live, p, defer);
+            if constexpr (kInline) {
+                if (defer && __ballot(amb && live) != 0)
+                    rescue_row<K>(p, w, j, lane, amb && live, [&](int q) { return wl[128 * win_in_tile + q]; });
+            }
             continue;
         }
         float xf[8];
@@ -274,8 +295,14 @@ __global__ __launch_bounds__(64 * WPB) void fold_tile_kernel(GoertzelParams p)
                 xi[k] = rk.y * t1[k] - rk.w * t2[k];
             }
             const long long w = wbase + win_in_tile;
-            window_sum_decide<K, false, MST>(xr, xi, lane, w, w < p.n_windows, p.sym, p.mag, 0, p.amb_tq,
-                                 p.amb_floor);
+            auto efn = [&]() {
+                float e = 0.f;
+#pragma unroll
+                for (int q = 0; q < 8; ++q) e = fmaf(xf[q], xf[q], e);
+                return row_sum16(e);
+            };
+            window_sum_decide<K, false, MST>(xr, xi, lane, w, w < p.n_windows, p.sym, p.mag, 0,
+                                             AmbTest{p.amb_tq, p.amb_floor, p.amb_t2e, false}, efn);
             continue;
         }
         float P[K];
@@ -297,8 +324,16 @@ __global__ __launch_bounds__(64 * WPB) void fold_tile_kernel(GoertzelParams p)
         }
 
         const long long w = wbase + win_in_tile;
+        auto efn = [&]() {
+            float e = 0.f;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) e = fmaf(xf[q], xf[q], e);
+            return group_sum_f(e, log2g);
+        };
+        bool amb;
+        const int arg = chain_decide<K>(P, w < p.n_windows, p.amb_tq, p.amb_floor, p.amb_t2e, efn, amb);
         if (w < p.n_windows) {
-            if (j == 0) out_store<NTS>(p.sym + w, chain_symbol<K>(P, p.amb_tq, p.amb_floor));
+            if (j == 0) out_store<NTS>(p.sym + w, (uint8_t)(arg | (amb ? kSymAmbiguous : 0)));
             if (p.mag) {
 #pragma unroll
                 for (int k = 0; k < K; ++k)
@@ -437,7 +472,7 @@ __global__ __launch_bounds__(64 * kPlainWPB) void fold_slide_kernel(GoertzelPara
                 }
             }
             const long long w = wbase + u;
-            fold_decide<K, F16>(acc, r, c16, lane, w, w < p.n_windows, p);
+            fold_decide<K, F16>(acc, r, c16, lane, w, w < p.n_windows, p, false);
         }
         // the next tile's samples overwrite this one's
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");

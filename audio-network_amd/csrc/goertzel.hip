@@ -49,6 +49,13 @@ __device__ __forceinline__ float group_sum(float v, int log2g)
     return v;
 }
 
+// 16-byte chunk i of the samples at sp (plain load: the lines were just
+// streamed in, L2 may still hold them)
+__device__ __forceinline__ u32x4 global_chunk(const int16_t *sp, int i)
+{
+    return reinterpret_cast<const u32x4 *>(sp)[i];
+}
+
 // LOG2G >= 0: lane-group size fixed at compile time (4 <=> n = 1024);
 // LOG2G == -1: taken from p.log2g at run time.
 // Tunables (defaults are the shipped configuration, chosen by scripts/probe):
@@ -293,8 +300,17 @@ __global__ __launch_bounds__(64 * WPB) void goertzel_tile_kernel(GoertzelParams 
                         xi[k] = fmaf(r[k].y, z.x, -(r[k].w * z.y));
                     }
                 }
+                // stage 2 of the ambiguity test: the window's energy from its
+                // segments, re-read from L2 (the samples in LDS are gone)
+                const int16_t *sp = p.pcm + tt * wins_per_tile * p.hop + 64 * sg;
+                auto efn = [&]() {
+                    return group_sum(seg_energy([&](int i) {
+                        return live ? global_chunk(sp, i) : u32x4{0u, 0u, 0u, 0u};
+                    }), 4);
+                };
                 if constexpr (WS) {
-                    window_sum_decide<K>(xr, xi, lane, w, live, p.sym, p.mag, 0, p.amb_tq, p.amb_floor);
+                    window_sum_decide<K>(xr, xi, lane, w, live, p.sym, p.mag, 0,
+                                         AmbTest{p.amb_tq, p.amb_floor, p.amb_t2e, false}, efn);
                 } else {
                     float P[K];
 #pragma unroll
@@ -302,8 +318,10 @@ __global__ __launch_bounds__(64 * WPB) void goertzel_tile_kernel(GoertzelParams 
                         const float re = group_sum(xr[k], 4), im = group_sum(xi[k], 4);
                         P[k] = fmaf(re, re, im * im);
                     }
+                    bool amb;
+                    const int arg = chain_decide<K>(P, live, p.amb_tq, p.amb_floor, p.amb_t2e, efn, amb);
                     if (live) {
-                        if (seg == 0) out_store<NTS>(p.sym + w, chain_symbol<K>(P, p.amb_tq, p.amb_floor));
+                        if (seg == 0) out_store<NTS>(p.sym + w, (uint8_t)(arg | (amb ? kSymAmbiguous : 0)));
                         if (p.mag) {
 #pragma unroll
                             for (int k = 0; k < K; ++k)
@@ -318,6 +336,31 @@ __global__ __launch_bounds__(64 * WPB) void goertzel_tile_kernel(GoertzelParams 
             return;
         }
         const long long w = tt * wins_per_tile + win_in_tile;
+        const bool live = w < p.n_windows;
+        // stage 2 of the ambiguity test (demod_internal.h): this lane's 64
+        // samples again (the tile is still in the wave's LDS slice, or from
+        // L2 for DIRECT), summed over the window's lanes
+        auto efn = [&]() {
+            float e;
+            if constexpr (DIRECT) {
+                const int16_t *sp = p.pcm + w * p.hop + 64 * seg;
+                e = seg_energy([&](int i) { return live ? global_chunk(sp, i) : u32x4{0u, 0u, 0u, 0u}; });
+            } else {
+                // an opaque offset: the recurrence read the same LDS bytes,
+                // and reusing those values would keep 32 VGPRs live across it
+                int off = rd_off;
+                asm volatile("" : "+v"(off));
+                e = seg_energy([&](int i) { return *reinterpret_cast<const u32x4 *>(wl + off + 16 * i); });
+            }
+            return group_sum(e, log2g);
+        };
+        // in-kernel rescue (n = 1024, tile in LDS): the window's chunk q
+        auto chunk = [&](int q) {
+            return *reinterpret_cast<const u32x4 *>(wl + (16 * win_in_tile + (q >> 3)) * kLdsSegStride +
+                                                    (q & 7) * 16);
+        };
+        constexpr bool kInline = LOG2G == 4 && !DIRECT && K >= 2 && K <= 16;
+        const bool defer = kInline && p.rescue_inline;
         if constexpr (WS && LOG2G == 4) {
             float xr[K], xi[K];
 #pragma unroll
@@ -329,8 +372,11 @@ __global__ __launch_bounds__(64 * WPB) void goertzel_tile_kernel(GoertzelParams 
                 xr[k] = X.x;
                 xi[k] = X.y;
             }
-            window_sum_decide<K>(xr, xi, lane, w, w < p.n_windows, p.sym, p.mag, 0, p.amb_tq,
-                                 p.amb_floor);
+            const bool amb = window_sum_decide<K>(xr, xi, lane, w, live, p.sym, p.mag, 0,
+                                                  AmbTest{p.amb_tq, p.amb_floor, p.amb_t2e, defer}, efn);
+            if constexpr (kInline) {
+                if (defer && __ballot(amb && live) != 0) rescue_row<K>(p, w, seg, lane, amb && live, chunk);
+            }
             return;
         }
         float P[K];
@@ -343,23 +389,20 @@ __global__ __launch_bounds__(64 * WPB) void goertzel_tile_kernel(GoertzelParams 
             P[k] = fmaf(re, re, im * im);
         }
 
-        const uint8_t sv = chain_symbol<K>(P, p.amb_tq, p.amb_floor);
-        if (w < p.n_windows) {
-            if (seg == 0) out_store<NTS>(p.sym + w, sv);
+        bool amb;
+        const int arg = chain_decide<K>(P, live, p.amb_tq, p.amb_floor, p.amb_t2e, efn, amb);
+        if (live && !(amb && defer)) {
+            if (seg == 0) out_store<NTS>(p.sym + w, (uint8_t)(arg | (amb ? kSymAmbiguous : 0)));
             if (p.mag) {
 #pragma unroll
                 for (int k = 0; k < K; ++k)
                     if ((k & (g - 1)) == seg) out_store<NTS>(p.mag + w * K + k, P[k]);
             }
         }
-        if constexpr (LOG2G == 4 && K >= 2 && K <= 16) {
-            // decision rescue in the kernel (demod_internal.h rescue_row): the
-            // row's verdict is its lane 0's (the all-reduced powers may round
-            // differently in other lanes)
-            if (p.rescue_inline) {
-                const bool amb_row = w < p.n_windows && (__shfl((int)sv, lane & 48) & kSymAmbiguous);
-                if (__ballot(amb_row) != 0) rescue_row<K>(p, w, seg, lane, amb_row, n);
-            }
+        if constexpr (kInline) {
+            // decision rescue in the kernel (demod_internal.h rescue_row); every
+            // lane of a row holds the same all-reduced powers, so the same verdict
+            if (defer && __ballot(amb && live) != 0) rescue_row<K>(p, w, seg, lane, amb && live, chunk);
         }
     };
 

@@ -15,7 +15,9 @@
 // fp32) over the window's magnitudes. (The FFT detector rescues its windows
 // inside its own kernel: rescue_fft.h.)
 //
-// Layout: one wave per 4096 consecutive windows. It first reads
+// Layout: one wave per 512 consecutive windows (round 3: 4096; with every
+// window of a chunk flagged a wave served them one group after another, so
+// eight times more waves bound the worst case eight times lower). It first reads
 // their symbol bytes (dword loads, all in flight at once) and exits if none is
 // flagged — the common case: one short pass over 1 byte per window. Otherwise
 // it compacts the flagged windows, in order, into an LDS list. Goertzel:
@@ -28,7 +30,7 @@
 namespace fskd {
 
 // windows whose symbols one wave scans
-constexpr int kRescueChunk = 4096;
+constexpr int kRescueChunk = 512;
 constexpr int kRescueLdsBytes = 32768;    // Goertzel: staged samples per group
 
 typedef unsigned int u32x4q __attribute__((ext_vector_type(4)));

@@ -352,9 +352,47 @@ void residue_tile_kernel(GoertzelParams p)
             xi[k] = X.y;
         }
         const long long w = wbase + win_in_tile;
+        const bool live = w < p.n_windows;
         if constexpr (WS && LOG2G == 4) {
-            window_sum_decide<K, DCLS>(xr, xi, lane, w, w < p.n_windows, p.sym, p.mag, p.perm,
-                                       p.amb_tq, p.amb_floor);
+            // Stage 2 of the ambiguity test and the in-kernel rescue both need
+            // the raw samples, which only lived in registers: the tile is read
+            // again (L2 / HBM), only by waves with a stage-1 flag, into the
+            // wave's LDS slice (the class file is dead by now) in the linear
+            // layout (window u's chunks at 128 u ..); lane j of a row sums
+            // chunks 8 j .. 8 j + 7 of its window.
+            u32x4r *wl = reinterpret_cast<u32x4r *>(zw - lane);
+            auto efn = [&]() {
+                long long bytes = ((p.n_windows - wbase - 1) * p.hop + n) * 2;
+                if (bytes > 0x7FFFFFF0LL) bytes = 0x7FFFFFF0LL;
+                __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                    (void *)(p.pcm + wbase * p.hop), (short)0, (int)bytes, 0x00020000);
+                u32x4r v2[8];
+#pragma unroll
+                for (int m = 0; m < 8; ++m) {
+                    const int q = 64 * m + lane;
+                    v2[m] = __builtin_amdgcn_raw_buffer_load_b128(
+                        rs, (int)(((long long)(q >> 7) * p.hop + (long long)(q & 127) * 8) * 2), 0, 0);
+                }
+                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+#pragma unroll
+                for (int m = 0; m < 8; ++m) wl[64 * m + lane] = v2[m];
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                return row_sum16(seg_energy([&](int i) { return wl[128 * win_in_tile + 8 * j + i]; }));
+            };
+            const bool defer = K >= 2 && p.rescue_inline;
+            const bool amb = window_sum_decide<K, DCLS>(xr, xi, lane, w, live, p.sym, p.mag, p.perm,
+                                                        AmbTest{p.amb_tq, p.amb_floor, p.amb_t2e, defer},
+                                                        efn);
+            if constexpr (K >= 2) {
+                if (defer && __ballot(amb && live) != 0)
+                    rescue_row<K>(p, w, j, lane, amb && live, [&](int q) { return wl[128 * win_in_tile + q]; });
+            }
+            // the next tile's class file overwrites the slice
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            __builtin_amdgcn_wave_barrier();
             continue;
         }
         static_assert(!DCLS || (WS && LOG2G == 4), "DCLS un-permutes in the window_sum epilogue");
@@ -365,8 +403,16 @@ void residue_tile_kernel(GoertzelParams p)
             const float im = group_sum_r(xi[k], log2g);
             P[k] = fmaf(re, re, im * im);
         }
-        if (w < p.n_windows) {
-            if (j == 0) p.sym[w] = chain_symbol<K>(P, p.amb_tq, p.amb_floor);
+        // stage 2: the lane's chunks again (L2 / HBM), only on flagged waves
+        auto efn = [&]() {
+            u32x4r v2[8];
+            load_tile(t, v2);
+            return group_sum_r(seg_energy([&](int i) { return v2[i]; }), log2g);
+        };
+        bool amb;
+        const int arg = chain_decide<K>(P, live, p.amb_tq, p.amb_floor, p.amb_t2e, efn, amb);
+        if (live) {
+            if (j == 0) p.sym[w] = (uint8_t)(arg | (amb ? kSymAmbiguous : 0));
             if (p.mag) {
 #pragma unroll
                 for (int k = 0; k < K; ++k)

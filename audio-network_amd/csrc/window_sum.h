@@ -155,11 +155,12 @@ __device__ __forceinline__ unsigned ws_argmax(unsigned pb0, bool ok0, int o0, un
 // per-row answer goes back to the lanes as a lane mask (inverse ballot), so
 // the count costs scalar instructions instead of a 16-lane DPP reduction
 // (FFT detector: ~8 VALU fewer per 4-window group).
-__device__ __forceinline__ bool ws_ambiguous(float mx, float a0, bool ok0, float a1, bool ok1,
-                                             float tq, float fl)
+// Threshold^2 = t2c mx, floor flc (stage 1: t2c = tq^2, flc = fl; stage 2:
+// t2c = t2e E, flc = t2e E / 16, E the row's energy; demod_internal.h).
+__device__ __forceinline__ bool ws_ambiguous_t(float mx, float a0, bool ok0, float a1, bool ok1,
+                                               float t2c, float flc)
 {
-    if (!(tq > 0.f)) return false;
-    const float t2 = (tq * tq) * mx;
+    const float t2 = t2c * mx;
     const float d0 = mx - a0, d1 = mx - a1;
     const bool n0 = ok0 && d0 * d0 < t2, n1 = ok1 && d1 * d1 < t2;
     const unsigned long long any = __ballot(n0 || n1), two = __ballot(n0 && n1);
@@ -169,20 +170,52 @@ __device__ __forceinline__ bool ws_ambiguous(float mx, float a0, bool ok0, float
         const unsigned f = (unsigned)(any >> (16 * r)) & 0xFFFFu;
         if ((f & (f - 1u)) != 0u || ((two >> (16 * r)) & 0xFFFFull) != 0) rows |= 0xFFFFull << (16 * r);
     }
-    return mx > 0.f && (__builtin_amdgcn_inverse_ballot_w64(rows) || mx < fl);
+    return mx > 0.f && (__builtin_amdgcn_inverse_ballot_w64(rows) || mx < flc);
 }
+
+__device__ __forceinline__ bool ws_ambiguous(float mx, float a0, bool ok0, float a1, bool ok1,
+                                             float tq, float fl)
+{
+    if (!(tq > 0.f)) return false;
+    return ws_ambiguous_t(mx, a0, ok0, a1, ok1, tq * tq, fl);
+}
+
+// Both stages over the wave (demod_internal.h amb_two_stage): stage 1 with
+// the int16 worst case, stage 2 only if some live row of the wave is flagged
+// (efn: the row energy, called by every lane). Row-uniform result.
+template <typename EFn>
+__device__ __forceinline__ bool ws_amb_two_stage(float mx, float a0, bool ok0, float a1, bool ok1,
+                                                 bool live, float tq, float fl, float t2e, EFn efn)
+{
+    const bool amb1 = ws_ambiguous(mx, a0, ok0, a1, ok1, tq, fl) && live;
+    if (__ballot(amb1) == 0) return false;
+    const float c = t2e * efn();
+    const bool amb2 = ws_ambiguous_t(mx, a0, ok0, a1, ok1, c, c * 0.0625f);  // every lane: ballots inside
+    return amb1 && amb2;
+}
+
+// The decision rescue's ambiguity test in an epilogue (demod_internal.h):
+// stage-1 tq / fl (tq = 0: off), stage-2 t2e, and `defer`: the kernel
+// re-decides flagged rows itself (rescue_row), so their symbol and magnitudes
+// are left to it; otherwise a flagged symbol leaves with kSymAmbiguous set
+// (rescue_kernel, or FSKD_NO_RESCUE=flags).
+struct AmbTest {
+    float tq, fl, t2e;
+    bool defer;
+};
 
 // X[k] = this lane's partial (re, im) of tone k. Writes the symbol of window
 // w (lane j == 0) and, if mag, its K magnitudes; `live` = w is a real window.
 // PERM: the kernel's tone slot s holds the host's tone (perm >> 4 s) & 15
 // (residue.hip DCLS); magnitudes, the tie rule and the symbol use that index.
-// tq / fl: the decision rescue's ambiguity test (tq = 0: off); an ambiguous
-// window's symbol carries kSymAmbiguous for rescue_kernel.
-template <int K, bool PERM = false, int MST = -1>
-__device__ __forceinline__ void window_sum_decide(const float (&re)[K], const float (&im)[K],
+// efn: the row's energy for stage 2 of the ambiguity test (called by every
+// lane, only when stage 1 flags some live row of the wave). Returns whether
+// the row is ambiguous (row-uniform).
+template <int K, bool PERM = false, int MST = -1, typename EFn>
+__device__ __forceinline__ bool window_sum_decide(const float (&re)[K], const float (&im)[K],
                                                   int lane, long long w, bool live,
                                                   uint8_t *sym, float *mag,
-                                                  unsigned long long perm, float tq, float fl)
+                                                  unsigned long long perm, const AmbTest &at, EFn efn)
 {
     static_assert(K >= 1 && K <= 16, "tones");
     constexpr int KP = K <= 1 ? 1 : K <= 2 ? 2 : K <= 4 ? 4 : K <= 8 ? 8 : 16;
@@ -214,16 +247,19 @@ __device__ __forceinline__ void window_sum_decide(const float (&re)[K], const fl
     const bool ok1 = V > 16 && re_lane && t0 + 8 < K;
     const int o0 = PERM ? (int)((perm >> (4 * t0)) & 15u) : t0;
     const int o1 = PERM ? (int)((perm >> (4 * ((t0 + 8) & 15))) & 15u) : t0 + 8;
-    constexpr int MS = MST >= 0 ? MST : kMagStore<K>;
-    if (live && mag) {
-        if (ok0) mag_store<MS>(mag, w * K + o0, P0);
-        if (ok1) mag_store<MS>(mag, w * K + o1, P1);
-    }
     float mx;
     const unsigned arg = ws_argmax_m<(V > 16)>(__float_as_uint(P0), ok0, o0, __float_as_uint(P1),
                                                ok1, o1, mx);
-    const bool amb = K >= 2 && ws_ambiguous(mx, P0, ok0, P1, ok1, tq, fl);
-    if (live && j == 0) sym[w] = (uint8_t)(arg | (amb ? kSymAmbiguous : 0u));
+    const bool amb = K >= 2 && ws_amb_two_stage(mx, P0, ok0, P1, ok1, live, at.tq, at.fl, at.t2e, efn);
+    constexpr int MS = MST >= 0 ? MST : kMagStore<K>;
+    if (live && !(amb && at.defer)) {
+        if (mag) {
+            if (ok0) mag_store<MS>(mag, w * K + o0, P0);
+            if (ok1) mag_store<MS>(mag, w * K + o1, P1);
+        }
+        if (j == 0) sym[w] = (uint8_t)(arg | (amb ? kSymAmbiguous : 0u));
+    }
+    return amb;
 }
 
 // The same epilogue for K = 8 when the kernel has already split the tones by
@@ -231,11 +267,12 @@ __device__ __forceinline__ void window_sum_decide(const float (&re)[K], const fl
 // tones 4-7, each over the whole window): that is the state after the first
 // reduce-scatter stage, so only stages 2, 1, 0 run (21 instead of 45
 // instructions). re/im = this lane's 4 tones (slots 4 * bit3 + s).
-template <bool PERM = false, int MST = -1>
-__device__ __forceinline__ void window_sum_decide_split8(const float (&re)[4], const float (&im)[4],
+template <bool PERM = false, int MST = -1, typename EFn>
+__device__ __forceinline__ bool window_sum_decide_split8(const float (&re)[4], const float (&im)[4],
                                                          int lane, long long w, bool live,
                                                          uint8_t *sym, float *mag,
-                                                         unsigned long long perm, float tq, float fl)
+                                                         unsigned long long perm, const AmbTest &at,
+                                                         EFn efn)
 {
     constexpr int K = 8;
     float v[8];
@@ -254,12 +291,15 @@ __device__ __forceinline__ void window_sum_decide_split8(const float (&re)[4], c
     const float sq = v[0] * v[0];
     const float P0 = sq + ws_dpp<0xB1>(sq);
     const int o0 = PERM ? (int)((perm >> (4 * t0)) & 15u) : t0;
-    constexpr int MS = MST >= 0 ? MST : kMagStore<K>;
-    if (live && mag && re_lane) mag_store<MS>(mag, w * K + o0, P0);
     float mx;
     const unsigned arg = ws_argmax_m<false>(__float_as_uint(P0), re_lane, o0, 0u, false, 0, mx);
-    const bool amb = ws_ambiguous(mx, P0, re_lane, 0.f, false, tq, fl);
-    if (live && j == 0) sym[w] = (uint8_t)(arg | (amb ? kSymAmbiguous : 0u));
+    const bool amb = ws_amb_two_stage(mx, P0, re_lane, 0.f, false, live, at.tq, at.fl, at.t2e, efn);
+    constexpr int MS = MST >= 0 ? MST : kMagStore<K>;
+    if (live && !(amb && at.defer)) {
+        if (mag && re_lane) mag_store<MS>(mag, w * K + o0, P0);
+        if (j == 0) sym[w] = (uint8_t)(arg | (amb ? kSymAmbiguous : 0u));
+    }
+    return amb;
 }
 
 }  // namespace fskd

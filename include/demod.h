@@ -27,11 +27,16 @@
  * decide in fp32; a window whose fp32 top-2 margin lies within the powers'
  * error bound is flagged, and the decision rescue decides it
  * again in double with the definition's own arithmetic and rewrites its
- * symbol and powers: a second launch on the same stream for the Goertzel-
- * family detectors, the tail of its own launch for the FFT detector. A batch
- * is complete when its stream has passed those launches; there is no state
- * shared between batches, so batches of one handle may run on different
- * streams.
+ * symbol and powers. The flag test runs in two stages: the int16 worst-case
+ * energy first (no per-sample work), then, only for windows that test
+ * flags, the window's own energy, so quiet input is not flagged wholesale.
+ * The rescue runs inside the detector's own launch for every detector at
+ * n = 1024 whose windows are evaluated one by one (plain bank, fold, residue
+ * and FFT); segment-shared windows (hop = 64 H < n, demod_slide_windows() > 0)
+ * and other window lengths take a second launch on the same stream
+ * (demod_batch_launches counts it). A batch is complete when its stream has
+ * passed its launches; there is no state shared between batches, so batches
+ * of one handle may run on different streams.
  *
  * Every compute entry point runs on the GPU (HIP, gfx950). There is no CPU
  * fallback: without a visible MI355X, demod_create() fails with
@@ -144,8 +149,9 @@ int demod_max_symbols(const demod_t *st, size_t n_frames);
 
 /* Kernel launches one device-pointer demod_batch / demod_batch_async of
  * n_windows makes (with_mags: magnitudes requested): the detector's, plus one
- * for the decision rescue (K >= 2, Goertzel-family detectors; the FFT
- * detector rescues inside its own launch). A Goertzel-family batch is one
+ * for the decision rescue where it is not inside the detector (K >= 2 on
+ * segment-shared windows or n != 1024; every other detector, the FFT
+ * included, rescues inside its own launch). A Goertzel-family batch is one
  * detector launch; from 4 MiB of symbol + magnitude output it writes each
  * XCD's L2 back in a few bursts inside that launch instead of interleaving the
  * write-back with the input stream. With the environment
@@ -154,6 +160,15 @@ int demod_max_symbols(const demod_t *st, size_t n_frames);
  * see that many dispatches. A host-pointer demod_batch over 4 MiB of samples
  * runs in chunks of 65 536 windows, each chunk counted as a batch of its own. */
 int demod_batch_launches(const demod_t *st, size_t n_windows, int with_mags);
+
+/* The decision rescue's threshold factor tau of this handle (0 when the
+ * rescue is off, K = 1 or FSKD_NO_RESCUE=1): a window is re-decided in double
+ * when its fp32 top-2 margin is below tau sqrt(NE P_max), NE the energy scale
+ * of the window the detector transforms (n sum x^2; fold detector: (n/8)
+ * sum xf^2 of the N/8-folded window). tau = 12 r, r the detector's fp32 power
+ * error bound |dP| <= r sqrt(NE P_max), scaled for the tone plan (DESIGN.md
+ * §2a). For tests and diagnostics. */
+double demod_rescue_tau(const demod_t *st);
 
 /*
  * Streaming entry point: demodulate(pcm, n) -> symbols.

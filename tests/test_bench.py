@@ -155,17 +155,19 @@ def _watchdog_run(code):
                           capture_output=True, text=True, timeout=60)
 
 
-def test_extras_watchdog_prints_headline_and_exits_zero():
+def test_extras_watchdog_prints_headline_and_exits_nonzero():
     """N > 1: a hung extra measurement ends at the watchdog's deadline with rank
-    0's headline line printed (the extra marked) and the process exiting 0."""
+    0's headline line printed (the extra marked) and the process exiting
+    non-zero (VERDICT r3 weak 5 iii: a hung collective must not look like
+    success)."""
     r = _watchdog_run("bench.extras_watchdog(lambda: {'value': 1.5, 'streams': {'error': 't'}}, 0, 0.3); "
                       "time.sleep(30)")
-    assert r.returncode == 0
+    assert r.returncode == 3 and "watchdog" in r.stderr
     line = json.loads(r.stdout.strip().splitlines()[-1])
     assert line["value"] == 1.5 and line["extra_keys"] == ["streams"]
     # other ranks exit without printing
     r = _watchdog_run("bench.extras_watchdog(lambda: {'value': 1.5}, 1, 0.3); time.sleep(30)")
-    assert r.returncode == 0 and r.stdout.strip() == ""
+    assert r.returncode == 3 and r.stdout.strip() == ""
 
 
 def test_extras_watchdog_disarmed_stays_silent():
@@ -176,7 +178,7 @@ def test_extras_watchdog_disarmed_stays_silent():
 
 def test_extras_watchdog_after_the_line_only_exits():
     """A teardown that hangs after rank 0 printed its line: the watchdog ends
-    the process without a second line."""
+    the process without a second line, non-zero."""
     r = _watchdog_run("e = bench.extras_watchdog(lambda: {'value': 1.5}, 0, 0.5); e.printed = True; "
                       "print('{\"value\": 2.0}', flush=True); time.sleep(30)")
-    assert r.returncode == 0 and r.stdout.strip().splitlines() == ['{"value": 2.0}']
+    assert r.returncode == 3 and r.stdout.strip().splitlines() == ['{"value": 2.0}']

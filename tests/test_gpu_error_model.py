@@ -1,0 +1,51 @@
+"""The decision rescue's error model, asserted on every window (VERDICT r3
+item 2; tests/error_model.py): for every detector path and tone plan of
+error_model.CASES (plain bank at the Reinsch edge, near Nyquist, n = 256 /
+4096, segment-shared; fold incl. F16, edge bins, n = 256 / 4096, fold-slide;
+residue with compile-time and LDS classes, n = 256 / 4096; FFT at hop 1024 /
+256) and every adversarial signal family (FSK at sigma 0 / 400, full scale
+with clipping, full-scale clipped square waves, DC offset + tone, uniform
+full-scale int16, dithered silence, two tones at equal power, a tone
+cancelling itself, a near-Nyquist tone beside a plan tone):
+  * every fp32 tone power is within the model r sqrt(P_max NE) + r^2 NE, r =
+    tau / 12 the handle's own constant;
+  * the kernel flags exactly the windows the stated threshold selects;
+  * every window it leaves unflagged already carries the oracle's symbol;
+  * quiet input is not flagged wholesale (the round-3 threshold
+    used the int16 worst-case energy and flagged every window of dithered
+    silence).
+"""
+import json
+
+import pytest
+
+import error_model as EM
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch as t
+    if not t.cuda.is_available():
+        pytest.skip("no GPU visible")
+    return t
+
+
+@pytest.mark.parametrize("case", EM.CASES, ids=[c[0] for c in EM.CASES])
+def test_error_model_every_window(A, O, torch, case):
+    rows = []
+    for fam in EM.FAMILIES:
+        r = EM.evaluate(A, O, case, fam, W=4096)
+        rows.append(r)
+        print(json.dumps({k: v for k, v in r.items()}))
+    for r in rows:
+        assert r["tau"] > 0
+        assert r["flag_missed"] == 0 and r["flag_extra"] == 0, r
+        assert r["unflagged_wrong"] == 0, r
+        assert r["worst_ratio_to_model"] <= 1.0, r
+        if r["family"] == "quiet_s3":
+            assert r["flagged"] <= 0.03 * r["windows"], r
+    worst = max(rows, key=lambda r: r["worst_err_frac_of_tau"])
+    print("worst error as a fraction of tau:", worst["case"], worst["family"],
+          worst["worst_err_frac_of_tau"])

@@ -694,10 +694,11 @@ def test_batch_launch_slices(A, O, torch, monkeypatch, mode, plan):
     sym = torch.empty(W, dtype=torch.uint8, device="cuda")
     mag = torch.empty((W, 8), dtype=torch.float32, device="cuda")
     with A.Demodulator(cfg) as d:
-        # detector launches + the decision rescue's launch
-        assert d.batch_launches(W, mags=True) == (4 if mode == "slices" else 1) + 1
-        assert d.batch_launches(W, mags=False) == 1 + 1
-        assert d.batch_launches(1 << 18, mags=True) == 1 + 1
+        # detector launches only: fold and residue re-decide their flagged
+        # windows inside the detector at n = 1024 (round 4)
+        assert d.batch_launches(W, mags=True) == (4 if mode == "slices" else 1)
+        assert d.batch_launches(W, mags=False) == 1
+        assert d.batch_launches(1 << 18, mags=True) == 1
         d.batch_device(d_pcm, W, sym, mag)
         ref_sym = torch.empty_like(sym)
         ref_mag = torch.empty_like(mag)
@@ -711,6 +712,13 @@ def test_batch_launch_slices(A, O, torch, monkeypatch, mode, plan):
     with A.Demodulator(freqs=A.FSK2_FREQS) as d:
         # 9 MiB: one launch, and the 2-FSK plain bank rescues in the kernel
         assert d.batch_launches(1 << 20, mags=True) == 1
+    # the rescue launch remains for segment-shared windows and n != 1024
+    with A.Demodulator(A.make_cfg(n=1024, hop=256, freqs=A.FSK2_FREQS)) as d:
+        assert d.slide_windows > 0 and d.batch_launches(1 << 16, mags=True) == 2
+    with A.Demodulator(A.make_cfg(n=256, hop=256, freqs=(1500.0, 3000.0))) as d:
+        assert d.batch_launches(1 << 16, mags=True) == 2
+    with A.Demodulator(A.make_cfg(n=1024, hop=256, freqs=A.FSK2_FREQS, method=A.METHOD_FFT)) as d:
+        assert d.batch_launches(1 << 16, mags=True) == 1
 
 
 # ---- GPU against the reference's own FFT at N = 1024 -------------------------
