@@ -46,6 +46,7 @@ struct demod {
     bool wb_bursts = true;
     bool rescue_kernel_forced = false;  // FSKD_RESCUE_LAUNCH=1: the rescue launch everywhere (measurement)
     int wb_force = 0;  // FSKD_WB_BURSTS=<n >= 1>: n bursts on every hop = n batch (measurement)
+    int fft_swp = 0;   // FSKD_FFT_SWP=<3|4>: the software-pipelined FFT variant (measurement)
     double tau = 0.0;           // decision rescue threshold factor (amb_tau)
     float amb_tq = 0.f;         // stage 1: amb_tq sqrt(P_max), the int16 worst-case energy
     float amb_floor = 0.f;
@@ -444,6 +445,8 @@ static int init_device_state(demod_t *st)
     st->rescue_launch = !(no_rescue && std::strcmp(no_rescue, "flags") == 0);
     const char *rl_env = std::getenv("FSKD_RESCUE_LAUNCH");
     st->rescue_kernel_forced = rl_env && std::strcmp(rl_env, "1") == 0;
+    const char *swp_env = std::getenv("FSKD_FFT_SWP");
+    st->fft_swp = swp_env ? std::max(0, std::min(4, std::atoi(swp_env))) : 0;
     const char *wb_env = std::getenv("FSKD_WB_BURSTS");
     st->wb_bursts = !(wb_env && std::strcmp(wb_env, "0") == 0);
     if (wb_env && std::atoi(wb_env) > 0) st->wb_force = std::min(std::atoi(wb_env), 64);
@@ -699,6 +702,7 @@ static int enqueue_fft(demod_t *st, const int16_t *d_pcm, size_t n_windows, uint
     // one launch, no symbol scan
     p.rescue = st->rescue && st->rescue_launch ? 1 : 0;
     p.rtw = st->d_rtw;
+    p.swp = st->fft_swp;
     HIP_TRY(launch_fft_quad(p, s));
     return (int)n_windows;
 }

@@ -11,7 +11,8 @@
 #   ab:<N>:<envA>:<envB>:<args>  N interleaved rounds of bench.py <args> with env A, env B
 #   kt               rocprofv3 --kernel-trace --stats of the driver's command
 #   pmc              HBM PMC passes (FETCH_SIZE, WRITE_SIZE separately): fsk2, fsk8, fft, fft+spectrum
-#   sq               one SQ pass of the tones-only FFT kernel
+#   sq[:<args>]      one SQ pass (issue counts) of the tones-only FFT kernel
+#   sqw[:<args>]     one SQ pass of its wait states (SQ_WAIT_ANY / _INST_ANY / _INST_LDS)
 #   precision        scripts/precision_probe.py
 #   py:<script args> python3 <script args> (probes under scripts/)
 set -o pipefail
@@ -59,6 +60,10 @@ for st in "$@"; do
       done ;;
     sq)
       (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU GRBM_GUI_ACTIVE --output-format csv -d "$O/sq_fft" -o run -- python3 "$R/bench.py" --config fft --no-cpu-baseline --no-rescue-ab --warmup 2 --steps 5 $arg) > "$log" 2>&1 || exit $? ;;
+    sqw)
+      # where the FFT kernel's waves wait: parked at s_waitcnt / barrier
+      # (SQ_WAIT_ANY) vs issue-stalled (SQ_WAIT_INST_ANY, its LDS part)
+      (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE --output-format csv -d "$O/sqw_fft" -o run -- python3 "$R/bench.py" --config fft --no-cpu-baseline --no-rescue-ab --warmup 2 --steps 5 $arg) > "$log" 2>&1 || exit $? ;;
     precision)
       timeout -k 10 600 python3 -u scripts/precision_probe.py $arg > "$log" 2>&1 || exit $? ;;
     py)

@@ -3,7 +3,8 @@
 For the decision rescue: a window's fp32 decision can differ
 from the exact one only if its top-2 margin is within the error of the two
 powers. The error of P_k is modelled as |dP_k| <= r * sqrt(P_max * NE) with
-NE = n * sum(x^2) (the window's energy scale: |X_k|^2 <= NE by Cauchy-Schwarz).
+NE = n * sum(x^2) (the window's energy scale: |X_k|^2 <= NE by Cauchy-Schwarz);
+for the fold detector NE = (n/8) * sum(xf^2), the folded window's (round 4).
 This prints, per detector and signal family, the largest r seen over all
 windows and tones, and the largest |dP| / NE (the second-order term).
 
@@ -64,6 +65,11 @@ def run_case(name, freqs, n, hop, method, W, rng, fft=False):
             idx = np.arange(nw)[:, None] * hop + np.arange(n)[None, :]
             xw = x[idx].astype(np.float64)
             NE = n * (xw * xw).sum(axis=1)
+            if int(d.method) == 3:
+                # round 4: the fold detector's energy scale is that of the
+                # folded window it transforms, (n/8) sum xf^2 (<= NE)
+                xf = xw.reshape(nw, 8, n // 8).sum(axis=1)
+                NE = (n / 8) * (xf * xf).sum(axis=1)
             P1 = rP.max(axis=1)
             dP = np.abs(mag.astype(np.float64) - rP).max(axis=1)
             ok = NE > 0
@@ -114,6 +120,12 @@ def main():
         ("fold_slide_k8_h256", f8, 1024, 256, A.METHOD_FOLDED, False),
         ("residue_k8_dcls", odd8, 1024, 1024, A.METHOD_RESIDUE, False),
         ("residue_k5_lds", k5, 1024, 1024, A.METHOD_RESIDUE, False),
+        # round 4: fold and residue at other window lengths
+        ("fold_k2_n256", (1500.0, 3000.0), 256, 256, A.METHOD_FOLDED, False),
+        ("fold_k8_n4096", f8, 4096, 4096, A.METHOD_FOLDED, False),
+        ("residue_k5_n256", tuple(187.5 * (8 + 3 * i) for i in range(5)), 256, 256, A.METHOD_RESIDUE, False),
+        ("residue_k8_n4096", tuple(48000.0 / 4096 * (128 + 9 * i) for i in range(8)), 4096, 4096,
+         A.METHOD_RESIDUE, False),
         ("fft_h1024", f2, 1024, 1024, A.METHOD_FFT, True),
         ("fft_h256", f8, 1024, 256, A.METHOD_FFT, True),
     ]
