@@ -290,7 +290,6 @@ struct FftParams {
     float amb_t2e;           // Parseval, amb_t2e = tau^2)
     int rescue;            // 1: flagged windows are re-decided in the kernel (rescue_fft.h)
     const double *rtw;       // rescue: [1023] (cos, sin), stage len at len / 2 - 1 + j
-    int swp;                 // measurement: software-pipelined variant, waves per SIMD (0: shipped)
 };
 
 // rescue.hip: re-decides every window whose symbol carries kSymAmbiguous.

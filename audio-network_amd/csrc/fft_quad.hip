@@ -733,11 +733,9 @@ constexpr int kFmtWord3 = 0xFAC | (3 << 12) | (5 << 15);
 // compile-time W32^j — one packed complex product (29 VALU per group) in
 // place of 8 ds_read2_b64.
 template <int WPB = 4, int MINW = 4, int PF = 0, bool SPEC = true, bool FMT = false, int AUX = 2,
-          int FUSED = 0, int RD = 0, int SPL = 0, int OVL = 0, int TW3R = 0, int RSC = 1, int PICK = 0,
-          int SWP = 0>
+          int FUSED = 0, int RD = 0, int SPL = 0, int OVL = 0, int TW3R = 0, int RSC = 1, int PICK = 0>
 __device__ __attribute__((always_inline)) inline void fft1024_quad_body(const FftParams &p)
 {
-    static_assert(!SWP || (PF == 0 && !OVL && !FMT), "SWP: loads at the group's top, plain transposes");
     static_assert(!OVL || (FUSED >= 4 && PF != 1), "OVL: the FUSED 4 column DFT-16");
     static_assert(PF != 2 || (SPEC && SPL), "PF 2: ahead of the linear-slab spectrum stores");
     static_assert(!SPL || SPEC, "SPL: the linear power slab of the spectrum store");
@@ -820,39 +818,23 @@ __device__ __attribute__((always_inline)) inline void fft1024_quad_body(const Ff
         }
     };
     if (PF && g < n_groups) load_group(g);
-    // the int16 pairs of the loaded group -> (re, im) = (x[2n], x[2n+1])
-    auto convert = [&](f2 (&aa)[32]) {
+    for (; g < n_groups; g += stride) {
+        const long long w = 4 * g + q;
+        if (!PF) load_group(g);
+        f2 a[32];
 #pragma unroll
         for (int n1 = 0; n1 < 32; ++n1) {
             if constexpr (FMT) {
-                aa[n1] = nxf[n1];
+                a[n1] = nxf[n1];
                 continue;
             }
-            aa[n1] = (f2){(float)(int)(short)(nx[FMT ? 0 : n1] & 0xFFFFu),
-                          (float)((int)nx[FMT ? 0 : n1] >> 16)};
-            asm("" : "+v"(aa[n1]));  // opaque: keep (float)a + (float)b a packed add
+            a[n1] = (f2){(float)(int)(short)(nx[FMT ? 0 : n1] & 0xFFFFu),
+                         (float)((int)nx[FMT ? 0 : n1] >> 16)};
+            asm("" : "+v"(a[n1]));  // opaque: keep (float)a + (float)b a packed add
         }
-    };
-    // SWP (software pipeline, two groups in flight per wave): group g + stride's
-    // loads, converts and DFT-32 run while group g's first transpose round is
-    // in LDS, so that round trip has the wave's own VALU work beside it
-    // (DESIGN.md §4.4). Its DFT-32 output is carried into
-    // the next iteration.
-    f2 a[32];
-    if (SWP && g < n_groups) {
-        load_group(g);
-        convert(a);
+
+        // 1. DFT-32 over n1 (fused twiddles), no stage-1 twiddle here
         dftf<32, 1, FUSED>(a);
-    }
-    for (; g < n_groups; g += stride) {
-        const long long w = 4 * g + q;
-        if constexpr (!SWP) {
-            if (!PF) load_group(g);
-            convert(a);
-            // 1. DFT-32 over n1 (fused twiddles), no stage-1 twiddle here
-            dftf<32, 1, FUSED>(a);
-        }
-        f2 an[SWP ? 32 : 1];
 
         // 2. transpose in two column rounds; lane (q, t') gets columns
         //    k1 = t' (round 0) and k1b (round 1) of its window
@@ -930,13 +912,6 @@ __device__ __attribute__((always_inline)) inline void fft1024_quad_body(const Ff
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             if (PF == 1 && r == 0) load_group(g + stride < n_groups ? g + stride : g);
-            if constexpr (SWP) {
-                if (r == 0 && g + stride < n_groups) {
-                    load_group(g + stride);
-                    convert(an);
-                    dftf<32, 1, FUSED>(an);
-                }
-            }
             const int col = r == 0 ? t : k1b - 16;
 #pragma unroll
             for (int n2 = 0; n2 < 16; ++n2) b[16 * r + n2] = win[n2 * kQRow + col];
@@ -1202,10 +1177,6 @@ __device__ __attribute__((always_inline)) inline void fft1024_quad_body(const Ff
             __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
             __builtin_amdgcn_wave_barrier();
         }
-        if constexpr (SWP) {
-#pragma unroll
-            for (int n1 = 0; n1 < 32; ++n1) a[n1] = an[n1];
-        }
     }
 
     // 6. decision rescue (rescue_fft.h), after the group loop
@@ -1286,11 +1257,11 @@ __device__ __attribute__((always_inline)) inline void fft1024_quad_body(const Ff
 }
 
 template <int WPB = 4, int MINW = 4, int PF = 0, bool SPEC = true, bool FMT = false, int AUX = 2,
-          int FUSED = 0, int SPL = 0, int OVL = 0, int TW3R = 0, int RSC = 1, int PICK = 0, int SWP = 0>
+          int FUSED = 0, int SPL = 0, int OVL = 0, int TW3R = 0, int RSC = 1, int PICK = 0>
 __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MINW > 0 ? MINW : 1)))
 void fft1024_quad_kernel(FftParams p)
 {
-    fft1024_quad_body<WPB, MINW, PF, SPEC, FMT, AUX, FUSED, 0, SPL, OVL, TW3R, RSC, PICK, SWP>(p);
+    fft1024_quad_body<WPB, MINW, PF, SPEC, FMT, AUX, FUSED, 0, SPL, OVL, TW3R, RSC, PICK>(p);
 }
 
 // (a device-code attribute: the host pass of hipcc does not know the feature)
@@ -1315,7 +1286,7 @@ FSKD_NO_LDS_PAIRING void fft1024_quad_kernel_r64(FftParams p)
 // Persistent grid: as many blocks as fit the chip, each wave strides over
 // groups of 4 windows (the LDS twiddle tables are built once per block).
 template <int WPB, int MINW, int PF, bool SPEC, bool FMT = false, int AUX = 2, int FUSED = 0, int RD = 0,
-          int SPL = 0, int OVL = 0, int TW3R = 0, int RSC = 1, int PICK = 0, int SWP = 0>
+          int SPL = 0, int OVL = 0, int TW3R = 0, int RSC = 1, int PICK = 0>
 hipError_t launch_fft_quad_t(const FftParams &p, hipStream_t s)
 {
     void (*kern)(FftParams);
@@ -1323,7 +1294,7 @@ hipError_t launch_fft_quad_t(const FftParams &p, hipStream_t s)
     if constexpr (RD > 0)
         kern = fft1024_quad_kernel_r64<WPB, MINW, PF, SPEC, FMT, AUX, FUSED, RD>;
     else
-        kern = fft1024_quad_kernel<WPB, MINW, PF, SPEC, FMT, AUX, FUSED, SPL, OVL, TW3R, RSC, PICK, SWP>;
+        kern = fft1024_quad_kernel<WPB, MINW, PF, SPEC, FMT, AUX, FUSED, SPL, OVL, TW3R, RSC, PICK>;
     int dev = 0, cus = 256, per_cu = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
@@ -1361,12 +1332,6 @@ hipError_t launch_fft_quad_t(const FftParams &p, hipStream_t s)
 hipError_t launch_fft_quad(const FftParams &p, hipStream_t s)
 {
     const bool lin = p.spec && ((uintptr_t)p.spec & 15) == 0;
-    if (p.swp && !p.spec)  // measurement variant (FSKD_FFT_SWP=<waves per SIMD>): tones only
-        return p.hop < 1024
-                   ? (p.swp == 4 ? launch_fft_quad_t<4, 4, 0, false, false, 0, 4, 0, 0, 0, 0, 1, 1, 1>(p, s)
-                                 : launch_fft_quad_t<4, 3, 0, false, false, 0, 4, 0, 0, 0, 0, 1, 1, 1>(p, s))
-                   : (p.swp == 4 ? launch_fft_quad_t<4, 4, 0, false, false, 2, 4, 0, 0, 0, 0, 1, 1, 1>(p, s)
-                                 : launch_fft_quad_t<4, 3, 0, false, false, 2, 4, 0, 0, 0, 0, 1, 1, 1>(p, s));
     if (p.hop < 1024)
         return lin ? launch_fft_quad_t<4, 4, 0, true, false, 0, 4, 0, 2>(p, s)
              : p.spec ? launch_fft_quad_t<4, 4, 0, true, false, 0, 4>(p, s)

@@ -12,7 +12,8 @@
 #   kt               rocprofv3 --kernel-trace --stats of the driver's command
 #   pmc              HBM PMC passes (FETCH_SIZE, WRITE_SIZE separately): fsk2, fsk8, fft, fft+spectrum
 #   sq[:<args>]      one SQ pass (issue counts) of the tones-only FFT kernel
-#   sqw[:<args>]     one SQ pass of its wait states (SQ_WAIT_ANY / _INST_ANY / _INST_LDS)
+#   sqw[:<ENV=V|-> <args>]  one SQ pass of its wait states (SQ_WAIT_ANY / _INST_ANY / _INST_LDS)
+#   testsall[:<args>] pytest -m gpu without -x (all failures in one call)
 #   precision        scripts/precision_probe.py
 #   py:<script args> python3 <script args> (probes under scripts/)
 set -o pipefail
@@ -63,7 +64,14 @@ for st in "$@"; do
     sqw)
       # where the FFT kernel's waves wait: parked at s_waitcnt / barrier
       # (SQ_WAIT_ANY) vs issue-stalled (SQ_WAIT_INST_ANY, its LDS part)
-      (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE --output-format csv -d "$O/sqw_fft" -o run -- python3 "$R/bench.py" --config fft --no-cpu-baseline --no-rescue-ab --warmup 2 --steps 5 $arg) > "$log" 2>&1 || exit $? ;;
+      # sqw:<ENV=VAL|-> [bench args]: the environment of the profiled run (e.g.
+      # FSKD_FFT_SWP=3), "-" for none; output under sqw_<i>/
+      ev=${arg%% *}; rest=${arg#* }; [ "$rest" = "$arg" ] && rest=""
+      [ -z "$ev" ] || [ "$ev" = "-" ] && ev="X=1"
+      (cd /tmp && export $ev && timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE --output-format csv -d "$O/sqw_$i" -o run -- python3 "$R/bench.py" --config fft --no-cpu-baseline --no-rescue-ab --warmup 2 --steps 5 $rest) > "$log" 2>&1 || exit $? ;;
+    testsall)
+      # the GPU suite without -x (every failure of a change set in one call)
+      timeout -k 10 1100 python -u -m pytest -v --timeout 300 --timeout-method thread -m gpu tests $arg > "$log" 2>&1 || exit $? ;;
     precision)
       timeout -k 10 600 python3 -u scripts/precision_probe.py $arg > "$log" 2>&1 || exit $? ;;
     py)

@@ -137,9 +137,10 @@ def evaluate(A, O, case, fam, W=4096, threads=16, seed=1):
     ok = bound > 0
     ratio = np.zeros(W)
     ratio[ok] = dP[ok] / bound[ok]
-    # error as a fraction of tau sqrt(P_max NE) (the margin threshold)
-    thr = tau * np.sqrt(Pm * NE)
-    frac_tau = np.where(thr > 0, dP / np.where(thr > 0, thr, 1.0), 0.0)
+    # the error as a fraction of tau's model (tau = 12 r): what fraction of
+    # the margin threshold tau sqrt(P_max NE) (+ its second-order term) one
+    # power's error uses
+    frac_tau = ratio / 12.0
     zero_ne = ~ok
     # 2. the flags against the stated threshold, from the kernel's own powers
     flag = (sym & 0x80) != 0

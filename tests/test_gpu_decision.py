@@ -88,6 +88,7 @@ def test_near_ties_follow_exact_argmax(A, O, torch, plan, method):
     with A.Demodulator(freqs=freqs, method=method) as d:
         assert d.method == method
         sym, mag = d.batch(x, mags=True)
+        tau = d.rescue_tau
     oracle = O.fft_demod if method == FFT else O.goertzel
     ref_sym, ref_P = oracle(x, freqs, 1024)
     in_band = check_decisions(sym, mag, ref_sym, ref_P)
@@ -101,11 +102,18 @@ def test_near_ties_follow_exact_argmax(A, O, torch, plan, method):
     assert tight.sum() >= 20, tight.sum()
     assert (tight & hi_wins).sum() >= 5, (tight & hi_wins).sum()
     assert in_band > 0
-    # windows whose oracle margin is far inside the rescue threshold (~2.6e-4
-    # of P_max at this level) were rescued: their powers are the oracle's own
-    # double powers, rounded to fp32 (bit-identical arithmetic, rescue.hip)
+    # windows whose oracle margin is well inside the rescue threshold tau
+    # sqrt(NE P_max) (NE the window's energy scale, the folded window's for
+    # the fold detector) were rescued: their powers are the
+    # oracle's own double powers, rounded to fp32 (bit-identical arithmetic)
+    xw = x.reshape(W, 1024).astype(np.float64)
+    if method == FOLDED:
+        xf = xw.reshape(W, 8, 128).sum(axis=1)
+        NE = 128.0 * (xf * xf).sum(axis=1)
+    else:
+        NE = 1024.0 * (xw * xw).sum(axis=1)
     Ps = np.sort(ref_P, axis=1)
-    sure = (Ps[:, -1] - Ps[:, -2]) < 1e-5 * Ps[:, -1]
+    sure = (Ps[:, -1] - Ps[:, -2]) < 0.5 * tau * np.sqrt(NE * Ps[:, -1])
     assert sure.sum() >= 20
     assert np.array_equal(mag[sure].view(np.uint32), ref_P[sure].astype(np.float32).view(np.uint32))
     # the same windows decided in fp32 alone: some differ from the oracle
@@ -173,6 +181,7 @@ def test_fft_rescue_spectrum_is_the_oracles(A, O, torch, hop):
     flat = x.reshape(-1)
     W = (flat.size - 1024) // hop + 1
     with A.Demodulator(freqs=freqs, hop=hop, method=FFT) as d:
+        tau = d.rescue_tau
         d_pcm = torch.from_numpy(flat.copy()).cuda()
         d_sym = torch.empty(W, dtype=torch.uint8, device="cuda")
         d_mag = torch.empty((W, len(freqs)), dtype=torch.float32, device="cuda")
@@ -183,7 +192,12 @@ def test_fft_rescue_spectrum_is_the_oracles(A, O, torch, hop):
     ref_sym, ref_P = O.fft_demod(flat, freqs, 1024, hop)
     check_decisions(sym, mag, ref_sym, ref_P)
     Ps = np.sort(ref_P, axis=1)
-    sure = np.flatnonzero((Ps[:, -1] - Ps[:, -2]) < 1e-5 * Ps[:, -1])
+    # well inside the threshold tau sqrt(NE P_max) (NE = n sum x^2 <= the
+    # kernel's Parseval energy): flagged, hence rescued
+    idx = np.arange(W)[:, None] * hop + np.arange(1024)[None, :]
+    xw = flat[idx].astype(np.float64)
+    NE = 1024.0 * (xw * xw).sum(axis=1)
+    sure = np.flatnonzero((Ps[:, -1] - Ps[:, -2]) < 0.5 * tau * np.sqrt(NE * Ps[:, -1]))
     assert sure.size >= (20 if hop == 1024 else 5), sure.size
     full = np.stack([O.fft_power(flat[i * hop:i * hop + 1024]) for i in sure]).astype(np.float32)
     assert np.array_equal(spec[sure].view(np.uint32), full.view(np.uint32))

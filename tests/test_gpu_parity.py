@@ -811,27 +811,3 @@ def test_fft_spectrum_store_paths_agree(A, O, torch, W, hop):
     ref_sym, ref_P = O.fft_demod(flat, A.FSK8_FREQS, n, hop)
     assert (s0 == ref_sym[:Wh]).all()
     assert rel_err(m0, ref_P[:Wh]) <= MAG_TOL
-
-
-@pytest.mark.parametrize("hop,W", [(256, (1 << 16) + 3), (1024, 4099), (8, 77)])
-@pytest.mark.parametrize("swp", ["3", "4"])
-def test_fft_software_pipelined_variant_is_bit_identical(A, O, torch, monkeypatch, hop, W, swp):
-    """The software-pipelined FFT detector (FSKD_FFT_SWP, a measurement
-    variant: the next group's loads and DFT-32 run during the current group's
-    first transpose round) computes exactly the shipped
-    kernel's arithmetic in another order: symbols and tone powers
-    bit-identical, including partial last groups, and every symbol the
-    oracle's."""
-    f = A.FSK8_FREQS
-    n_blocks = -(-((W - 1) * hop + 1024) // 1024)
-    pcm, _ = O.synth_fsk(f, 1024, n_blocks, 77 + hop, 8000, 400)
-    flat = pcm.reshape(-1)[:(W - 1) * hop + 1024]
-    with A.Demodulator(freqs=f, hop=hop, method=FFT) as d:
-        s0, m0 = d.batch(flat, n_windows=W, mags=True)
-    monkeypatch.setenv("FSKD_FFT_SWP", swp)
-    with A.Demodulator(freqs=f, hop=hop, method=FFT) as d:
-        s1, m1 = d.batch(flat, n_windows=W, mags=True)
-    assert np.array_equal(s0, s1)
-    assert np.array_equal(m0.view(np.int32), m1.view(np.int32))
-    ref_sym, ref_P = O.fft_demod(flat, f, 1024, hop, threads=16)
-    check_decisions(s1, m1, ref_sym, ref_P)
