@@ -1126,7 +1126,12 @@ __device__ __attribute__((always_inline)) inline void fft1024_quad_body(const Ff
         auto efn = [&]() {
             float e = 0.f;
             if constexpr (SPEC && SPL) {
-                for (int i = tt; i < 513; i += 16) e += pw[rowb + i];
+                // the fenced lane id again (as the stores below): the row
+                // base is not kept live from the post-pass
+                int tl2 = (int)(threadIdx.x & 63);
+                asm volatile("" : "+v"(tl2));
+                const float *row = pw + (tl2 >> 4) * 513;
+                for (int i = tl2 & 15; i < 513; i += 16) e += row[i];
             } else if constexpr (SPEC) {
                 for (int i = t; i < 513; i += 16) e += pq[quad_slot(i)];
             } else {

@@ -383,49 +383,94 @@ def run_config(A, D, torch, dist, args, config, rank, world, local, use_dist, st
     gdone_evs = [e for e in (gevs or []) if e is not None]
     gather_ms = (float(np.mean([a.elapsed_time(b) for a, b in gdone_evs])) if gdone_evs else None)
     ms_per_step_eager = None
+    breakdown = None
     if use_dist and dev_framing and getattr(args, "graph", False) and args.dist_backend == "nccl":
-        # HIP graph of one step: the detector kernel on a
+        # HIP graphs of the step: the detector kernel on a
         # forked branch; the framing kernel and the RCCL gather of the other
         # slot (the previous step's symbols) on the capture stream, beside
-        # it; joined at the end; two graphs alternate the slots. One graph launch per step
-        # instead of the eager step's ~10 host calls, which at 8 GPUs (an
-        # ~82 us kernel per rank) would otherwise set the step time.
-        graphs = []
-        for sl in (0, 1):
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                cap = torch.cuda.current_stream()
-                comp.wait_stream(cap)
-                with torch.cuda.stream(comp):
-                    demod.batch_async(d_pcm, n_eval, slots[sl], d_mag, stream=comp.cuda_stream)
-                # the other slot (the previous step's symbols) is framed and
-                # gathered beside this step's detector kernel
-                A.frame_streams_async(slots[1 - sl], s_count, wps, bits, fslots[1 - sl],
-                                      stream=cap.cuda_stream)
-                gout = D.gather_symbols(fslots[1 - sl][:s_count * fstride], gunits, world,
-                                        unit=fstride, group=group)
-                cap.wait_stream(comp)
-            graphs.append((g, gout))
-        for i in range(warm):
-            graphs[i % 2][0].replay()
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for i in range(steps + 1):   # + 1: the last replay gathers the last step's frames
-            graphs[i % 2][0].replay()
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        gel = time.perf_counter() - t0
-        if world > 1:
-            t = torch.tensor([gel], dtype=torch.float64, device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            gel = float(t.item())
+        # it. One graph holds S = --graph-steps steps (S even, the slots
+        # alternating step by step; S = 1: two graphs alternate), so one
+        # graph launch per S steps instead of the eager step's ~10 host calls,
+        # which at 8 GPUs (an ~80 us kernel per rank) would set the step time.
+        # Inside a graph, step s's detector waits for step s - 1's framing +
+        # gather (they read the slot it writes) and the framing of step s - 1
+        # for step s - 1's detector: each step is max(detector, framing +
+        # gather) on its critical path.
+        def build(kind, S):
+            """kind: full (detector + framing + gather), det_frame, det."""
+            out = []
+            for g_i in range(1 if S > 1 else 2):
+                g = torch.cuda.CUDAGraph()
+                gouts = []
+                with torch.cuda.graph(g):
+                    cap = torch.cuda.current_stream()
+                    comp.wait_stream(cap)
+                    fdone = None
+                    for s in range(S):
+                        sl = (s if S > 1 else g_i) % 2
+                        if fdone is not None:
+                            comp.wait_event(fdone)      # step s - 1's framing read this slot's twin
+                        with torch.cuda.stream(comp):
+                            demod.batch_async(d_pcm, n_eval, slots[sl], d_mag, stream=comp.cuda_stream)
+                        if kind != "det":
+                            # the previous step's slot, beside this detector kernel
+                            if s > 0:
+                                cap.wait_event(kev)
+                            A.frame_streams_async(slots[1 - sl], s_count, wps, bits, fslots[1 - sl],
+                                                  stream=cap.cuda_stream)
+                            if kind == "full":
+                                gouts.append(D.gather_symbols(fslots[1 - sl][:s_count * fstride], gunits,
+                                                              world, unit=fstride, group=group))
+                            fdone = torch.cuda.Event()
+                            fdone.record(cap)
+                        kev = torch.cuda.Event()
+                        kev.record(comp)
+                    cap.wait_stream(comp)
+                out.append((g, gouts))
+            return out
+
+        def time_graphs(graphs, S, n_rep):
+            for i in range(max(4, warm // S)):
+                graphs[i % len(graphs)][0].replay()
+            if world > 1:
+                dist.barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for i in range(n_rep):
+                graphs[i % len(graphs)][0].replay()
+            if world > 1:
+                dist.barrier()
+            torch.cuda.synchronize()
+            el = time.perf_counter() - t0
+            if world > 1:
+                t = torch.tensor([el], dtype=torch.float64, device=dev)
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
+                el = float(t.item())
+            return el / (n_rep * S) * 1e3
+
+        S = max(1, int(getattr(args, "graph_steps", 1)))
+        if S > 1 and S % 2:
+            S += 1
+        graphs = build("full", S)
+        n_rep = -(-(steps + 1) // S)       # + 1 step: the last replay gathers the last step's frames
         ms_per_step_eager = ms_per_step
-        ms_per_step = gel / (steps + 1) * 1e3
-        all_sym = graphs[steps % 2][1]          # frames of the slot the last replay gathered
-        st["i"] = steps + 1                     # the slot holding the last demodulated symbols
+        ms_per_step = time_graphs(graphs, S, n_rep)
+        all_sym = graphs[(n_rep - 1) % len(graphs)][1][-1]   # frames gathered by the last step
+        st["i"] = n_rep * S                                  # the slot holding the last demodulated symbols
+        if getattr(args, "breakdown", False):
+            # where the step's time above the kernel goes (VERDICT r3 item 1):
+            # the same detector back to back with no graph, graphs of the
+            # detector alone and with the framing, at 1 and S steps per graph
+            def eager_det():
+                demod.batch_async(d_pcm, n_eval, slots[0], d_mag, stream=comp.cuda_stream)
+            breakdown = {"graph_steps": S,
+                         "eager_detector_only_ms": round(time_steps(torch, eager_det, steps, warm), 4)}
+            for kind in ("det", "det_frame", "full"):
+                for s2 in sorted({1, S, 8}):
+                    gr = build(kind, s2)
+                    breakdown[f"graph_{kind}_{s2}step_ms"] = round(time_graphs(gr, s2, -(-steps // s2)), 4)
+                    del gr
+            torch.cuda.synchronize()
 
     # correctness of the timed output: every symbol vs the transmitted one
     # (sliding windows straddle two symbols: compare the aligned ones only)
@@ -504,8 +549,12 @@ def run_config(A, D, torch, dist, args, config, rank, world, local, use_dist, st
                          "step_minus_kernel_ms": round(ms_per_step - kernel_ms, 4)}
         if ms_per_step_eager is not None:
             r["overhead"]["ms_per_step_eager"] = round(ms_per_step_eager, 4)
-            r["overhead"]["step"] = ("hip graph: detector kernel on one branch; framing + RCCL "
-                                     "gather of the previous step's symbols on the other")
+            r["overhead"]["step"] = ("hip graph (%d step%s per graph): detector kernel on one branch; "
+                                     "framing + RCCL gather of the previous step's symbols on the other"
+                                     % (max(1, int(getattr(args, "graph_steps", 1))),
+                                        "" if int(getattr(args, "graph_steps", 1)) <= 1 else "s"))
+        if breakdown is not None:
+            r["overhead"]["breakdown"] = breakdown
     if config == "fft":
         # the FFT is reported against the VALU roof too.
         # Algorithmic flops per window: 2.5 N log2 N for the real N-point
@@ -722,7 +771,7 @@ def summary(r) -> dict:
     return out
 
 
-def streams_child(args, n_streams: int = 1024) -> dict:
+def streams_child(args, n_streams: int = 1024, breakdown: bool = False) -> dict:
     """configs[4] at N = 1 as the 8-GPU run's step takes it: a child
     `bench.py --config streams --force-dist` (RCCL at world size 1, one HIP
     graph per step), its line reduced to the entry of this one. n_streams =
@@ -731,8 +780,10 @@ def streams_child(args, n_streams: int = 1024) -> dict:
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT", "MASTER_ADDR"):
         env.pop(k, None)
     cmd = [sys.executable, "-u", os.path.abspath(__file__), "--config", "streams", "--force-dist",
-           "--streams-total", str(n_streams),
+           "--streams-total", str(n_streams), "--graph-steps", str(args.graph_steps),
            "--steps", str(args.steps), "--warmup", str(args.warmup), "--no-cpu-baseline"]
+    if breakdown:
+        cmd.append("--breakdown")
     r = subprocess.run(cmd, capture_output=True, timeout=600, cwd=ROOT, env=env)
     lines = [ln for ln in r.stdout.decode().splitlines() if ln.startswith("{")]
     if r.returncode != 0 or not lines:
@@ -954,7 +1005,12 @@ def main():
                     help="initialise torch.distributed and run the gather even at N = 1 "
                          "(exercises the RCCL path on one GPU)")
     ap.add_argument("--no-graph", dest="graph", action="store_false",
-                    help="streams config: time eager steps instead of one HIP graph per step")
+                    help="streams config: time eager steps instead of HIP graphs")
+    ap.add_argument("--graph-steps", type=int, default=1,
+                    help="streams config: steps per HIP graph (1: two graphs alternate the slots)")
+    ap.add_argument("--breakdown", action="store_true",
+                    help="streams config: also time the step's pieces (detector alone, graphs "
+                         "without the gather / framing, 1 / S / 8 steps per graph)")
     ap.add_argument("--extras-timeout", type=float, default=240.0,
                     help="N > 1: seconds the configs[4] extra may take before a watchdog prints "
                          "the headline line without it and ends every rank")
@@ -1033,7 +1089,7 @@ def main():
         # one rank's shard of the 8-GPU run (128 of the 1024 streams), the
         # same graph step: the projected 8-GPU scaling of configs[4] measured
         # on one GPU
-        sh = streams_child(args, 128)
+        sh = streams_child(args, 128, breakdown=True)
         if "ms_per_step" in sh and "ms_per_step" in extras["streams"]:
             sh["projected_scaling_8"] = round(extras["streams"]["ms_per_step"] / sh["ms_per_step"], 3)
             sh["projection"] = ("streams.ms_per_step / streams_shard.ms_per_step: each of 8 ranks runs "

@@ -63,14 +63,20 @@ def test_config5_rank_shard_world1():
     env.pop("MASTER_PORT", None)
     r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--config", "streams",
                         "--force-dist", "--streams-total", "128", "--steps", "20", "--warmup", "5",
-                        "--no-cpu-baseline"], capture_output=True, timeout=400, cwd=ROOT, env=env)
+                        "--graph-steps", "4", "--breakdown", "--no-cpu-baseline"],
+                       capture_output=True, timeout=400, cwd=ROOT, env=env)
     out = r.stdout.decode()
     assert r.returncode == 0, (out[-2000:], r.stderr.decode()[-4000:])
     line = json.loads([ln for ln in out.splitlines() if ln.startswith("{")][-1])
     assert line["config"]["windows_per_gpu"] == 128 * 2048
     assert line["symbol_errors"] == 0 and line["framing"]["roundtrip_ok"]
     assert line["config"]["workload"].startswith("configs[4]: 128 streams")
-    assert "step" in line["overhead"] and line["ms_per_step"] > 0
+    assert "4 steps per graph" in line["overhead"]["step"] and line["ms_per_step"] > 0
+    bd = line["overhead"]["breakdown"]
+    assert bd["graph_steps"] == 4 and bd["eager_detector_only_ms"] > 0
+    for kind in ("det", "det_frame", "full"):
+        for s in (1, 4, 8):
+            assert bd[f"graph_{kind}_{s}step_ms"] > 0
 
 
 def _torchrun(nproc, port, extra, timeout=400):
