@@ -42,6 +42,21 @@ def gather_symbols(local, total_units: int, world: int, unit: int = 1, group=Non
     return torch.cat(parts) if parts else out[:0]
 
 
+def gather_blocks(local, world: int, block: int, group=None):
+    """All-gather one variable-length byte block per rank (at most `block`
+    bytes each, padded to it): returns [world][block] uint8 on every rank.
+    Configs[4]'s bucketed step gathers each rank's frames of S steps this
+    way (bench.py), one collective per S steps."""
+    import torch
+    import torch.distributed as dist
+
+    buf = torch.zeros(block, dtype=torch.uint8, device=local.device)
+    buf[: local.numel()] = local.reshape(-1)
+    out = torch.empty(block * world, dtype=torch.uint8, device=local.device)
+    dist.all_gather_into_tensor(out, buf, group=group)
+    return out.view(world, block)
+
+
 def frame_symbols(A, symbols: np.ndarray, k: int) -> bytes:
     """Rank-0 framing of the gathered symbol stream (delimited ToReceiver)."""
     return A.frame_symbols(np.ascontiguousarray(symbols, dtype=np.uint8), A.bits_per_symbol(k))

@@ -384,53 +384,66 @@ def run_config(A, D, torch, dist, args, config, rank, world, local, use_dist, st
     gather_ms = (float(np.mean([a.elapsed_time(b) for a, b in gdone_evs])) if gdone_evs else None)
     ms_per_step_eager = None
     breakdown = None
+    bucket = None
     if use_dist and dev_framing and getattr(args, "graph", False) and args.dist_backend == "nccl":
-        # HIP graphs of the step: the detector kernel on a
-        # forked branch; the framing kernel and the RCCL gather of the other
-        # slot (the previous step's symbols) on the capture stream, beside
-        # it. One graph holds S = --graph-steps steps (S even, the slots
-        # alternating step by step; S = 1: two graphs alternate), so one
-        # graph launch per S steps instead of the eager step's ~10 host calls,
-        # which at 8 GPUs (an ~80 us kernel per rank) would set the step time.
-        # Inside a graph, step s's detector waits for step s - 1's framing +
-        # gather (they read the slot it writes) and the framing of step s - 1
-        # for step s - 1's detector: each step is max(detector, framing +
-        # gather) on its critical path.
-        def build(kind, S):
-            """kind: full (detector + framing + gather), det_frame, det."""
+        # HIP graph of S = --graph-steps steps. The graph's
+        # branches do not run concurrently (measured: a framing kernel on a
+        # forked branch beside the detector adds its whole duration to the
+        # step, profiles/round4/r4d/), so the step is built for that: S
+        # detector launches back to back, each into its own slot of an
+        # [S][windows] symbol buffer, then ONE framing launch over all S slots
+        # (S x s_count "streams" of wps windows each: one ToReceiver run per
+        # stream per step) and ONE RCCL all-gather of the S steps' frames: a
+        # bucket of S steps per collective, so the framing launch, the
+        # collective's latency (tens of us over xGMI at 8 ranks) and the graph
+        # launch are paid once per S steps. S = 1 keeps round 3's step (two
+        # alternating one-step graphs, framing + gather of the previous step's
+        # slot on a forked branch) for the breakdown.
+        S = max(1, int(getattr(args, "graph_steps", 1)))
+        SB = max(S, 16 if getattr(args, "breakdown", False) else 1)   # slots for the largest bucket timed
+        symS = torch.empty((SB, n_eval), dtype=torch.uint8, device=dev)
+        frS = torch.empty(max(SB * s_count * fstride, 1), dtype=torch.uint8, device=dev)
+        max_count = -(-n_streams // world)
+
+        def build_bucket(kind, S_):
+            g = torch.cuda.CUDAGraph()
+            gout = None
+            with torch.cuda.graph(g):
+                cs = torch.cuda.current_stream()
+                for s in range(S_):
+                    demod.batch_async(d_pcm, n_eval, symS[s], d_mag, stream=cs.cuda_stream)
+                if kind != "det":
+                    A.frame_streams_async(symS[:S_].reshape(-1), S_ * s_count, wps, bits, frS,
+                                          stream=cs.cuda_stream)
+                if kind == "full":
+                    gout = D.gather_blocks(frS[:S_ * s_count * fstride], world,
+                                           S_ * max_count * fstride, group=group)
+            return [(g, gout)]
+
+        def build_fork(kind):
+            """round 3's step: two one-step graphs, framing + gather of the
+            previous step's slot on a forked branch beside the detector"""
             out = []
-            for g_i in range(1 if S > 1 else 2):
+            for sl in (0, 1):
                 g = torch.cuda.CUDAGraph()
-                gouts = []
+                gout = None
                 with torch.cuda.graph(g):
                     cap = torch.cuda.current_stream()
                     comp.wait_stream(cap)
-                    fdone = None
-                    for s in range(S):
-                        sl = (s if S > 1 else g_i) % 2
-                        if fdone is not None:
-                            comp.wait_event(fdone)      # step s - 1's framing read this slot's twin
-                        with torch.cuda.stream(comp):
-                            demod.batch_async(d_pcm, n_eval, slots[sl], d_mag, stream=comp.cuda_stream)
-                        if kind != "det":
-                            # the previous step's slot, beside this detector kernel
-                            if s > 0:
-                                cap.wait_event(kev)
-                            A.frame_streams_async(slots[1 - sl], s_count, wps, bits, fslots[1 - sl],
-                                                  stream=cap.cuda_stream)
-                            if kind == "full":
-                                gouts.append(D.gather_symbols(fslots[1 - sl][:s_count * fstride], gunits,
-                                                              world, unit=fstride, group=group))
-                            fdone = torch.cuda.Event()
-                            fdone.record(cap)
-                        kev = torch.cuda.Event()
-                        kev.record(comp)
+                    with torch.cuda.stream(comp):
+                        demod.batch_async(d_pcm, n_eval, slots[sl], d_mag, stream=comp.cuda_stream)
+                    if kind != "det":
+                        A.frame_streams_async(slots[1 - sl], s_count, wps, bits, fslots[1 - sl],
+                                              stream=cap.cuda_stream)
+                    if kind == "full":
+                        gout = D.gather_symbols(fslots[1 - sl][:s_count * fstride], gunits, world,
+                                                unit=fstride, group=group)
                     cap.wait_stream(comp)
-                out.append((g, gouts))
+                out.append((g, gout))
             return out
 
-        def time_graphs(graphs, S, n_rep):
-            for i in range(max(4, warm // S)):
+        def time_graphs(graphs, S_, n_rep):
+            for i in range(max(4, -(-warm // S_))):
                 graphs[i % len(graphs)][0].replay()
             if world > 1:
                 dist.barrier()
@@ -446,42 +459,67 @@ def run_config(A, D, torch, dist, args, config, rank, world, local, use_dist, st
                 t = torch.tensor([el], dtype=torch.float64, device=dev)
                 dist.all_reduce(t, op=dist.ReduceOp.MAX)
                 el = float(t.item())
-            return el / (n_rep * S) * 1e3
+            return el / (n_rep * S_) * 1e3
 
-        S = max(1, int(getattr(args, "graph_steps", 1)))
-        if S > 1 and S % 2:
-            S += 1
-        graphs = build("full", S)
-        n_rep = -(-(steps + 1) // S)       # + 1 step: the last replay gathers the last step's frames
         ms_per_step_eager = ms_per_step
-        ms_per_step = time_graphs(graphs, S, n_rep)
-        all_sym = graphs[(n_rep - 1) % len(graphs)][1][-1]   # frames gathered by the last step
-        st["i"] = n_rep * S                                  # the slot holding the last demodulated symbols
+        if S > 1:
+            graphs = build_bucket("full", S)
+            n_rep = -(-steps // S)
+            ms_per_step = time_graphs(graphs, S, n_rep)
+            bucket = {"S": S, "gathered": graphs[0][1]}
+            st["i"] = None
+        else:
+            graphs = build_fork("full")
+            n_rep = steps + 1              # + 1: the last replay gathers the last step's frames
+            ms_per_step = time_graphs(graphs, 1, n_rep)
+            all_sym = graphs[(n_rep - 1) % 2][1]
+            st["i"] = n_rep
         if getattr(args, "breakdown", False):
-            # where the step's time above the kernel goes:
-            # the same detector back to back with no graph, graphs of the
-            # detector alone and with the framing, at 1 and S steps per graph
+            # where the step's time above the kernel goes
             def eager_det():
                 demod.batch_async(d_pcm, n_eval, slots[0], d_mag, stream=comp.cuda_stream)
             breakdown = {"graph_steps": S,
                          "eager_detector_only_ms": round(time_steps(torch, eager_det, steps, warm), 4)}
             for kind in ("det", "det_frame", "full"):
-                for s2 in sorted({1, S, 8}):
-                    gr = build(kind, s2)
-                    breakdown[f"graph_{kind}_{s2}step_ms"] = round(time_graphs(gr, s2, -(-steps // s2)), 4)
-                    del gr
+                breakdown[f"fork_1step_{kind}_ms"] = round(time_graphs(build_fork(kind), 1, steps), 4)
+                for s2 in sorted({S, 8, 16} - {1}):
+                    breakdown[f"bucket_{s2}step_{kind}_ms"] = round(
+                        time_graphs(build_bucket(kind, s2), s2, -(-steps // s2)), 4)
             torch.cuda.synchronize()
 
     # correctness of the timed output: every symbol vs the transmitted one
     # (sliding windows straddle two symbols: compare the aligned ones only)
-    d_sym = slots[(st["i"] - 1) % len(slots)]
+    d_sym = symS[bucket["S"] - 1] if bucket else slots[(st["i"] - 1) % len(slots)]
     if hop == n:
         sym_err = int((d_sym != d_true).sum().item())
     else:
         step_w = n // hop
         sym_err = int((d_sym[::step_w][:W] != d_true).sum().item())
     framed = None
-    if dev_framing:
+    if dev_framing and bucket:
+        # the last bucket's frames of every rank, every step: each must decode
+        # to the transmitted symbols of its streams
+        all_true = D.gather_symbols(d_true, gunits, world, unit=gunit) if world > 1 else d_true
+        if rank == 0:
+            blocks = bucket["gathered"].cpu().numpy()          # [world][padded block]
+            tru = all_true.cpu().numpy().reshape(n_streams, wps)
+            bad = 0
+            for r_ in range(world):
+                first, cnt = D.shard_range(n_streams, r_, world)
+                for s in range(bucket["S"]):
+                    for j in range(cnt):
+                        off = (s * cnt + j) * fstride
+                        back = D.unframe_symbols(A, blocks[r_][off:off + fstride].tobytes(), wps, K)
+                        bad += int((back != tru[first + j]).sum())
+            sym_err = bad
+            framed = {"frames_bytes": int(sum(D.shard_range(n_streams, r_, world)[1]
+                                              for r_ in range(world)) * bucket["S"] * fstride),
+                      "frame_bytes_per_stream": fstride, "bits_per_symbol": bits,
+                      "framing": "device (demod_frame_streams_async, %d steps per launch)" % bucket["S"],
+                      "gathered": "frames of %d steps (RCCL all_gather_into_tensor, %d rank%s)"
+                                  % (bucket["S"], world, "" if world == 1 else "s"),
+                      "roundtrip_ok": bad == 0}
+    elif dev_framing:
         # frames of the last step: gathered (with the gather) or this rank's own
         frames = all_sym if use_dist else fslots[(st["i"] - 1) % len(slots)][:s_count * fstride]
         all_true = D.gather_symbols(d_true, gunits, world, unit=gunit) if world > 1 else d_true
@@ -549,10 +587,12 @@ def run_config(A, D, torch, dist, args, config, rank, world, local, use_dist, st
                          "step_minus_kernel_ms": round(ms_per_step - kernel_ms, 4)}
         if ms_per_step_eager is not None:
             r["overhead"]["ms_per_step_eager"] = round(ms_per_step_eager, 4)
-            r["overhead"]["step"] = ("hip graph (%d step%s per graph): detector kernel on one branch; "
-                                     "framing + RCCL gather of the previous step's symbols on the other"
-                                     % (max(1, int(getattr(args, "graph_steps", 1))),
-                                        "" if int(getattr(args, "graph_steps", 1)) <= 1 else "s"))
+            S_ = max(1, int(getattr(args, "graph_steps", 1)))
+            r["overhead"]["step"] = (
+                "hip graph of %d steps: %d detector launches, one framing launch over their %d slots, "
+                "one RCCL all-gather of the %d steps' frames" % (S_, S_, S_, S_) if S_ > 1 else
+                "hip graph per step: detector kernel on one branch; framing + RCCL gather of the "
+                "previous step's symbols on the other")
         if breakdown is not None:
             r["overhead"]["breakdown"] = breakdown
     if config == "fft":
@@ -1006,8 +1046,10 @@ def main():
                          "(exercises the RCCL path on one GPU)")
     ap.add_argument("--no-graph", dest="graph", action="store_false",
                     help="streams config: time eager steps instead of HIP graphs")
-    ap.add_argument("--graph-steps", type=int, default=1,
-                    help="streams config: steps per HIP graph (1: two graphs alternate the slots)")
+    ap.add_argument("--graph-steps", type=int, default=16,
+                    help="streams config: steps per HIP graph and per framing launch + RCCL gather "
+                         "(a bucket of S steps); 1: round 3's step, one graph per step with the "
+                         "previous step's framing + gather on a forked branch")
     ap.add_argument("--breakdown", action="store_true",
                     help="streams config: also time the step's pieces (detector alone, graphs "
                          "without the gather / framing, 1 / S / 8 steps per graph)")

@@ -16,6 +16,7 @@ cancelling itself, a near-Nyquist tone beside a plan tone):
     silence).
 """
 import json
+import os
 
 import pytest
 
@@ -35,10 +36,14 @@ def torch():
 @pytest.mark.parametrize("case", EM.CASES, ids=[c[0] for c in EM.CASES])
 def test_error_model_every_window(A, O, torch, case):
     rows = []
+    out = os.environ.get("FSKD_ERROR_MODEL_OUT")  # optional: the rows as JSON lines (profiles)
     for fam in EM.FAMILIES:
         r = EM.evaluate(A, O, case, fam, W=4096)
         rows.append(r)
         print(json.dumps({k: v for k, v in r.items()}))
+        if out:
+            with open(out, "a") as f:
+                f.write(json.dumps(r) + "\n")
     for r in rows:
         assert r["tau"] > 0
         assert r["flag_missed"] == 0 and r["flag_extra"] == 0, r

@@ -44,7 +44,8 @@ def test_config5_streams_rccl_gather_world1():
     assert line["symbol_errors"] == 0
     fr = line["framing"]
     assert fr["roundtrip_ok"] and "RCCL" in fr["gathered"]
-    assert fr["frames_bytes"] == 1024 * fr["frame_bytes_per_stream"]
+    # the graph step gathers a bucket of S steps' frames (--graph-steps, default 16)
+    assert fr["frames_bytes"] == 16 * 1024 * fr["frame_bytes_per_stream"]
     ov = line["overhead"]
     assert ov["frame_kernel_ms"] is not None and ov["gather_ms"] is not None
     ps = line["parity_sample"]
@@ -71,12 +72,14 @@ def test_config5_rank_shard_world1():
     assert line["config"]["windows_per_gpu"] == 128 * 2048
     assert line["symbol_errors"] == 0 and line["framing"]["roundtrip_ok"]
     assert line["config"]["workload"].startswith("configs[4]: 128 streams")
-    assert "4 steps per graph" in line["overhead"]["step"] and line["ms_per_step"] > 0
+    assert "hip graph of 4 steps" in line["overhead"]["step"] and line["ms_per_step"] > 0
+    assert "4 steps" in line["framing"]["gathered"]
     bd = line["overhead"]["breakdown"]
     assert bd["graph_steps"] == 4 and bd["eager_detector_only_ms"] > 0
     for kind in ("det", "det_frame", "full"):
-        for s in (1, 4, 8):
-            assert bd[f"graph_{kind}_{s}step_ms"] > 0
+        assert bd[f"fork_1step_{kind}_ms"] > 0
+        for s in (4, 8, 16):
+            assert bd[f"bucket_{s}step_{kind}_ms"] > 0
 
 
 def _torchrun(nproc, port, extra, timeout=400):
