@@ -461,11 +461,18 @@ def run_config(A, D, torch, dist, args, config, rank, world, local, use_dist, st
                 el = float(t.item())
             return el / (n_rep * S_) * 1e3
 
+        def note(msg):
+            if getattr(args, "breakdown", False):
+                print(f"bench.py: streams graph: {msg}", file=sys.stderr, flush=True)
+
         ms_per_step_eager = ms_per_step
+        note(f"eager {ms_per_step:.4f} ms per step; capturing the {S}-step graph")
         if S > 1:
             graphs = build_bucket("full", S)
+            note("captured")
             n_rep = -(-steps // S)
             ms_per_step = time_graphs(graphs, S, n_rep)
+            note(f"timed {ms_per_step:.4f} ms per step")
             bucket = {"S": S, "gathered": graphs[0][1]}
             st["i"] = None
         else:
@@ -482,9 +489,11 @@ def run_config(A, D, torch, dist, args, config, rank, world, local, use_dist, st
                          "eager_detector_only_ms": round(time_steps(torch, eager_det, steps, warm), 4)}
             for kind in ("det", "det_frame", "full"):
                 breakdown[f"fork_1step_{kind}_ms"] = round(time_graphs(build_fork(kind), 1, steps), 4)
+                note(f"fork {kind} {breakdown[f'fork_1step_{kind}_ms']}")
                 for s2 in sorted({S, 8, 16} - {1}):
                     breakdown[f"bucket_{s2}step_{kind}_ms"] = round(
                         time_graphs(build_bucket(kind, s2), s2, -(-steps // s2)), 4)
+                    note(f"bucket {s2} {kind} {breakdown[f'bucket_{s2}step_{kind}_ms']}")
             torch.cuda.synchronize()
 
     # correctness of the timed output: every symbol vs the transmitted one

@@ -16,6 +16,7 @@
 #   testsall[:<args>] pytest -m gpu without -x (all failures in one call)
 #   precision        scripts/precision_probe.py
 #   py:<script args> python3 <script args> (probes under scripts/)
+#   pyt:<secs>:<args> the same under a time limit of its own
 set -o pipefail
 export TMPDIR=/tmp
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -76,6 +77,10 @@ for st in "$@"; do
       timeout -k 10 600 python3 -u scripts/precision_probe.py $arg > "$log" 2>&1 || exit $? ;;
     py)
       timeout -k 10 600 python3 -u $arg > "$log" 2>&1 || exit $? ;;
+    pyt)
+      # pyt:<seconds>:<script args>: python3 under its own shorter time limit
+      secs=${arg%%:*}; rest=${arg#*:}
+      timeout -k 10 "$secs" python3 -u $rest > "$log" 2>&1 || exit $? ;;
     *)
       echo "unknown step $st" >&2; exit 2 ;;
   esac
