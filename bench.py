@@ -830,7 +830,9 @@ def streams_child(args, n_streams: int = 1024, breakdown: bool = False) -> dict:
         env.pop(k, None)
     cmd = [sys.executable, "-u", os.path.abspath(__file__), "--config", "streams", "--force-dist",
            "--streams-total", str(n_streams), "--graph-steps", str(args.graph_steps),
-           "--steps", str(args.steps), "--warmup", str(args.warmup), "--no-cpu-baseline"]
+           # >= 16 replays of the 16-step graph: 2 replays (the driver's
+           # --steps 20) left the shard's rate within +-7 % run to run (r4g)
+           "--steps", str(max(args.steps, 256)), "--warmup", str(args.warmup), "--no-cpu-baseline"]
     if breakdown:
         cmd.append("--breakdown")
     r = subprocess.run(cmd, capture_output=True, timeout=600, cwd=ROOT, env=env)
