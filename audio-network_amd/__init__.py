@@ -149,6 +149,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "demod_max_symbols": (ctypes.c_int, [_P, _SZ]),
         "demod_batch_launches": (ctypes.c_int, [_P, _SZ, ctypes.c_int]),
         "demod_rescue_tau": (ctypes.c_double, [_P]),
+        "demod_rescue_tau64": (ctypes.c_double, [_P]),
         "demodulate": (ctypes.c_int, [_P, _P, _SZ, _P, _SZ]),
         "demodulate_mags": (ctypes.c_int, [_P, _P, _SZ, _P, _P, _SZ]),
         "demod_batch": (ctypes.c_int, [_P, _P, _SZ, _P, _P]),
@@ -343,6 +344,12 @@ class Demodulator:
     def rescue_tau(self) -> float:
         """The decision rescue's threshold factor tau (demod_rescue_tau; 0: off)."""
         return float(self._lib.demod_rescue_tau(self._h))
+
+    @property
+    def rescue_tau64(self) -> float:
+        """The in-kernel rescue's double-stage threshold factor
+        (demod_rescue_tau64; 0: flagged windows take the exact chain)."""
+        return float(self._lib.demod_rescue_tau64(self._h))
 
     def batch_launches(self, n_windows: int, mags: bool = True) -> int:
         """Kernel launches one batch of n_windows makes (demod_batch_launches)."""

@@ -51,6 +51,8 @@ struct demod {
     float amb_floor = 0.f;
     float amb_t2e = 0.f;        // stage 2: threshold^2 = amb_t2e E P_max
     double rcoef[kMaxTones] = {};  // 2 cos(2 pi f_k / fs) in double, the caller's tone order
+    double *d_rot64 = nullptr;  // in-kernel rescue, first step: [k][16][4] segment rotations in double
+    double tau64 = 0.0;         // its threshold factor (rescue_r64 x 12; 0: off)
     double *d_rtw = nullptr;    // FFT: radix-2 twiddles (cos, sin)(-2 pi j / len), [n - 1]
     float coef[kMaxTones] = {};
     float sgn[kMaxTones] = {};  // plain detector, Reinsch form: sign of cos(w_k)
@@ -229,6 +231,28 @@ static double amb_tau(int detector, int log2g, const demod_cfg_t &c, bool reinsc
     const double G = (double)(1 << log2g);
     if (G > 16.0) r *= std::sqrt(G / 16.0);
     return 12.0 * r;
+}
+
+// The in-kernel rescue's first step (rescue_row_seg, demod_internal.h): the
+// flagged row's powers in double by 64-sample segments. Its error against the
+// oracle's double powers is the oracle's own (one 1024-step chain) plus the
+// segmented sum's; both grow like 1 / sin^2 w at the band edges. Measured
+// (tests/test_rescue_model64.py, numpy restatement vs the oracle, ten signal
+// families x bins 0.3 .. 511.7): at most 1.1e-11 sqrt(P_max NE) at bin 1 /
+// 511, 1e-13 .. 1e-12 elsewhere. r64 = 2^-30 = 9.3e-10, x (sin(2 pi / 1024) /
+// s_min)^2 for plans with a tone below bin 1 (or above 511), keeps ~80x over
+// the worst measured; a plan with a tone at 0 or fs/2 exactly gets none (0:
+// every flagged row takes the exact chain).
+static double rescue_r64(const demod_cfg_t &c)
+{
+    const double s1 = std::sin(2.0 * M_PI / 1024.0);
+    double smin = 1.0;
+    for (uint32_t k = 0; k < c.k; ++k)
+        smin = std::min(smin, std::fabs(std::sin(2.0 * M_PI * c.freqs[k] / c.fs)));
+    if (smin < 1e-6) return 0.0;
+    double r = std::ldexp(1.0, -30);
+    if (smin < s1) r *= (s1 / smin) * (s1 / smin);
+    return r;
 }
 
 static int init_device_state(demod_t *st)
@@ -439,6 +463,39 @@ static int init_device_state(demod_t *st)
     // plus the floor tau^2 Q / 16 below which the fp32 error's second-order
     // term could reach the margin.
     for (uint32_t k = 0; k < c.k; ++k) st->rcoef[k] = 2.0 * std::cos(2.0 * M_PI * c.freqs[k] / c.fs);
+    // the in-kernel rescue's first step (n = 1024): per tone and lane segment
+    // j the rotation of the segment's end state into the window's phase,
+    // X = A s1 - B s2, A = e^{-i w (64 j + 63)}, B = e^{-i w (64 j + 64)}, in
+    // double and in the caller's tone order; FSKD_RESCUE_SEG=0 (measurement
+    // switch) sends every flagged row to the exact chain
+    // (the FFT detector: at its tone bins' frequencies b n / fs, with 2 cos
+    // (2 pi b / n), for its own first pass, rescue_fft_seg)
+    const char *seg_env = std::getenv("FSKD_RESCUE_SEG");
+    if (c.n == 1024 && c.k >= 2) {
+        const bool fft = st->detector == kDetFft;
+        std::vector<double> r64((size_t)c.k * 16 * 4 + c.k);
+        demod_cfg_t cb = c;  // the frequencies the first pass evaluates
+        for (uint32_t k = 0; k < c.k; ++k) {
+            if (fft) cb.freqs[k] = (double)st->fft_bins[k] * c.fs / (double)c.n;
+            r64[(size_t)c.k * 64 + k] =
+                fft ? 2.0 * std::cos(2.0 * M_PI * st->fft_bins[k] / (double)c.n) : st->rcoef[k];
+        }
+        for (uint32_t k = 0; k < c.k; ++k) {
+            const double w = fft ? 2.0 * M_PI * st->fft_bins[k] / (double)c.n
+                                 : 2.0 * M_PI * c.freqs[k] / c.fs;
+            for (int j = 0; j < 16; ++j) {
+                const double a = -w * (64.0 * j + 63.0), b = -w * (64.0 * j + 64.0);
+                double *o = &r64[((size_t)k * 16 + j) * 4];
+                o[0] = std::cos(a);
+                o[1] = std::sin(a);
+                o[2] = std::cos(b);
+                o[3] = std::sin(b);
+            }
+        }
+        HIP_TRY(hipMalloc(&st->d_rot64, r64.size() * sizeof(double)));
+        HIP_TRY(hipMemcpy(st->d_rot64, r64.data(), r64.size() * sizeof(double), hipMemcpyHostToDevice));
+        if (!(seg_env && std::strcmp(seg_env, "0") == 0)) st->tau64 = 12.0 * rescue_r64(cb);
+    }
     // measurement switches: FSKD_NO_RESCUE=1 turns the rescue off, =flags
     // keeps the detectors' flags but skips the launch (the flagged windows'
     // symbols keep bit 7: counting them is how bench.py reports the rate)
@@ -480,6 +537,7 @@ static void free_state(demod_t *st)
 {
     if (st->stream) (void)hipStreamSynchronize(st->stream);
     if (st->d_rot) (void)hipFree(st->d_rot);
+    if (st->d_rot64) (void)hipFree(st->d_rot64);
     if (st->d_tw512) (void)hipFree(st->d_tw512);
     if (st->d_tw1024) (void)hipFree(st->d_tw1024);
     if (st->d_bins) (void)hipFree(st->d_bins);
@@ -622,7 +680,7 @@ static int burst_count(const demod_t *st, size_t n_windows, bool mags)
 
 // The direct Goertzel-family kernels at n = 1024 (plain bank, fold, residue;
 // any hop without segment sharing) re-decide their flagged windows inside the
-// detector kernel (rescue_row, demod_internal.h) from the tile they hold in
+// detector kernel (rescue_rows, demod_internal.h) from the tile they hold in
 // LDS: no rescue launch. Segment-shared windows (SLIDE, fold_slide_kernel)
 // and other window lengths keep rescue_kernel's launch; the FFT detector
 // always rescues in its own kernel (rescue_fft.h).
@@ -635,6 +693,12 @@ double demod_rescue_tau(const demod_t *st)
 {
     if (!st || !st->rescue) return 0.0;
     return st->tau;
+}
+
+double demod_rescue_tau64(const demod_t *st)
+{
+    if (!st || !st->rescue || !(rescue_in_kernel(st) || st->detector == kDetFft)) return 0.0;
+    return st->tau64;
 }
 
 int demod_batch_launches(const demod_t *st, size_t n_windows, int with_mags)
@@ -702,6 +766,10 @@ static int enqueue_fft(demod_t *st, const int16_t *d_pcm, size_t n_windows, uint
     // one launch, no symbol scan
     p.rescue = st->rescue && st->rescue_launch ? 1 : 0;
     p.rtw = st->d_rtw;
+    // the rescue's first pass (tones only; with the spectrum stored every
+    // flagged window takes the double FFT, whose spectrum row is the oracle's)
+    p.rot64 = st->d_rot64;
+    p.t2e64 = st->tau64 * st->tau64 * (double)st->cfg.n * (1.0 + 1e-3);
     HIP_TRY(launch_fft_quad(p, s));
     return (int)n_windows;
 }
@@ -747,6 +815,11 @@ static int enqueue_batch(demod_t *st, const int16_t *d_pcm, size_t n_windows, ui
     p.wb_bursts = burst_count(st, n_windows, d_mag != nullptr);
     p.rescue_inline = st->rescue && st->rescue_launch && rescue_in_kernel(st) ? 1 : 0;
     for (uint32_t k = 0; k < st->cfg.k; ++k) p.rcoef[k] = st->rcoef[k];
+    // the in-kernel rescue's tables; its first pass's threshold^2 = t2e64 E
+    // P_max, E = sum x^2 (fp32 in the kernel: the (1 + 1e-3) covers its
+    // rounding), 0: the exact chain only
+    p.rot64 = st->d_rot64;
+    p.t2e64 = st->tau64 * st->tau64 * (double)st->cfg.n * (1.0 + 1e-3);
     for (size_t w0 = 0; w0 < n_windows; w0 += per) {
         const size_t cnt = std::min(per, n_windows - w0);
         p.pcm = d_pcm + w0 * st->cfg.hop;

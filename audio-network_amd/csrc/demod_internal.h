@@ -47,11 +47,18 @@ struct GoertzelParams {
     // write-back bursts (wb_burst): 0 = none, else the number of bursts per
     // XCD in this launch
     int wb_bursts;
-    // in-kernel decision rescue (goertzel.hip, n = 1024, K <= 2 chain path):
-    // flagged windows are re-decided by their own row instead of a rescue
-    // launch; rcoef = 2 cos(2 pi f_k / fs) in double, the caller's tone order
+    // in-kernel decision rescue (the direct Goertzel-family kernels at n =
+    // 1024): flagged windows are re-decided by their own row instead of a
+    // rescue launch; rcoef = 2 cos(2 pi f_k / fs) in double, the caller's tone
+    // order
     int rescue_inline;
     double rcoef[kMaxTones];
+    // rescue_rows' tables: rot64 = [k][16][4] {Ar, Ai, Br, Bi} in double (the
+    // caller's tone order), then rcoef[k] again (read with a per-lane index);
+    // pass 0 leaves a row to the exact chain when margin^2 < t2e64 E P_max;
+    // t2e64 = 0: every flagged row takes the exact chain
+    const double *rot64;
+    double t2e64;
     // decision rescue (rescue.hip): ambiguity test constants.
     // Stage 1 (every window, no per-sample work): the int16 worst case
     // Q >= NE, threshold amb_tq sqrt(P_max), amb_tq = tau sqrt(Q); 0: no
@@ -72,7 +79,7 @@ struct GoertzelParams {
 // tau sqrt(NE P_max) (tau = 12 r: two powers' errors, x 6), or P_max is so
 // small that the second-order term could dominate, the fp32 argmax may
 // differ from the exact one: the detector marks the window ambiguous and the
-// rescue (rescue_row in the detector, or rescue_kernel) re-decides it with
+// rescue (rescue_rows in the detector, or rescue_kernel) re-decides it with
 // the definition's double-precision arithmetic (bit-identical to
 // oracle/fsk_oracle.c). The test runs in two stages: NE <= Q = n^2 2^30 for
 // int16 input, so a window whose margin clears tau sqrt(Q P_max) clears the
@@ -206,60 +213,127 @@ __device__ __forceinline__ long long tile_block(int swz)
 // writes that XCD's L2 back with an agent-scope release, so the output lines
 // leave in a few bursts instead of trickling out between the input's reads;
 // the launch slices this replaces paid a drain and a ramp per slice.
-// In-kernel decision rescue of one window by its 16-lane row (n = 1024; round
-// 3 for the 2-FSK plain bank, round 4 every direct Goertzel-family kernel at
-// n = 1024): lane seg < K runs tone seg's recurrence in double over the
-// window's 1024 samples with exactly rescue_kernel's operations and order (so
-// exactly oracle/fsk_oracle.c's), the row's argmax (ties to the lowest tone)
-// replaces the symbol, and the powers (rounded to fp32) the magnitudes.
+// In-kernel decision rescue of a wave's flagged windows, each by its 16-lane
+// row (n = 1024; round 3 for the 2-FSK plain bank, round 4 every direct
+// Goertzel-family kernel at n = 1024). Two passes of one loop (one copy of
+// the code, so the detector's VGPR budget pays for one):
+//  pass 0 (round 4, when t2e64 > 0): the row's K powers in double, computed
+//    the way the fp32 plain bank computes them — lane seg runs every tone's
+//    recurrence over its own 64 samples, rotates its end state into the
+//    window's phase (rot64) and the row sums — K x 64 double steps per lane
+//    on all 16 lanes, instead of one 1024-step chain per tone on K lanes
+//    (~10x fewer wave instructions at K = 2). These powers are not the
+//    oracle's bits, but they are within |dP| <= r64 sqrt(P_max NE) of them
+//    (r64 ~1e-9: their error plus the oracle's own; demod_api.cpp
+//    rescue_r64, checked by tests/test_rescue_model64.py), so where their
+//    top-2 margin clears tau64 sqrt(NE P_max) (tau64 = 12 r64) the argmax is
+//    the oracle's and the row is decided here (its magnitudes: these powers
+//    rounded to fp32, within 1 ulp of the oracle's). Rows inside that band
+//    (exact ties; margins within ~1e-8 of P_max) go on to
+//  pass 1: lane seg < K runs tone seg's recurrence in double over the
+//    window's 1024 samples with exactly rescue_kernel's operations and order
+//    (so exactly oracle/fsk_oracle.c's: contraction off); the row's argmax
+//    (ties to the lowest tone) replaces the symbol, and the powers (rounded
+//    to fp32) the magnitudes, bit-identical to the oracle's.
 // chunk(q) returns the window's 16-byte chunk q (samples 8q .. 8q + 7) from
-// wherever the kernel holds the tile (its LDS slice: no global round trip per
-// chunk; the next chunk's read is issued before the current one's 24
-// dependent double operations). Every lane of the wave calls it (the
-// shuffles); rows with amb_row false change nothing. The detector leaves the
-// symbol and magnitudes of a flagged row to this function (no second store).
+// wherever the kernel holds the tile (its LDS slice: no global round trip).
+// Every lane of the wave calls it (the shuffles); rows with amb_row false
+// change nothing. The detector leaves the symbol and magnitudes of a flagged
+// row to this function (no second store).
 template <int K, typename Chunk>
-__device__ __forceinline__ void rescue_row(const GoertzelParams &p, long long w, int seg, int lane,
-                                           bool amb_row, Chunk chunk)
+__device__ __forceinline__ void rescue_rows(const GoertzelParams &p, long long w, int seg, int lane,
+                                            bool amb_row, Chunk chunk)
 {
 #pragma clang fp contract(off)
-    double P = 0.0;
-    if (amb_row && seg < K) {
-        const double c = p.rcoef[seg];
-        double s1 = 0.0, s2 = 0.0;
-        u32x4e d = chunk(0);
-        for (int q = 0; q < 128; ++q) {
-            const u32x4e nx = chunk(q < 127 ? q + 1 : q);
-            const unsigned d4[4] = {d.x, d.y, d.z, d.w};
-            double xv[8];
+#pragma unroll 1
+    for (int pass = p.t2e64 > 0.0 ? 0 : 1; pass < 2; ++pass) {
+        const bool exact = pass == 1;
+        const bool run = exact ? amb_row && seg < K : true;  // lanes that run chains
+        const int q0 = exact ? 0 : 8 * seg, q1 = exact ? 128 : 8 * seg + 8;
+        double best = -1.0, second = -1.0, mine = 0.0;
+        float e = 0.f;  // pass 0: the lane's sum x^2
+        int arg = 0;
+#pragma unroll 1
+        for (int t = 0; t < (exact ? 1 : K); ++t) {
+            const int k = exact ? seg : t;
+            const double c = p.rot64[64 * K + (k < K ? k : 0)];  // rcoef[k], read per lane
+            double s1 = 0.0, s2 = 0.0;
+            if (run) {
+#pragma unroll 1
+                for (int q = q0; q < q1; ++q) {
+                    const u32x4e d = chunk(q);
+                    const unsigned d4[4] = {d.x, d.y, d.z, d.w};
+                    if (!exact && t == 0) {
 #pragma unroll
-            for (int e = 0; e < 8; ++e) xv[e] = (double)(short)((d4[e >> 1] >> (16 * (e & 1))) & 0xFFFFu);
+                        for (int i = 0; i < 8; ++i) {
+                            const float xf = (float)(short)((d4[i >> 1] >> (16 * (i & 1))) & 0xFFFFu);
+                            e = __builtin_fmaf(xf, xf, e);
+                        }
+                    }
 #pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                double s = xv[e] + c * s1;
-                s = s - s2;
-                s2 = s1;
-                s1 = s;
+                    for (int i = 0; i < 8; ++i) {
+                        const double x = (double)(short)((d4[i >> 1] >> (16 * (i & 1))) & 0xFFFFu);
+                        double s = x + c * s1;
+                        s = s - s2;
+                        s2 = s1;
+                        s1 = s;
+                    }
+                }
             }
-            d = nx;
-        }
-        const double a = s1 * s1 + s2 * s2;
-        const double b = c * s1;
-        P = a - b * s2;
-    }
-    double best = -1.0;
-    int arg = 0;
+            if (exact) {
+                const double a = s1 * s1 + s2 * s2;
+                const double b = c * s1;
+                mine = run ? a - b * s2 : 0.0;
+            } else {
+                // the rotation's loads after the chain (an offset that depends
+                // on its result): hoisted above it they hold 8 VGPRs through it
+                // (and B's after A's products: 4 VGPRs of table live at a time)
+                int ro = 4 * (k * 16 + seg);
+                asm volatile("" : "+v"(ro) : "v"(s1));
+                const double2 A = *reinterpret_cast<const double2 *>(p.rot64 + ro);
+                double re = A.x * s1, im = A.y * s1;
+                asm volatile("" : "+v"(ro) : "v"(re), "v"(im));
+                const double2 B = *reinterpret_cast<const double2 *>(p.rot64 + ro + 2);
+                re = re - B.x * s2;
+                im = im - B.y * s2;
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
-        const double pk = __shfl(P, (lane & 48) + k);
-        if (pk > best) {
-            best = pk;
-            arg = k;
+                for (int m = 1; m < 16; m <<= 1) {
+                    re += __shfl_xor(re, m);
+                    im += __shfl_xor(im, m);
+                }
+                const double pk = re * re + im * im;
+                if (pk > best) {
+                    second = best;
+                    best = pk;
+                    arg = k;
+                } else if (pk > second) {
+                    second = pk;
+                }
+                if (k == seg) mine = pk;
+            }
         }
-    }
-    if (amb_row) {
-        if (seg == 0) p.sym[w] = (uint8_t)arg;
-        if (p.mag && seg < K) p.mag[w * K + seg] = (float)P;
+        bool still = false;
+        if (exact) {
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const double pk = __shfl(mine, (lane & 48) + k);
+                if (pk > best) {
+                    best = pk;
+                    arg = k;
+                }
+            }
+        } else {
+            // stage threshold^2 = t2e64 E P_max, E the row's sum x^2 (fp32,
+            // within 1e-5: the host's t2e64 carries (1 + 1e-3))
+            const double cth = p.t2e64 * (double)row_sum16(e), dm = best - second;
+            still = !(best > 0.0) || dm * dm < cth * best || 16.0 * best < cth;
+        }
+        if (amb_row && !still) {
+            if (seg == 0) p.sym[w] = (uint8_t)arg;
+            if (p.mag && seg < K) p.mag[w * K + seg] = (float)mine;
+        }
+        amb_row = amb_row && still;
+        if (__ballot(amb_row) == 0) break;
     }
 }
 
@@ -290,6 +364,12 @@ struct FftParams {
     float amb_t2e;           // Parseval, amb_t2e = tau^2)
     int rescue;            // 1: flagged windows are re-decided in the kernel (rescue_fft.h)
     const double *rtw;       // rescue: [1023] (cos, sin), stage len at len / 2 - 1 + j
+    // the rescue's first pass (rescue_fft_seg, tones only): the tone bins'
+    // powers in double by segments, rot64 = [k][16][4] {Ar, Ai, Br, Bi} at the
+    // bins' frequencies, then 2 cos(2 pi b_k / n); t2e64 = 0: every flagged
+    // window takes the double FFT
+    const double *rot64;
+    double t2e64;
 };
 
 // rescue.hip: re-decides every window whose symbol carries kSymAmbiguous.

@@ -1223,8 +1223,22 @@ __device__ __attribute__((always_inline)) inline void fft1024_quad_body(const Ff
                 while (m) {
                     const int src = __builtin_ctzll(m);
                     m &= m - 1;
-                    const unsigned fs = (unsigned)__builtin_amdgcn_readlane((int)f, src);
+                    unsigned fs = (unsigned)__builtin_amdgcn_readlane((int)f, src);
                     const long long gs = gb + (long long)src * stride;
+                    if (p.t2e64 > 0.0 && !p.spec) {
+                        // first pass over the group's flagged windows, one per
+                        // row (rescue_fft_seg); the double FFT for what it leaves
+                        const int row = lane >> 4;
+                        const long long ww = 4 * gs + row;
+                        const bool amb = (fs >> row) & 1u;
+                        const bool still = rescue_fft_seg(
+                            p.pcm + (amb ? ww : 0) * p.hop, p.rot64, p.t2e64, p.k, lane & 15, amb,
+                            p.sym + ww, p.mag ? p.mag + ww * p.k : nullptr);
+                        const unsigned long long sm = __ballot(still);
+                        fs = 0;
+#pragma unroll
+                        for (int q0 = 0; q0 < 4; ++q0) fs |= (unsigned)((sm >> (16 * q0)) & 1ull) << q0;
+                    }
                     for (int q0 = 0; q0 < 4; ++q0)
                         if ((fs >> q0) & 1u) rescue_one(4 * gs + q0, xs);
                 }

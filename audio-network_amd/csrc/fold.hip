@@ -54,7 +54,7 @@ __device__ __forceinline__ float group_sum_f(float v, int log2g)
 // detector transforms, E = sum xf^2 over its N/8 positions (the lanes' acc;
 // amb_t2e = tau^2 N/8): the fold itself is exact, so the fp32 error scales with
 // the folded window, and E <= 8 sum x^2. defer: flagged rows are left to the
-// kernel's rescue_row. Returns the row's ambiguity verdict.
+// kernel's rescue_rows. Returns the row's ambiguity verdict.
 template <int K, bool F16, int MST = -1>
 __device__ __forceinline__ bool fold_decide(const int (&acc)[8], const float4 *r,
                                             const float (&c16)[4], int lane, long long w,
@@ -249,7 +249,7 @@ __global__ __launch_bounds__(64 * WPB) void fold_tile_kernel(GoertzelParams p)
             const bool amb = fold_decide<K, F16, MST>(acc, r, c16, lane, w, live, p, defer);
             if constexpr (kInline) {
                 if (defer && __ballot(amb && live) != 0)
-                    rescue_row<K>(p, w, j, lane, amb && live, [&](int q) { return wl[128 * win_in_tile + q]; });
+                    rescue_rows<K>(p, w, j, lane, amb && live, [&](int q) { return wl[128 * win_in_tile + q]; });
             }
             continue;
         }

@@ -24,6 +24,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "demod_internal.h"
+
 namespace fskd {
 
 typedef __attribute__((address_space(3))) double lds_double;
@@ -176,6 +178,75 @@ __device__ __attribute__((always_inline)) inline void rescue_fft_window(const in
     }
     if (lane == 0) *sym = (uint8_t)arg;
     rf_wave_sync();
+}
+
+// The FFT rescue's first pass (round 4, tones only): the
+// Goertzel family's pass 0 (demod_internal.h rescue_rows) for the four
+// windows of a flagged group, one per 16-lane row as the detector holds them:
+// lane seg runs each tone bin's recurrence in double over its own 64 samples
+// (read once from global memory / L2 into 32 VGPRs: the group loop's
+// registers are dead here), rotates its end state into the window's phase
+// and the row sums. The bins' powers come within r64 sqrt(P_max NE) of the
+// oracle's double FFT (the recurrence's error; the FFT's own is ~1e-15), so
+// where their top-2 margin clears tau64 sqrt(NE P_max) the row is decided
+// here (symbol; tone powers rounded to fp32, within 1 ulp of the oracle's).
+// Returns the lane's row verdict: still ambiguous (for rescue_fft_window).
+// x: the row's window (valid where amb_row); k tones at runtime.
+__device__ __forceinline__ bool rescue_fft_seg(const int16_t *__restrict__ x, const double *__restrict__ rot64,
+                                               double t2e64, int k, int seg, bool amb_row, uint8_t *sym,
+                                               float *mag)
+{
+#pragma clang fp contract(off)
+    unsigned v[32];
+    const unsigned *src = reinterpret_cast<const unsigned *>(x + 64 * seg);
+#pragma unroll
+    for (int i = 0; i < 32; ++i) v[i] = amb_row ? src[i] : 0u;
+    float e = 0.f;
+#pragma unroll
+    for (int i = 0; i < 64; ++i) {
+        const float xf = (float)(short)((v[i >> 1] >> (16 * (i & 1))) & 0xFFFFu);
+        e = __builtin_fmaf(xf, xf, e);
+    }
+    double best = -1.0, second = -1.0, mine = 0.0;
+    int arg = 0;
+#pragma unroll 1
+    for (int t = 0; t < k; ++t) {
+        const double c = rot64[64 * k + t];
+        double s1 = 0.0, s2 = 0.0;
+#pragma unroll
+        for (int i = 0; i < 64; ++i) {
+            const double xd = (double)(short)((v[i >> 1] >> (16 * (i & 1))) & 0xFFFFu);
+            double s = xd + c * s1;
+            s = s - s2;
+            s2 = s1;
+            s1 = s;
+        }
+        const double *r = rot64 + 4 * (t * 16 + seg);
+        double re = r[0] * s1, im = r[1] * s1;
+        re = re - r[2] * s2;
+        im = im - r[3] * s2;
+#pragma unroll
+        for (int m = 1; m < 16; m <<= 1) {
+            re += __shfl_xor(re, m);
+            im += __shfl_xor(im, m);
+        }
+        const double pk = re * re + im * im;
+        if (pk > best) {
+            second = best;
+            best = pk;
+            arg = t;
+        } else if (pk > second) {
+            second = pk;
+        }
+        if (t == seg) mine = pk;
+    }
+    const double cth = t2e64 * (double)row_sum16(e), dm = best - second;
+    const bool still = !(best > 0.0) || dm * dm < cth * best || 16.0 * best < cth;
+    if (amb_row && !still) {
+        if (seg == 0) *sym = (uint8_t)arg;
+        if (mag && seg < k) mag[seg] = (float)mine;
+    }
+    return amb_row && still;
 }
 
 }  // namespace fskd

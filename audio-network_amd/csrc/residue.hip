@@ -388,7 +388,7 @@ void residue_tile_kernel(GoertzelParams p)
                                                         efn);
             if constexpr (K >= 2) {
                 if (defer && __ballot(amb && live) != 0)
-                    rescue_row<K>(p, w, j, lane, amb && live, [&](int q) { return wl[128 * win_in_tile + q]; });
+                    rescue_rows<K>(p, w, j, lane, amb && live, [&](int q) { return wl[128 * win_in_tile + q]; });
             }
             // the next tile's class file overwrites the slice
             __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");

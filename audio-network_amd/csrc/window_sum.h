@@ -196,7 +196,7 @@ __device__ __forceinline__ bool ws_amb_two_stage(float mx, float a0, bool ok0, f
 
 // The decision rescue's ambiguity test in an epilogue (demod_internal.h):
 // stage-1 tq / fl (tq = 0: off), stage-2 t2e, and `defer`: the kernel
-// re-decides flagged rows itself (rescue_row), so their symbol and magnitudes
+// re-decides flagged rows itself (rescue_rows), so their symbol and magnitudes
 // are left to it; otherwise a flagged symbol leaves with kSymAmbiguous set
 // (rescue_kernel, or FSKD_NO_RESCUE=flags).
 struct AmbTest {

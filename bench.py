@@ -1064,6 +1064,10 @@ def main():
     ap.add_argument("--breakdown", action="store_true",
                     help="streams config: also time the step's pieces (detector alone, graphs "
                          "without the gather / framing, 1 / S / 8 steps per graph)")
+    ap.add_argument("--extras-only", default="",
+                    help="comma-separated subset of the default line's extras (measurement calls): "
+                         "fsk8, fft_hop256, fft_hop256_spectrum, host_e2e, error_model, rescue_worst, "
+                         "streams")
     ap.add_argument("--extras-timeout", type=float, default=240.0,
                     help="N > 1: seconds the configs[4] extra may take before a watchdog prints "
                          "the headline line without it and ends every rank")
@@ -1115,8 +1119,14 @@ def main():
         # configs[2] and configs[3], same steps / warmup, in their own buffers
         # (the main run's stay alive for the CPU baseline's parity sample)
         main_keep = {k: r[k] for k in ("d_pcm", "d_sym", "d_mag", "d_true")}
+        only = set(args.extras_only.split(",")) if args.extras_only else None
+
+        def want(key):  # --extras-only: a measurement call's subset of the extras
+            return only is None or key in only
         for key, cfgname, spec in (("fsk8", "fsk8", False), ("fft_hop256", "fft", False),
                                    ("fft_hop256_spectrum", "fft", True)):
+            if not want(key):
+                continue
             rr = run_config(A, D, torch, dist, args, cfgname, rank, world, local, False,
                             args.steps, args.warmup, hop_fft=256, spectrum=spec,
                             rescue_ab=not spec and not args.no_rescue_ab,
@@ -1126,9 +1136,10 @@ def main():
             del rr
             torch.cuda.empty_cache()
         r.update(main_keep)
-        extras["host_e2e"] = host_e2e(A, torch, r)
+        if want("host_e2e"):
+            extras["host_e2e"] = host_e2e(A, torch, r)
         torch.cuda.empty_cache()
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and want("error_model"):
             extras["error_model"] = error_model_headroom(A)
         # the main run's buffers go before the worst-case sweep allocates its own
         keep_cpu = {k: r[k][:65536].clone() if r[k] is not None else None
@@ -1136,19 +1147,21 @@ def main():
         for k in ("d_pcm", "d_sym", "d_mag", "d_true"):
             r.pop(k, None)
         torch.cuda.empty_cache()
-        extras["rescue_worst"] = rescue_worst(A, torch, args.steps, args.warmup)
+        if want("rescue_worst"):
+            extras["rescue_worst"] = rescue_worst(A, torch, args.steps, args.warmup)
         r.update(keep_cpu)
-        extras["streams"] = streams_child(args)
-        # one rank's shard of the 8-GPU run (128 of the 1024 streams), the
-        # same graph step: the projected 8-GPU scaling of configs[4] measured
-        # on one GPU
-        sh = streams_child(args, 128, breakdown=True)
-        if "ms_per_step" in sh and "ms_per_step" in extras["streams"]:
-            sh["projected_scaling_8"] = round(extras["streams"]["ms_per_step"] / sh["ms_per_step"], 3)
-            sh["projection"] = ("streams.ms_per_step / streams_shard.ms_per_step: each of 8 ranks runs "
-                                "this shard's step; the 8-rank all-gather of 8 x the shard's frames "
-                                "replaces this step's world-1 gather beside the kernel")
-        extras["streams_shard"] = sh
+        if want("streams"):
+            extras["streams"] = streams_child(args)
+            # one rank's shard of the 8-GPU run (128 of the 1024 streams), the
+            # same graph step: the projected 8-GPU scaling of configs[4]
+            # measured on one GPU
+            sh = streams_child(args, 128, breakdown=True)
+            if "ms_per_step" in sh and "ms_per_step" in extras["streams"]:
+                sh["projected_scaling_8"] = round(extras["streams"]["ms_per_step"] / sh["ms_per_step"], 3)
+                sh["projection"] = ("streams.ms_per_step / streams_shard.ms_per_step: each of 8 ranks "
+                                    "runs this shard's step; the 8-rank all-gather of 8 x the shard's "
+                                    "frames replaces this step's world-1 gather beside the kernel")
+            extras["streams_shard"] = sh
     elif world > 1 and args.config == "fsk2" and not args.no_extras:
         # the headline is already measured: a failure here (every rank runs the
         # same code, so every rank raises alike) costs the entry, not the line;

@@ -170,6 +170,14 @@ int demod_batch_launches(const demod_t *st, size_t n_windows, int with_mags);
  * §2a). For tests and diagnostics. */
 double demod_rescue_tau(const demod_t *st);
 
+/* The in-kernel rescue's first step (n = 1024 Goertzel-family detectors): a
+ * flagged window's powers in double by 64-sample segments decide it when
+ * their top-2 margin clears tau64 sqrt(NE P_max); windows inside that band
+ * take the exact double chain. Returns tau64 (0: every flagged window takes
+ * the exact chain — other detectors, FSKD_RESCUE_SEG=0, degenerate plans).
+ * For tests and diagnostics. */
+double demod_rescue_tau64(const demod_t *st);
+
 /*
  * Streaming entry point: demodulate(pcm, n) -> symbols.
  * pcm: host pointer to n_frames frames of `channels` interleaved int16

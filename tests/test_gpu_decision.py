@@ -12,6 +12,7 @@ oracle's own double arithmetic (rescue.hip). With the rescue
 switched off (FSKD_NO_RESCUE=1, a measurement switch) the fp32 decisions
 differ from the oracle on some of them: the rescue is what makes them exact.
 """
+import contextlib
 import os
 import zlib
 
@@ -115,21 +116,93 @@ def test_near_ties_follow_exact_argmax(A, O, torch, plan, method):
     Ps = np.sort(ref_P, axis=1)
     sure = (Ps[:, -1] - Ps[:, -2]) < 0.5 * tau * np.sqrt(NE * Ps[:, -1])
     assert sure.sum() >= 20
-    assert np.array_equal(mag[sure].view(np.uint32), ref_P[sure].astype(np.float32).view(np.uint32))
+    ref32 = ref_P[sure].astype(np.float32).view(np.int32)
+    # the in-kernel rescue's first pass decides most of them from its own
+    # double powers (within ~1e-11 of the oracle's: 1 ulp of fp32 at most)
+    assert np.abs(mag[sure].view(np.int32).astype(np.int64) - ref32).max() <= 1
+    # with that pass off every rescued window takes the exact chain (the
+    # double FFT for the FFT detector): the oracle's powers rounded to fp32,
+    # bit for bit, and the same symbols
+    with env(FSKD_RESCUE_SEG="0"):
+        with A.Demodulator(freqs=freqs, method=method) as d:
+            assert d.rescue_tau64 == 0.0
+            sym_x, mag_x = d.batch(x, mags=True)
+    assert np.array_equal(sym_x, sym)
+    assert np.array_equal(mag_x[sure].view(np.int32), ref32)
     # the same windows decided in fp32 alone: some differ from the oracle
-    old = os.environ.get("FSKD_NO_RESCUE")
-    os.environ["FSKD_NO_RESCUE"] = "1"
-    try:
+    with env(FSKD_NO_RESCUE="1"):
         with A.Demodulator(freqs=freqs, method=method) as d:
             sym32 = d.batch(x)
-    finally:
-        if old is None:
-            del os.environ["FSKD_NO_RESCUE"]
-        else:
-            os.environ["FSKD_NO_RESCUE"] = old
     assert (sym32 & 0x80).sum() == 0
     assert (sym32 != ref_sym).sum() > 0
     assert (sym32 == sym).mean() > 0.9
+
+
+@contextlib.contextmanager
+def env(**kv):
+    """Measurement switches read at demod_create."""
+    old = {k: os.environ.get(k) for k in kv}
+    os.environ.update(kv)
+    try:
+        yield
+    finally:
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+
+
+@pytest.mark.parametrize("plan,method", [("FSK2_FREQS", GOERTZEL), ("FSK8_FREQS", FOLDED),
+                                         ("FSK8_ODD", RESIDUE), ("NONINT8", GOERTZEL),
+                                         ("FSK8_FREQS", FFT)])
+def test_rescue_double_ties_take_the_exact_chain(A, O, torch, plan, method):
+    """Windows whose tone powers tie in exact arithmetic (a single impulse:
+    |X_k| = its amplitude at every frequency; two impulses symmetric about the
+    window's middle for pairs of tones) are inside the first pass's double
+    band, so they reach the exact chain: symbols and every magnitude are the
+    oracle's, bit for bit."""
+    freqs = {"FSK2_FREQS": A.FSK2_FREQS, "FSK8_FREQS": A.FSK8_FREQS, "FSK8_ODD": FSK8_ODD,
+             "NONINT8": NONINT8}[plan]
+    rng = np.random.default_rng(zlib.crc32(plan.encode()))
+    W = 512
+    x = np.zeros((W, 1024), np.int16)
+    pos = rng.integers(0, 1024, W)
+    x[np.arange(W), pos] = rng.integers(1000, 30000, W) * rng.choice([-1, 1], W)
+    with A.Demodulator(freqs=freqs, method=method) as d:
+        tau64 = d.rescue_tau64
+        sym, mag = d.batch(x, mags=True)
+    assert tau64 > 0
+    ref_sym, ref_P = (O.fft_demod if method == FFT else O.goertzel)(x, freqs, 1024)
+    assert np.array_equal(sym, ref_sym)
+    assert np.array_equal(mag.view(np.int32), ref_P.astype(np.float32).view(np.int32))
+
+
+@pytest.mark.parametrize("freqs,method,n,hop,expect", [
+    ((1500.0, 3000.0), GOERTZEL, 1024, 1024, True),
+    (tuple(1500.0 + 375.0 * i for i in range(8)), FOLDED, 1024, 1024, True),
+    (FSK8_ODD, RESIDUE, 1024, 1024, True),
+    ((46.875 * 1, 46.875 * 2), GOERTZEL, 1024, 1024, True),      # bin 1: r64 x 1
+    ((46.875 * 0.3, 1500.0), GOERTZEL, 1024, 1024, True),        # below bin 1: scaled
+    ((1500.0, 3000.0), GOERTZEL, 1024, 256, False),              # SLIDE: rescue launch
+    ((1500.0, 3000.0), GOERTZEL, 4096, 4096, False),             # n != 1024
+    ((1500.0, 3000.0), FFT, 1024, 1024, True),                   # FFT: at its bins
+    ((1500.0, 3000.0), FFT, 1024, 256, True),
+    ((0.0, 3000.0), FFT, 1024, 1024, False),                     # a bin at DC: none
+])
+def test_rescue_tau64_is_the_stated_model(A, torch, freqs, method, n, hop, expect):
+    """The handle's tau64 is 12 x tests/test_rescue_model64.r64 (the constant
+    the CPU test checks the first pass's error model with; the FFT detector's
+    at its tone bins' frequencies), and 0 where no first pass runs."""
+    import test_rescue_model64 as M
+    with A.Demodulator(A.make_cfg(n=n, hop=hop, freqs=freqs, method=method)) as d:
+        t = d.rescue_tau64
+    if method == FFT:
+        freqs = tuple(round(f * 1024 / 48000.0) * 48000.0 / 1024 for f in freqs)
+    if expect:
+        assert t == pytest.approx(12.0 * M.r64(freqs), rel=1e-12)
+    else:
+        assert t == 0.0
 
 
 @pytest.mark.parametrize("plan,method", [("FSK8_FREQS", FOLDED), ("FSK8_ODD", RESIDUE),
