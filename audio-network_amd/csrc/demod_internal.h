@@ -228,7 +228,7 @@ __device__ __forceinline__ long long tile_block(int swz)
 //    rescue_r64, checked by tests/test_rescue_model64.py), so where their
 //    top-2 margin clears tau64 sqrt(NE P_max) (tau64 = 12 r64) the argmax is
 //    the oracle's and the row is decided here (its magnitudes: these powers
-//    rounded to fp32, within 1 ulp of the oracle's). Rows inside that band
+//    rounded to fp32, within the model of the oracle's). Rows inside that band
 //    (exact ties; margins within ~1e-8 of P_max) go on to
 //  pass 1: lane seg < K runs tone seg's recurrence in double over the
 //    window's 1024 samples with exactly rescue_kernel's operations and order

@@ -189,7 +189,7 @@ __device__ __attribute__((always_inline)) inline void rescue_fft_window(const in
 // and the row sums. The bins' powers come within r64 sqrt(P_max NE) of the
 // oracle's double FFT (the recurrence's error; the FFT's own is ~1e-15), so
 // where their top-2 margin clears tau64 sqrt(NE P_max) the row is decided
-// here (symbol; tone powers rounded to fp32, within 1 ulp of the oracle's).
+// here (symbol; tone powers rounded to fp32, within the model of the oracle's).
 // Returns the lane's row verdict: still ambiguous (for rescue_fft_window).
 // x: the row's window (valid where amb_row); k tones at runtime.
 __device__ __forceinline__ bool rescue_fft_seg(const int16_t *__restrict__ x, const double *__restrict__ rot64,

@@ -404,14 +404,34 @@ def run_config(A, D, torch, dist, args, config, rank, world, local, use_dist, st
         symS = torch.empty((SB, n_eval), dtype=torch.uint8, device=dev)
         frS = torch.empty(max(SB * s_count * fstride, 1), dtype=torch.uint8, device=dev)
         max_count = -(-n_streams // world)
+        # The bucket's input ring (round 4, --ring, default): S steps' batches
+        # in S consecutive slots of one buffer ([S][windows][n], 64 GiB for
+        # 1024 streams at S = 16: HBM3E holds it), so the bucket's detector
+        # work is ONE launch over S x windows instead of S launches over the
+        # same buffer (each launch pays its ramp and drain: 2.5 us of a 77 us
+        # shard step, profiles/round4/r4g/). Every slot is a copy of the
+        # synthesised batch (the symbols of every step are checked below);
+        # nothing is cached between steps: the ring is 250x the MALL.
+        ring = d_magR = None
+        if getattr(args, "ring", True) and S > 1:
+            ring = torch.empty((S, W, n), dtype=torch.int16, device=dev)
+            for s in range(S):
+                ring[s].copy_(d_pcm)
+            d_magR = None if d_mag is None else torch.empty((S * n_eval, K), dtype=torch.float32,
+                                                             device=dev)
+            torch.cuda.synchronize()
 
-        def build_bucket(kind, S_):
+        def build_bucket(kind, S_, use_ring=False):
             g = torch.cuda.CUDAGraph()
             gout = None
             with torch.cuda.graph(g):
                 cs = torch.cuda.current_stream()
-                for s in range(S_):
-                    demod.batch_async(d_pcm, n_eval, symS[s], d_mag, stream=cs.cuda_stream)
+                if use_ring:
+                    demod.batch_async(ring, S_ * n_eval, symS[:S_].reshape(-1), d_magR,
+                                      stream=cs.cuda_stream)
+                else:
+                    for s in range(S_):
+                        demod.batch_async(d_pcm, n_eval, symS[s], d_mag, stream=cs.cuda_stream)
                 if kind != "det":
                     A.frame_streams_async(symS[:S_].reshape(-1), S_ * s_count, wps, bits, frS,
                                           stream=cs.cuda_stream)
@@ -468,7 +488,7 @@ def run_config(A, D, torch, dist, args, config, rank, world, local, use_dist, st
         ms_per_step_eager = ms_per_step
         note(f"eager {ms_per_step:.4f} ms per step; capturing the {S}-step graph")
         if S > 1:
-            graphs = build_bucket("full", S)
+            graphs = build_bucket("full", S, use_ring=ring is not None)
             note("captured")
             n_rep = -(-steps // S)
             ms_per_step = time_graphs(graphs, S, n_rep)
@@ -494,6 +514,11 @@ def run_config(A, D, torch, dist, args, config, rank, world, local, use_dist, st
                     breakdown[f"bucket_{s2}step_{kind}_ms"] = round(
                         time_graphs(build_bucket(kind, s2), s2, -(-steps // s2)), 4)
                     note(f"bucket {s2} {kind} {breakdown[f'bucket_{s2}step_{kind}_ms']}")
+                if ring is not None:
+                    # the same bucket with its detector work as one launch over the ring
+                    breakdown[f"bucket_{S}step_{kind}_ring_ms"] = round(
+                        time_graphs(build_bucket(kind, S, use_ring=True), S, -(-steps // S)), 4)
+                    note(f"bucket {S} {kind} ring {breakdown[f'bucket_{S}step_{kind}_ring_ms']}")
             torch.cuda.synchronize()
 
     # correctness of the timed output: every symbol vs the transmitted one
@@ -598,8 +623,11 @@ def run_config(A, D, torch, dist, args, config, rank, world, local, use_dist, st
             r["overhead"]["ms_per_step_eager"] = round(ms_per_step_eager, 4)
             S_ = max(1, int(getattr(args, "graph_steps", 1)))
             r["overhead"]["step"] = (
-                "hip graph of %d steps: %d detector launches, one framing launch over their %d slots, "
-                "one RCCL all-gather of the %d steps' frames" % (S_, S_, S_, S_) if S_ > 1 else
+                ("hip graph of %d steps: one detector launch over the %d steps' batches (an input ring "
+                 "of %d slots), one framing launch over their %d symbol slots, one RCCL all-gather of "
+                 "the %d steps' frames" % (S_, S_, S_, S_, S_)) if S_ > 1 and getattr(args, "ring", True)
+                else "hip graph of %d steps: %d detector launches, one framing launch over their %d "
+                     "slots, one RCCL all-gather of the %d steps' frames" % (S_, S_, S_, S_) if S_ > 1 else
                 "hip graph per step: detector kernel on one branch; framing + RCCL gather of the "
                 "previous step's symbols on the other")
         if breakdown is not None:
@@ -923,7 +951,8 @@ def rescue_worst(A, torch, steps, warm, W=1 << 20) -> dict:
     windows of the two-tone worst case (two_tone_stream): 2-FSK (plain bank,
     rescue inside the kernel), 8-FSK (fold F16, inside the kernel), FFT hop
     256 over the same 2^30-sample stream (inside the kernel). Per detector the
-    step with the rescue (shipped), without it (FSKD_NO_RESCUE=1), the
+    step with the rescue (shipped), without it (FSKD_NO_RESCUE=1), with its
+    exact path only (FSKD_RESCUE_SEG=0: no first pass by segments), the
     flagged fraction (FSKD_NO_RESCUE=flags) and a parity sample of the first
     4096 windows against the oracle (every symbol must be the oracle's)."""
     sys.path.insert(0, ROOT)
@@ -943,13 +972,17 @@ def rescue_worst(A, torch, steps, warm, W=1 << 20) -> dict:
         mag = torch.empty((n_eval, K), dtype=torch.float32, device=dev)
         cfg = A.make_cfg(freqs=freqs, n=n, hop=hop, method=method)
         res = {}
-        for mode in ("flags", "1", None):
+        # modes: flags only (count), no rescue, the exact path only (the
+        # rescue's first pass off, FSKD_RESCUE_SEG=0), shipped (last: its
+        # symbols are the parity sample's)
+        for mode in ("flags", "1", "exact", None):
+            var = "FSKD_RESCUE_SEG" if mode == "exact" else "FSKD_NO_RESCUE"
             if mode is not None:
-                os.environ["FSKD_NO_RESCUE"] = mode
+                os.environ[var] = "0" if mode == "exact" else mode
             try:
                 d = A.Demodulator(cfg)
             finally:
-                os.environ.pop("FSKD_NO_RESCUE", None)
+                os.environ.pop(var, None)
             with d:
                 if mode == "flags":
                     d.batch_device(d_pcm, n_eval, sym, mag)
@@ -957,7 +990,8 @@ def rescue_worst(A, torch, steps, warm, W=1 << 20) -> dict:
                     continue
                 fn = (lambda: d.batch_async(d_pcm, n_eval, sym, mag))
                 t = time_steps(torch, fn, max(10, steps // 4), max(4, warm // 8))
-                res["ms_per_step" if mode is None else "ms_per_step_without_rescue"] = round(t, 4)
+                res[{None: "ms_per_step", "1": "ms_per_step_without_rescue",
+                     "exact": "ms_per_step_exact_path_only"}[mode]] = round(t, 4)
                 res["detector"] = {A.METHOD_GOERTZEL: "goertzel", A.METHOD_FOLDED: "folded",
                                    A.METHOD_RESIDUE: "residue", A.METHOD_FFT: "fft1024"}.get(d.method)
                 res["launches_per_step"] = d.batch_launches(n_eval, True)
@@ -1061,6 +1095,9 @@ def main():
                     help="streams config: steps per HIP graph and per framing launch + RCCL gather "
                          "(a bucket of S steps); 1: round 3's step, one graph per step with the "
                          "previous step's framing + gather on a forked branch")
+    ap.add_argument("--no-ring", dest="ring", action="store_false",
+                    help="configs[4] graph bucket: S detector launches over one input buffer instead "
+                         "of one launch over an S-slot input ring")
     ap.add_argument("--breakdown", action="store_true",
                     help="streams config: also time the step's pieces (detector alone, graphs "
                          "without the gather / framing, 1 / S / 8 steps per graph)")

@@ -170,12 +170,13 @@ int demod_batch_launches(const demod_t *st, size_t n_windows, int with_mags);
  * §2a). For tests and diagnostics. */
 double demod_rescue_tau(const demod_t *st);
 
-/* The in-kernel rescue's first step (n = 1024 Goertzel-family detectors): a
- * flagged window's powers in double by 64-sample segments decide it when
- * their top-2 margin clears tau64 sqrt(NE P_max); windows inside that band
- * take the exact double chain. Returns tau64 (0: every flagged window takes
- * the exact chain — other detectors, FSKD_RESCUE_SEG=0, degenerate plans).
- * For tests and diagnostics. */
+/* The in-kernel rescue's first pass (n = 1024 Goertzel-family detectors, and
+ * the FFT detector's tones-only batches at its tone bins): a flagged
+ * window's powers in double by 64-sample segments decide it when their
+ * top-2 margin clears tau64 sqrt(NE P_max); windows inside that band take
+ * the exact double chain (or double FFT). Returns tau64 (0: every flagged
+ * window takes the exact path — rescue launches, FSKD_RESCUE_SEG=0, plans
+ * with a tone at 0 or fs/2). For tests and diagnostics. */
 double demod_rescue_tau64(const demod_t *st);
 
 /*

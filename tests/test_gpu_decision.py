@@ -90,6 +90,8 @@ def test_near_ties_follow_exact_argmax(A, O, torch, plan, method):
         assert d.method == method
         sym, mag = d.batch(x, mags=True)
         tau = d.rescue_tau
+        tau64 = d.rescue_tau64
+    assert tau64 > 0
     oracle = O.fft_demod if method == FFT else O.goertzel
     ref_sym, ref_P = oracle(x, freqs, 1024)
     in_band = check_decisions(sym, mag, ref_sym, ref_P)
@@ -105,8 +107,8 @@ def test_near_ties_follow_exact_argmax(A, O, torch, plan, method):
     assert in_band > 0
     # windows whose oracle margin is well inside the rescue threshold tau
     # sqrt(NE P_max) (NE the window's energy scale, the folded window's for
-    # the fold detector) were rescued: their powers are the
-    # oracle's own double powers, rounded to fp32 (bit-identical arithmetic)
+    # the fold detector) were rescued: their powers are double
+    # powers rounded to fp32 (the first pass's, or the oracle's own exactly)
     xw = x.reshape(W, 1024).astype(np.float64)
     if method == FOLDED:
         xf = xw.reshape(W, 8, 128).sum(axis=1)
@@ -118,8 +120,15 @@ def test_near_ties_follow_exact_argmax(A, O, torch, plan, method):
     assert sure.sum() >= 20
     ref32 = ref_P[sure].astype(np.float32).view(np.int32)
     # the in-kernel rescue's first pass decides most of them from its own
-    # double powers (within ~1e-11 of the oracle's: 1 ulp of fp32 at most)
-    assert np.abs(mag[sure].view(np.int32).astype(np.int64) - ref32).max() <= 1
+    # double powers: each within r64 sqrt(P_max NE) + r64^2 NE of the
+    # oracle's (its error model, tests/test_rescue_model64.py; ~1e-9 of P_max,
+    # so the top powers agree to an ulp of fp32 and a leakage bin at 1e-16 of
+    # P_max may not), then rounded to fp32
+    r64 = tau64 / 12.0
+    Pm = ref_P[sure].max(axis=1, keepdims=True)
+    ne = 1024.0 * (xw[sure] * xw[sure]).sum(axis=1)[:, None]   # the raw window's (fold too)
+    bound = r64 * np.sqrt(Pm * ne) + r64 * r64 * ne + 2.0 ** -23 * np.abs(ref_P[sure])
+    assert (np.abs(mag[sure].astype(np.float64) - ref_P[sure]) <= bound).all()
     # with that pass off every rescued window takes the exact chain (the
     # double FFT for the FFT detector): the oracle's powers rounded to fp32,
     # bit for bit, and the same symbols
