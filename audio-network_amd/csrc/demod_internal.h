@@ -309,7 +309,9 @@ __device__ __forceinline__ void rescue_rows(const GoertzelParams &p, long long w
                 } else if (pk > second) {
                     second = pk;
                 }
-                if (k == seg) mine = pk;
+                // the row's magnitudes now (pass 1 rewrites those of the rows
+                // it takes over): no register holds them across the loop
+                if (k == seg && amb_row && p.mag) p.mag[w * K + seg] = (float)pk;
             }
         }
         bool still = false;
@@ -330,7 +332,7 @@ __device__ __forceinline__ void rescue_rows(const GoertzelParams &p, long long w
         }
         if (amb_row && !still) {
             if (seg == 0) p.sym[w] = (uint8_t)arg;
-            if (p.mag && seg < K) p.mag[w * K + seg] = (float)mine;
+            if (exact && p.mag && seg < K) p.mag[w * K + seg] = (float)mine;
         }
         amb_row = amb_row && still;
         if (__ballot(amb_row) == 0) break;

@@ -1225,9 +1225,14 @@ __device__ __attribute__((always_inline)) inline void fft1024_quad_body(const Ff
                     m &= m - 1;
                     unsigned fs = (unsigned)__builtin_amdgcn_readlane((int)f, src);
                     const long long gs = gb + (long long)src * stride;
-                    if (p.t2e64 > 0.0 && !p.spec) {
-                        // first pass over the group's flagged windows, one per
-                        // row (rescue_fft_seg); the double FFT for what it leaves
+                    // first pass over the group's flagged windows, one per row
+                    // (rescue_fft_seg), where it is cheaper than their double
+                    // FFTs: it costs ~k x 200 double operations per lane for
+                    // the whole group, a double FFT ~800 per flagged window
+                    // (at k = 8 and ~1.8 flagged windows per group both cost
+                    // the same, profiles/round4/r4l/); the double FFT for what
+                    // it leaves
+                    if (p.t2e64 > 0.0 && !p.spec && p.k <= 4 * __builtin_popcount(fs)) {
                         const int row = lane >> 4;
                         const long long ww = 4 * gs + row;
                         const bool amb = (fs >> row) & 1u;

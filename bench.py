@@ -385,6 +385,7 @@ def run_config(A, D, torch, dist, args, config, rank, world, local, use_dist, st
     ms_per_step_eager = None
     breakdown = None
     bucket = None
+    ring_slots = 1
     if use_dist and dev_framing and getattr(args, "graph", False) and args.dist_backend == "nccl":
         # HIP graph of S = --graph-steps steps. The graph's
         # branches do not run concurrently (measured: a framing kernel on a
@@ -404,20 +405,30 @@ def run_config(A, D, torch, dist, args, config, rank, world, local, use_dist, st
         symS = torch.empty((SB, n_eval), dtype=torch.uint8, device=dev)
         frS = torch.empty(max(SB * s_count * fstride, 1), dtype=torch.uint8, device=dev)
         max_count = -(-n_streams // world)
-        # The bucket's input ring (round 4, --ring, default): S steps' batches
-        # in S consecutive slots of one buffer ([S][windows][n], 64 GiB for
-        # 1024 streams at S = 16: HBM3E holds it), so the bucket's detector
-        # work is ONE launch over S x windows instead of S launches over the
-        # same buffer (each launch pays its ramp and drain: 2.5 us of a 77 us
-        # shard step, profiles/round4/r4g/). Every slot is a copy of the
-        # synthesised batch (the symbols of every step are checked below);
-        # nothing is cached between steps: the ring is 250x the MALL.
+        # The bucket's input ring (round 4, --ring, default): R consecutive
+        # steps' batches in R slots of one buffer ([R][windows][n]), so the
+        # bucket's detector work is S / R launches over R x windows each
+        # instead of S launches (each launch pays its ramp and drain: 2.5 us
+        # of a 77 us shard step, profiles/round4/r4g/). R is the largest
+        # power of two <= S whose ring stays within --ring-gib (8 GiB): one
+        # launch over 64 GiB (1024 streams, R = 16) measured slower per step
+        # than 16 launches over 4 GiB (0.642 vs 0.595 ms, profiles/round4/
+        # r4l/), one over 8 GiB (the 128-stream shard) faster (74.5 vs 77.5
+        # us). Every slot is a copy of the synthesised batch (the symbols of
+        # every step are checked below); nothing is cached between steps:
+        # the ring is >= 32x the MALL.
         ring = d_magR = None
+        R = 1
         if getattr(args, "ring", True) and S > 1:
-            ring = torch.empty((S, W, n), dtype=torch.int16, device=dev)
-            for s in range(S):
+            cap = float(getattr(args, "ring_gib", 8.0)) * 2 ** 30
+            while 2 * R <= S and S % (2 * R) == 0 and 2 * R * W * n * 2 <= cap:
+                R *= 2
+        ring_slots = R
+        if R > 1:
+            ring = torch.empty((R, W, n), dtype=torch.int16, device=dev)
+            for s in range(R):
                 ring[s].copy_(d_pcm)
-            d_magR = None if d_mag is None else torch.empty((S * n_eval, K), dtype=torch.float32,
+            d_magR = None if d_mag is None else torch.empty((R * n_eval, K), dtype=torch.float32,
                                                              device=dev)
             torch.cuda.synchronize()
 
@@ -427,8 +438,9 @@ def run_config(A, D, torch, dist, args, config, rank, world, local, use_dist, st
             with torch.cuda.graph(g):
                 cs = torch.cuda.current_stream()
                 if use_ring:
-                    demod.batch_async(ring, S_ * n_eval, symS[:S_].reshape(-1), d_magR,
-                                      stream=cs.cuda_stream)
+                    for c in range(S_ // R):
+                        demod.batch_async(ring, R * n_eval, symS[c * R:(c + 1) * R].reshape(-1), d_magR,
+                                          stream=cs.cuda_stream)
                 else:
                     for s in range(S_):
                         demod.batch_async(d_pcm, n_eval, symS[s], d_mag, stream=cs.cuda_stream)
@@ -505,7 +517,7 @@ def run_config(A, D, torch, dist, args, config, rank, world, local, use_dist, st
             # where the step's time above the kernel goes
             def eager_det():
                 demod.batch_async(d_pcm, n_eval, slots[0], d_mag, stream=comp.cuda_stream)
-            breakdown = {"graph_steps": S,
+            breakdown = {"graph_steps": S, "ring_slots": R,
                          "eager_detector_only_ms": round(time_steps(torch, eager_det, steps, warm), 4)}
             for kind in ("det", "det_frame", "full"):
                 breakdown[f"fork_1step_{kind}_ms"] = round(time_graphs(build_fork(kind), 1, steps), 4)
@@ -623,9 +635,11 @@ def run_config(A, D, torch, dist, args, config, rank, world, local, use_dist, st
             r["overhead"]["ms_per_step_eager"] = round(ms_per_step_eager, 4)
             S_ = max(1, int(getattr(args, "graph_steps", 1)))
             r["overhead"]["step"] = (
-                ("hip graph of %d steps: one detector launch over the %d steps' batches (an input ring "
-                 "of %d slots), one framing launch over their %d symbol slots, one RCCL all-gather of "
-                 "the %d steps' frames" % (S_, S_, S_, S_, S_)) if S_ > 1 and getattr(args, "ring", True)
+                ("hip graph of %d steps: %d detector launch(es), each over %d steps' batches (an input "
+                 "ring of %d slots, <= %g GiB), one framing launch over the %d steps' symbol slots, one "
+                 "RCCL all-gather of the %d steps' frames"
+                 % (S_, S_ // ring_slots, ring_slots, ring_slots, getattr(args, "ring_gib", 8.0), S_, S_))
+                if S_ > 1 and ring_slots > 1
                 else "hip graph of %d steps: %d detector launches, one framing launch over their %d "
                      "slots, one RCCL all-gather of the %d steps' frames" % (S_, S_, S_, S_) if S_ > 1 else
                 "hip graph per step: detector kernel on one branch; framing + RCCL gather of the "
@@ -1095,6 +1109,8 @@ def main():
                     help="streams config: steps per HIP graph and per framing launch + RCCL gather "
                          "(a bucket of S steps); 1: round 3's step, one graph per step with the "
                          "previous step's framing + gather on a forked branch")
+    ap.add_argument("--ring-gib", type=float, default=8.0,
+                    help="configs[4] graph bucket: the input ring's size cap (one detector launch per ring)")
     ap.add_argument("--no-ring", dest="ring", action="store_false",
                     help="configs[4] graph bucket: S detector launches over one input buffer instead "
                          "of one launch over an S-slot input ring")

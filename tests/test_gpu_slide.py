@@ -15,6 +15,17 @@ from decision import check_decisions
 
 pytestmark = pytest.mark.gpu
 
+
+@pytest.fixture(autouse=True)
+def _exact_rescue_everywhere(monkeypatch):
+    """The segment-shared kernels rescue their flagged windows with the exact
+    double chain (rescue launch); the direct kernels' in-kernel rescue first
+    tries a double pass by segments, whose powers are within
+    its model of the exact ones but not the same bits. These tests compare
+    the two kernels' arithmetic bit for bit, so the direct runs take the
+    exact path too (FSKD_RESCUE_SEG=0, read at demod_create)."""
+    monkeypatch.setenv("FSKD_RESCUE_SEG", "0")
+
 MAG_TOL = 1e-5
 GOERTZEL = 1
 FSK8_ODD = tuple(46.875 * (32 + 9 * i) for i in range(8))

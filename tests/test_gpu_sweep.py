@@ -230,13 +230,17 @@ N_SLIDE_CASES = 40
 
 
 @pytest.mark.parametrize("i", range(N_SLIDE_CASES))
-def test_random_segment_shared(A, O, torch, i):
+def test_random_segment_shared(A, O, torch, i, monkeypatch):
     """The segment-shared paths at n = 1024, hop = 64 H < n:
     the plain SLIDE (any plan) and the fold detector's running sums (plans on
     multiples of 8 bins, incl. fold-by-16 plans), drawn with random H, K,
     tone order, batch size and level; against the oracle with the same bar,
-    and bit-identical to the direct kernels (FSKD_NO_SLIDE=1)."""
+    and bit-identical to the direct kernels (FSKD_NO_SLIDE=1). Both rescue
+    their flagged windows with the exact double chain (FSKD_RESCUE_SEG=0: the
+    direct kernels' first pass by segments is within its model of the exact
+    powers, not the same bits)."""
     import os
+    monkeypatch.setenv("FSKD_RESCUE_SEG", "0")
     rng = np.random.default_rng(0x511DE + i + SEED_OFFSET)
     n = 1024
     kind = ("fold", "fold16", "plain")[i % 3]
