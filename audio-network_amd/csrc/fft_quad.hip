@@ -1217,33 +1217,43 @@ __device__ __attribute__((always_inline)) inline void fft1024_quad_body(const Ff
             __builtin_amdgcn_s_waitcnt(0);
             __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
             lds_double *xs = (lds_double *)(slab[wave]);
+            if (p.t2e64 > 0.0 && !p.spec) {
+                // first pass over each flagged group's windows, one per row
+                // (rescue_fft_seg), where it is cheaper than their double
+                // FFTs: it costs ~k x 200 double operations per lane for the
+                // whole group, a double FFT ~800 per flagged window (at k = 8
+                // and ~1.8 flagged windows per group both cost the same,
+                // profiles/round4/r4l/). It clears the flag of every window
+                // it decides; the loop below then finds only what it left.
+                // (A separate loop: folded into the one below it made that
+                // loop's double FFTs 30 % slower, profiles/round4/r4n/.)
+                for (long long gb = g_first; gb < n_groups; gb += 64 * stride) {
+                    const unsigned f = flags4(gb + (long long)lane * stride);
+                    unsigned long long m = __ballot(f != 0);
+                    while (m) {
+                        const int src = __builtin_ctzll(m);
+                        m &= m - 1;
+                        const unsigned fs = (unsigned)__builtin_amdgcn_readlane((int)f, src);
+                        if (p.k > 4 * __builtin_popcount(fs)) continue;
+                        const long long gs = gb + (long long)src * stride;
+                        const int row = lane >> 4;
+                        const long long ww = 4 * gs + row;
+                        const bool amb = (fs >> row) & 1u;
+                        (void)rescue_fft_seg(p.pcm + (amb ? ww : 0) * p.hop, p.rot64, p.t2e64, p.k, lane & 15,
+                                             amb, p.sym + ww, p.mag ? p.mag + ww * p.k : nullptr);
+                    }
+                }
+                __builtin_amdgcn_s_waitcnt(0);
+                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+            }
             for (long long gb = g_first; gb < n_groups; gb += 64 * stride) {
                 const unsigned f = flags4(gb + (long long)lane * stride);
                 unsigned long long m = __ballot(f != 0);
                 while (m) {
                     const int src = __builtin_ctzll(m);
                     m &= m - 1;
-                    unsigned fs = (unsigned)__builtin_amdgcn_readlane((int)f, src);
+                    const unsigned fs = (unsigned)__builtin_amdgcn_readlane((int)f, src);
                     const long long gs = gb + (long long)src * stride;
-                    // first pass over the group's flagged windows, one per row
-                    // (rescue_fft_seg), where it is cheaper than their double
-                    // FFTs: it costs ~k x 200 double operations per lane for
-                    // the whole group, a double FFT ~800 per flagged window
-                    // (at k = 8 and ~1.8 flagged windows per group both cost
-                    // the same, profiles/round4/r4l/); the double FFT for what
-                    // it leaves
-                    if (p.t2e64 > 0.0 && !p.spec && p.k <= 4 * __builtin_popcount(fs)) {
-                        const int row = lane >> 4;
-                        const long long ww = 4 * gs + row;
-                        const bool amb = (fs >> row) & 1u;
-                        const bool still = rescue_fft_seg(
-                            p.pcm + (amb ? ww : 0) * p.hop, p.rot64, p.t2e64, p.k, lane & 15, amb,
-                            p.sym + ww, p.mag ? p.mag + ww * p.k : nullptr);
-                        const unsigned long long sm = __ballot(still);
-                        fs = 0;
-#pragma unroll
-                        for (int q0 = 0; q0 < 4; ++q0) fs |= (unsigned)((sm >> (16 * q0)) & 1ull) << q0;
-                    }
                     for (int q0 = 0; q0 < 4; ++q0)
                         if ((fs >> q0) & 1u) rescue_one(4 * gs + q0, xs);
                 }
