@@ -1,13 +1,13 @@
 #!/usr/bin/env python3
 """profiles/pmc_fft.json and profiles/pmc_fftspec.json (bench.py's
 roofline.traffic of the fft_hop256 and fft_hop256_spectrum entries) from the
-FETCH_SIZE / WRITE_SIZE passes of scripts/gpu_r3_close.sh
-(gpurun_out/<dir>/pmc_{fft,fftspec}_{FETCH,WRITE}_SIZE): round 3, the FFT
-detector with the decision rescue inside the kernel. Averaged over every
+FETCH_SIZE / WRITE_SIZE passes of `scripts/gpu_run.sh <dir> pmc`
+(gpurun_out/<dir>/pmc_{fft,fftspec}_{FETCH,WRITE}_SIZE): the FFT detector
+with the decision rescue inside the kernel. Averaged over every
 launch of the detector kernel in `bench.py --config fft [--spectrum]
---no-rescue-ab`; the counter CSVs are copied to profiles/round3/<dir>/.
+--no-rescue-ab`; the counter CSVs are copied to profiles/<round>/<dir>/.
 
-    python scripts/pmc_fft_r3_json.py r3close
+    python scripts/pmc_fft_r3_json.py r4z [round4]
 
 bytes = KB * 1024; FETCH_SIZE doubled (gfx950 counts half of streaming
 reads, MI355X_MICROARCH.md §HBM; the hop-1024 run of round 2 confirmed the
@@ -34,9 +34,9 @@ def per_launch(path, spec):
     return name, sum(v) / len(v), len(v)
 
 
-def main(tag="r3close"):
+def main(tag="r4z", rnd="round4"):
     src = os.path.join(ROOT, "gpurun_out", tag)
-    dst = os.path.join(ROOT, "profiles", "round3", tag)
+    dst = os.path.join(ROOT, "profiles", rnd, tag)
     os.makedirs(dst, exist_ok=True)
     W, hop, n = 1 << 20, 256, 1024
     Wev = (W * n - n) // hop + 1
@@ -61,9 +61,9 @@ def main(tag="r3close"):
                "method": ("rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate runs of "
                           "bench.py --config fft" + (" --spectrum" if spec else "") +
                           " --no-cpu-baseline --no-rescue-ab --warmup 2 --steps 5 "
-                          "(scripts/gpu_r3_close.sh, gpu_r3_o.sh); bytes = KB*1024, FETCH doubled per "
-                          "MI355X_MICROARCH.md §HBM; round 3: the decision rescue inside the kernel"),
-               "source": f"profiles/round3/{tag}/pmc_{cfg}_FETCH_SIZE.csv, pmc_{cfg}_WRITE_SIZE.csv"}
+                          f"(scripts/gpu_run.sh {tag} pmc); bytes = KB*1024, FETCH doubled per "
+                          "MI355X_MICROARCH.md §HBM; the decision rescue inside the kernel"),
+               "source": f"profiles/{rnd}/{tag}/pmc_{cfg}_FETCH_SIZE.csv, pmc_{cfg}_WRITE_SIZE.csv"}
         with open(os.path.join(ROOT, "profiles", f"pmc_{cfg}.json"), "w") as fh:
             json.dump(out, fh, indent=1)
         print(cfg, launches, round(out["traffic_over_alg"], 5), round(rd / 1e9, 4), round(wr / 1e9, 4))

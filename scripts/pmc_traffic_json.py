@@ -1,12 +1,12 @@
 #!/usr/bin/env python3
 """Per-launch HBM traffic of the detector kernels from the PMC passes of
-scripts/gpu_pmc_traffic.sh (merged into gpurun_out/): writes
+`scripts/gpu_run.sh <dir> pmc` (merged into gpurun_out/<dir>/): writes
 profiles/pmc_<cfg>.json (read by bench.py for roofline.traffic) and copies the
 counter CSVs to profiles/<round>/.
 
-    python scripts/pmc_traffic_json.py [round2]
-    python scripts/pmc_traffic_json.py round3/r3z r3z   # round 3 closing check:
-        # passes under gpurun_out/r3z/ (scripts/gpu_r3_z.sh), CSVs to profiles/round3/r3z/
+    python scripts/pmc_traffic_json.py round4/r4z r4z   # a closing check:
+        # passes under gpurun_out/r4z/, CSVs to profiles/round4/r4z/
+        # (the FFT passes: scripts/pmc_fft_r3_json.py)
 
 Round 2 (scripts/gpu_profile_r2.sh, scripts/gpu_r2_fft.sh) adds the FFT
 detector at hop 256 (configs[3]) and hop 1024.
@@ -78,8 +78,8 @@ def main(rnd="round1", sub=""):
             "hbm_bytes_per_launch": rd + wr, "alg_bytes_per_launch": alg,
             "traffic_over_alg": (rd + wr) / alg,
             "method": ("rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate runs of "
-                       "bench.py (" + ("scripts/gpu_r3_z.sh, round 3 closing check" if sub else
-                                       "scripts/gpu_pmc_traffic.sh, round 2: gpu_profile_r2.sh / gpu_r2_fft.sh")
+                       "bench.py (" + (f"scripts/gpu_run.sh {sub} pmc, closing check" if sub else
+                                       "round 2 profiling scripts")
                        + "); bytes = KB*1024, FETCH doubled "
                        "per MI355X_MICROARCH.md §HBM (gfx950 counts 1/2 of 16 B/lane streaming "
                        "reads); calibration: the 16 B/lane synth_kernel write of 2 GiB reads "
