@@ -1217,6 +1217,7 @@ __device__ __attribute__((always_inline)) inline void fft1024_quad_body(const Ff
             __builtin_amdgcn_s_waitcnt(0);
             __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
             lds_double *xs = (lds_double *)(slab[wave]);
+            bool rescan = true;  // the double FFTs' scan (below) has work
             if (p.t2e64 > 0.0 && !p.spec) {
                 // first pass over each flagged group's windows, one per row
                 // (rescue_fft_seg), where it is cheaper than their double
@@ -1227,9 +1228,13 @@ __device__ __attribute__((always_inline)) inline void fft1024_quad_body(const Ff
                 // it decides; the loop below then finds only what it left.
                 // (A separate loop: folded into the one below it made that
                 // loop's double FFTs 30 % slower, profiles/round4/r4n/.)
+                // (a wave that finds no flagged window here, nearly all of
+                // them, skips the second scan of its symbol bytes)
+                bool any = false;
                 for (long long gb = g_first; gb < n_groups; gb += 64 * stride) {
                     const unsigned f = flags4(gb + (long long)lane * stride);
                     unsigned long long m = __ballot(f != 0);
+                    any = any || m != 0;
                     while (m) {
                         const int src = __builtin_ctzll(m);
                         m &= m - 1;
@@ -1245,8 +1250,9 @@ __device__ __attribute__((always_inline)) inline void fft1024_quad_body(const Ff
                 }
                 __builtin_amdgcn_s_waitcnt(0);
                 __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+                rescan = any;
             }
-            for (long long gb = g_first; gb < n_groups; gb += 64 * stride) {
+            for (long long gb = g_first; rescan && gb < n_groups; gb += 64 * stride) {
                 const unsigned f = flags4(gb + (long long)lane * stride);
                 unsigned long long m = __ballot(f != 0);
                 while (m) {

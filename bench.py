@@ -1169,7 +1169,7 @@ def main():
     extras = {}
     guard = None
     if plain and args.config == "fsk2" and not args.no_extras:
-        # configs[2] and configs[3], same steps / warmup, in their own buffers
+        # configs[2] and configs[3], same warmup, in their own buffers
         # (the main run's stay alive for the CPU baseline's parity sample)
         main_keep = {k: r[k] for k in ("d_pcm", "d_sym", "d_mag", "d_true")}
         only = set(args.extras_only.split(",")) if args.extras_only else None
@@ -1180,8 +1180,12 @@ def main():
                                    ("fft_hop256_spectrum", "fft", True)):
             if not want(key):
                 continue
+            # >= 100 timed steps (>= 25 event-timed launches): at the driver's
+            # --steps 20 the kernel mean rests on 5 launches, and one slow
+            # launch moved 8-FSK's mean by 3 % (profiles/round4/r4z/: p50
+            # 0.3126, mean 0.3197 ms)
             rr = run_config(A, D, torch, dist, args, cfgname, rank, world, local, False,
-                            args.steps, args.warmup, hop_fft=256, spectrum=spec,
+                            max(args.steps, 100), args.warmup, hop_fft=256, spectrum=spec,
                             rescue_ab=not spec and not args.no_rescue_ab,
                             parity_windows=16384 if (cfgname == "fft" and not spec) else 0,
                             parity_every=0 if spec or args.no_cpu_baseline else 1)
@@ -1233,8 +1237,11 @@ def main():
                 r.pop(k, None)
             torch.cuda.empty_cache()
             args.graph = args.dist_backend == "nccl"
+            # >= 16 replays of the 16-step graph bucket, at N ranks and at N = 1
+            # alike (2 replays left the rate within +-7 %, profiles/round4/r4g/)
+            s_steps = max(args.steps, 256) if args.graph else args.steps
             rs = run_config(A, D, torch, dist, args, "streams", rank, world, local, True,
-                            args.steps, args.warmup)
+                            s_steps, args.warmup)
             ent = {"workload": f"configs[4]: 1024 streams x 2048 windows sharded over {world} GPUs",
                    "scaling": "strong", "value": round(rs["total_windows"] * 1024 /
                                                        (rs["ms_per_step"] / 1e3) / 1e6, 1),
@@ -1250,7 +1257,7 @@ def main():
             dist.barrier()
             if rank == 0:
                 r1 = run_config(A, D, torch, dist, args, "streams", 0, 1, local, True,
-                                args.steps, args.warmup, group=g0)
+                                s_steps, args.warmup, group=g0)
                 ent["n1_ms_per_step"] = round(r1["ms_per_step"], 4)
                 ent["n1_kernel_ms"] = round(r1["kernel_ms"], 4)
                 ent["n1_how"] = ("the same 1024 streams on rank 0's GPU alone in this job, the same "
