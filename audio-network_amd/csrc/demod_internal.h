@@ -86,21 +86,29 @@ struct GoertzelParams {
 // exact test too and no per-sample work is spent on it (stage 1); only rows
 // stage 1 flags compute their energy (stage 2), so quiet input (dithered
 // silence, idle-channel noise) is not flagged wholesale.
-// P_max == 0 (every tone power exactly zero: silence) is decided as a tie
-// (tone 0) without a rescue.
+// P_max == 0 (every fp32 tone power exactly zero) is a stage-1 candidate and
+// ambiguous when the window's energy is not zero: input with no energy at the
+// tones (a fold detector's folded window that cancels to a constant, say)
+// leaves the oracle's double powers at its own rounding noise, whose argmax
+// only its own arithmetic reproduces (round 4: tests/test_gpu_error_model.py
+// test_rescued_decisions_every_window found one such window of clipped
+// square waves on the fold-slide path). Digital silence (zero energy) is
+// decided as a tie (tone 0) without a rescue, as the oracle's exact zeros are.
 constexpr uint8_t kSymAmbiguous = 0x80;
 
-// stage 1: margin within tau sqrt(Q P_max) (amb_tq = tau sqrt(Q))
+// stage 1: margin within tau sqrt(Q P_max) (amb_tq = tau sqrt(Q)), or
+// P_max == 0 (a candidate: stage 2 asks for energy)
 __device__ __forceinline__ bool amb_margin(float p1, float p2, float tq, float fl)
 {
-    return tq > 0.f && p1 > 0.f && (p1 - p2 < tq * __builtin_amdgcn_sqrtf(p1) || p1 < fl);
+    return tq > 0.f && (p1 == 0.f || p1 - p2 < tq * __builtin_amdgcn_sqrtf(p1) || p1 < fl);
 }
 
-// stage 2: (p1 - p2)^2 < t2e E p1, or p1 below the floor t2e E / 16
+// stage 2: (p1 - p2)^2 < t2e E p1, or p1 below the floor t2e E / 16, or p1 ==
+// 0 with E > 0
 __device__ __forceinline__ bool amb_energy(float p1, float p2, float e, float t2e)
 {
     const float c = t2e * e, d = p1 - p2;
-    return p1 > 0.f && (d * d < c * p1 || 16.f * p1 < c);
+    return p1 > 0.f ? (d * d < c * p1 || 16.f * p1 < c) : c > 0.f;
 }
 
 // The two stages over a wave: `amb1` is this lane's stage-1 verdict (false for
@@ -171,6 +179,25 @@ __device__ __forceinline__ float seg_energy(Chunk chunk)
         }
     }
     return (a.x + a.y) + (b.x + b.y);
+}
+
+// The same sum one chunk at a time (4 VGPRs of samples live instead of 32:
+// for rare paths inside kernels at their VGPR limit)
+template <typename Chunk>
+__device__ __forceinline__ float seg_energy_serial(Chunk chunk)
+{
+    float e = 0.f;
+#pragma unroll 1
+    for (int i = 0; i < 8; ++i) {
+        const u32x4e d = chunk(i);
+        const unsigned d4[4] = {d.x, d.y, d.z, d.w};
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const float x = (float)(short)((d4[q >> 1] >> (16 * (q & 1))) & 0xFFFFu);
+            e = __builtin_fmaf(x, x, e);
+        }
+    }
+    return e;
 }
 
 // Sum over the 16 lanes of a row (n = 1024 windows), every lane the same total.

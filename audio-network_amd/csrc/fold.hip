@@ -42,6 +42,23 @@ __device__ __forceinline__ float group_sum_f(float v, int log2g)
     return v;
 }
 
+// The energy stage 2 compares against: the folded window's, E_f = sum xf^2.
+// Where it is 0 (every folded sum zero, so every fp32 tone power is too) the
+// row is a candidate only if the window itself is not digital silence:
+// rawfn() (called by every lane, only when some live row of the wave has E_f
+// == 0) returns the raw window's sum x^2, which the P_max == 0 test of
+// demod_internal.h amb_energy then reads (> 0: ambiguous). A window with
+// E_f > 0 has raw energy too, so only its threshold scale matters.
+template <typename RawFn>
+__device__ __forceinline__ float fold_energy(float ef, bool live, RawFn rawfn)
+{
+    if (__ballot(live && ef == 0.f) != 0) {
+        const float er = rawfn();
+        if (ef == 0.f) ef = er;
+    }
+    return ef;
+}
+
 // The decision of one window at n = 1024 from this lane's folded integer sums
 // acc[0..7] (lane j of the window: positions 8j .. 8j + 7 of the N/8 fold,
 // i.e. the even-segment half of positions 8(j & 7).. for j < 8 and the odd
@@ -55,10 +72,11 @@ __device__ __forceinline__ float group_sum_f(float v, int log2g)
 // amb_t2e = tau^2 N/8): the fold itself is exact, so the fp32 error scales with
 // the folded window, and E <= 8 sum x^2. defer: flagged rows are left to the
 // kernel's rescue_rows. Returns the row's ambiguity verdict.
-template <int K, bool F16, int MST = -1>
+template <int K, bool F16, int MST = -1, typename RawFn>
 __device__ __forceinline__ bool fold_decide(const int (&acc)[8], const float4 *r,
                                             const float (&c16)[4], int lane, long long w,
-                                            bool live, const GoertzelParams &p, bool defer)
+                                            bool live, const GoertzelParams &p, bool defer,
+                                            RawFn rawfn)
 {
     float xf[8];
 #pragma unroll
@@ -68,7 +86,7 @@ __device__ __forceinline__ bool fold_decide(const int (&acc)[8], const float4 *r
 #pragma unroll
         for (int q = 0; q < 8; q += 2)
             a = __builtin_elementwise_fma(f32x2f{xf[q], xf[q + 1]}, f32x2f{xf[q], xf[q + 1]}, a);
-        return row_sum16(a.x + a.y);
+        return fold_energy(row_sum16(a.x + a.y), live, rawfn);
     };
     const AmbTest at{p.amb_tq, p.amb_floor, p.amb_t2e, defer};
     if constexpr (F16) {
@@ -207,6 +225,22 @@ __global__ __launch_bounds__(64 * WPB) void fold_tile_kernel(GoertzelParams p)
     const long long stride = (long long)gridDim.x * WPB;
     for (long long t = tile_block(p.xcd_swizzle) * WPB + wave; t < n_tiles; t += stride) {
         const long long wbase = t * wins_per_tile;
+        // the raw window's sum x^2 (fold_energy's fallback: rows whose folded
+        // sums are all zero), from the tile in LDS (LDST) or L2
+        auto rawfn = [&]() {
+            float e;
+            if constexpr (LDST) {
+                e = seg_energy([&](int m) { return wl[128 * win_in_tile + 16 * m + j]; });
+            } else {
+                const long long w = wbase + win_in_tile;
+                const int16_t *sp = p.pcm + w * p.hop + 8 * j;
+                const bool live = w < p.n_windows;
+                e = seg_energy_serial([&](int m) {
+                    return live ? *reinterpret_cast<const u32x4f *>(sp + 8 * g * m) : u32x4f{0u, 0u, 0u, 0u};
+                });
+            }
+            return group_sum_f(e, log2g);
+        };
         long long bytes = ((p.n_windows - wbase - 1) * p.hop + n) * 2;
         if (bytes > 0x7FFFFFF0LL) bytes = 0x7FFFFFF0LL;
         __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
@@ -246,7 +280,7 @@ __global__ __launch_bounds__(64 * WPB) void fold_tile_kernel(GoertzelParams p)
             // LDS slice, window u's chunks at 128 u ..)
             constexpr bool kInline = LDST && K >= 2;
             const bool defer = kInline && p.rescue_inline;
-            const bool amb = fold_decide<K, F16, MST>(acc, r, c16, lane, w, live, p, defer);
+            const bool amb = fold_decide<K, F16, MST>(acc, r, c16, lane, w, live, p, defer, rawfn);
             if constexpr (kInline) {
                 if (defer && __ballot(amb && live) != 0)
                     rescue_rows<K>(p, w, j, lane, amb && live, [&](int q) { return wl[128 * win_in_tile + q]; });
@@ -299,7 +333,7 @@ __global__ __launch_bounds__(64 * WPB) void fold_tile_kernel(GoertzelParams p)
                 float e = 0.f;
 #pragma unroll
                 for (int q = 0; q < 8; ++q) e = fmaf(xf[q], xf[q], e);
-                return row_sum16(e);
+                return fold_energy(row_sum16(e), w < p.n_windows, rawfn);
             };
             window_sum_decide<K, false, MST>(xr, xi, lane, w, w < p.n_windows, p.sym, p.mag, 0,
                                              AmbTest{p.amb_tq, p.amb_floor, p.amb_t2e, false}, efn);
@@ -328,7 +362,7 @@ __global__ __launch_bounds__(64 * WPB) void fold_tile_kernel(GoertzelParams p)
             float e = 0.f;
 #pragma unroll
             for (int q = 0; q < 8; ++q) e = fmaf(xf[q], xf[q], e);
-            return group_sum_f(e, log2g);
+            return fold_energy(group_sum_f(e, log2g), w < p.n_windows, rawfn);
         };
         bool amb;
         const int arg = chain_decide<K>(P, w < p.n_windows, p.amb_tq, p.amb_floor, p.amb_t2e, efn, amb);
@@ -472,7 +506,12 @@ __global__ __launch_bounds__(64 * kPlainWPB) void fold_slide_kernel(GoertzelPara
                 }
             }
             const long long w = wbase + u;
-            fold_decide<K, F16>(acc, r, c16, lane, w, w < p.n_windows, p, false);
+            // the raw window's sum x^2 (fold_energy's fallback): segment j of
+            // window u from the tile in LDS
+            auto rawfn = [&]() {
+                return row_sum16(seg_energy([&](int c) { return wl[8 * (u * H + j) + c]; }));
+            };
+            fold_decide<K, F16>(acc, r, c16, lane, w, w < p.n_windows, p, false, rawfn);
         }
         // the next tile's samples overwrite this one's
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");

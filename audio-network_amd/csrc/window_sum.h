@@ -147,8 +147,9 @@ __device__ __forceinline__ unsigned ws_argmax(unsigned pb0, bool ok0, int o0, un
 // Decision-rescue test over a row (demod_internal.h
 // amb_margin): the window is ambiguous when a second tone's power lies within
 // the threshold of the row's max mx (the max's own lane counts once), or mx is
-// below the floor; mx == 0 is silence, decided without a rescue. Every lane
-// of the row gets the same answer.
+// below the floor; mx == 0 is a stage-1 candidate and ambiguous in stage 2
+// when the row's energy is not zero (t2c > 0; digital silence is decided
+// without a rescue). Every lane of the row gets the same answer.
 // Squared form, (mx - a)^2 < tq^2 mx (mx >= a >= 0; no square root), and
 // the row count from two ballots: a row is ambiguous when two of its lanes
 // hold a near tone (two bits in its 16-bit field) or one lane holds two; the
@@ -170,7 +171,7 @@ __device__ __forceinline__ bool ws_ambiguous_t(float mx, float a0, bool ok0, flo
         const unsigned f = (unsigned)(any >> (16 * r)) & 0xFFFFu;
         if ((f & (f - 1u)) != 0u || ((two >> (16 * r)) & 0xFFFFull) != 0) rows |= 0xFFFFull << (16 * r);
     }
-    return mx > 0.f && (__builtin_amdgcn_inverse_ballot_w64(rows) || mx < flc);
+    return mx > 0.f ? (__builtin_amdgcn_inverse_ballot_w64(rows) || mx < flc) : t2c > 0.f;
 }
 
 __device__ __forceinline__ bool ws_ambiguous(float mx, float a0, bool ok0, float a1, bool ok1,

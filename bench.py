@@ -1023,6 +1023,60 @@ def rescue_worst(A, torch, steps, warm, W=1 << 20) -> dict:
     return out
 
 
+def quiet_cost(A, torch, steps, warm, W=1 << 20) -> dict:
+    """The detectors on quiet input (round 3 flagged every window
+    of it): digital silence (all zeros) and dithered silence (Gaussian sigma
+    3, rounded), 2^20 windows each; per detector the step's time against the
+    same detector on the bench's FSK stream, and the flagged fraction
+    (FSKD_NO_RESCUE=flags). Digital silence is decided without a rescue; the
+    P_max == 0 candidates of stage 1 only cost the energy test."""
+    dev = torch.device("cuda", torch.cuda.current_device())
+    n = 1024
+    d_pcm = torch.empty((W, n), dtype=torch.int16, device=dev)
+    d_true = torch.empty(W, dtype=torch.uint8, device=dev)
+    out = {"workload": f"{W} x 1024-sample windows: FSK (bench stream), digital silence, dithered "
+                       "silence (sigma 3)"}
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(3)
+    for key, freqs, method, hop in (("fsk2", A.FSK2_FREQS, A.METHOD_AUTO, n),
+                                    ("fsk8", A.FSK8_FREQS, A.METHOD_AUTO, n),
+                                    ("fft_hop256", A.FSK8_FREQS, A.METHOD_FFT, 256)):
+        n_eval = (W * n - n) // hop + 1
+        K = len(freqs)
+        sym = torch.empty(n_eval, dtype=torch.uint8, device=dev)
+        mag = torch.empty((n_eval, K), dtype=torch.float32, device=dev)
+        cfg = A.make_cfg(freqs=freqs, n=n, hop=hop, method=method)
+        res = {}
+        for inp in ("fsk", "zeros", "dither3"):
+            if inp == "fsk":
+                A.synth_fsk(cfg, A.BENCH_SEED, W, 8000, 400, d_pcm, d_true)
+            elif inp == "zeros":
+                d_pcm.zero_()
+            else:
+                d_pcm.copy_(torch.round(3.0 * torch.randn((W, n), device=dev, generator=gen)).to(torch.int16))
+            torch.cuda.synchronize()
+            os.environ["FSKD_NO_RESCUE"] = "flags"
+            try:
+                d = A.Demodulator(cfg)
+            finally:
+                os.environ.pop("FSKD_NO_RESCUE", None)
+            with d:
+                d.batch_device(d_pcm, n_eval, sym, mag)
+                flagged = float((sym >= 128).sum().item()) / n_eval
+            with A.Demodulator(cfg) as d:
+                t = time_steps(torch, lambda: d.batch_async(d_pcm, n_eval, sym, mag),
+                               max(20, steps), max(8, warm))
+                if inp == "zeros":
+                    zeros_ok = bool((sym == 0).all().item())
+            res[inp] = {"ms_per_step": round(t, 4), "flagged_frac": round(flagged, 6)}
+        res["zeros"]["all_tone_0"] = zeros_ok
+        out[key] = res
+        del sym, mag
+    del d_pcm, d_true
+    torch.cuda.empty_cache()
+    return out
+
+
 def error_model_headroom(A) -> dict:
     """The decision rescue's error model on the shipped configurations
     (tests/error_model.py; the full sweep is tests/test_gpu_error_model.py):
@@ -1120,7 +1174,7 @@ def main():
     ap.add_argument("--extras-only", default="",
                     help="comma-separated subset of the default line's extras (measurement calls): "
                          "fsk8, fft_hop256, fft_hop256_spectrum, host_e2e, error_model, rescue_worst, "
-                         "streams")
+                         "quiet_cost, streams")
     ap.add_argument("--extras-timeout", type=float, default=240.0,
                     help="N > 1: seconds the configs[4] extra may take before a watchdog prints "
                          "the headline line without it and ends every rank")
@@ -1206,6 +1260,8 @@ def main():
         torch.cuda.empty_cache()
         if want("rescue_worst"):
             extras["rescue_worst"] = rescue_worst(A, torch, args.steps, args.warmup)
+        if want("quiet_cost"):
+            extras["quiet_cost"] = quiet_cost(A, torch, args.steps, args.warmup)
         r.update(keep_cpu)
         if want("streams"):
             extras["streams"] = streams_child(args)

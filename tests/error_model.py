@@ -18,7 +18,9 @@ magnitude is the kernel's fp32 value) and checks, on every window:
      worst error as a fraction of tau, VERDICT r3 item 2);
   2. the kernel flags exactly the windows the stated threshold selects
      (within 1e-3 of it, the fp32 rounding of the test itself; the FFT's
-     stage-2 energy is Parseval's 2 sum_{b<=512} P_b, between NE and 2 NE);
+     stage-2 energy is Parseval's 2 sum_{b<=512} P_b, between NE and 2 NE),
+     and every window whose fp32 tone powers are all exactly 0 unless it is
+     digital silence;
   3. every window it leaves unflagged carries the oracle's symbol.
 Test infrastructure: only tests/ and bench.py's checker legs import this.
 """
@@ -155,12 +157,19 @@ def evaluate(A, O, case, fam, W=4096, threads=16, seed=1):
         return (p1 > 0) & ((m * m < c * p1) | (16 * p1 < c))
     must = sel(lo_ne, 0.999)     # below the threshold: flagged
     may = sel(hi_ne, 1.001)      # above it: not flagged
+    # every fp32 tone power exactly 0: flagged unless the window is digital
+    # silence (the oracle's powers are then its own rounding noise)
+    raw = window_energy(x, n, hop, W, False)
+    zero = (p1 == 0) & (raw > 0)
+    must |= zero
+    may |= zero
     if g.shape[1] < 2:
         must = may = np.zeros(W, bool)
     missed = np.flatnonzero(must & ~flag)
     extra = np.flatnonzero(flag & ~may)
-    # 3. unflagged decisions equal the oracle's (silence: all fp32 powers 0 -> tone 0)
-    silent = (g == 0).all(axis=1)
+    # 3. unflagged decisions equal the oracle's (digital silence: all powers 0
+    # in fp32 and in double -> tone 0)
+    silent = (g == 0).all(axis=1) & (raw == 0)
     wrong = np.flatnonzero(~flag & ~silent & ((sym & 0x7F) != rs))
     return {"case": name, "family": fam, "method": got, "windows": W, "tau": tau,
             "r": r, "worst_ratio_to_model": float(ratio.max()),

@@ -54,3 +54,26 @@ def test_error_model_every_window(A, O, torch, case):
     worst = max(rows, key=lambda r: r["worst_err_frac_of_tau"])
     print("worst error as a fraction of tau:", worst["case"], worst["family"],
           worst["worst_err_frac_of_tau"])
+
+
+@pytest.mark.parametrize("case", EM.CASES, ids=[c[0] for c in EM.CASES])
+def test_rescued_decisions_every_window(A, O, torch, case):
+    """The same paths with the rescue on (shipped): on the families that flag
+    the most windows (two tones at equal power: every window; clipped square
+    waves; a near-Nyquist tone beside a plan tone; dithered silence) every
+    window's symbol is the oracle's and no flag bit is left — through the
+    in-kernel rescue's first pass by segments and its exact chain, the
+    rescue launch (segment-shared windows, n != 1024) and the FFT's."""
+    import numpy as np
+    name, freqs, n, hop, method = case
+    W = 4096
+    for fi, fam in enumerate(("two_tone_equal", "clipped_square", "near_nyquist_tone", "quiet_s3")):
+        blocks = -(-((W - 1) * hop + n) // n)
+        x = EM.family(fam, freqs, n, blocks, 7 + fi)[:(W - 1) * hop + n]
+        with A.Demodulator(A.make_cfg(n=n, hop=hop, freqs=freqs, method=method)) as d:
+            fft = int(d.method) == 2
+            sym = d.batch(x, n_windows=W)
+        rs, _ = (O.fft_demod if fft else O.goertzel)(x, freqs, n, hop=hop, fs=EM.FS, threads=16)
+        assert not (sym & 0x80).any(), (name, fam)
+        bad = np.flatnonzero(sym != rs[:W])
+        assert bad.size == 0, (name, fam, bad[:8].tolist())
