@@ -67,9 +67,12 @@ def test_rescued_decisions_every_window(A, O, torch, case):
     import numpy as np
     name, freqs, n, hop, method = case
     W = 4096
-    for fi, fam in enumerate(("two_tone_equal", "clipped_square", "near_nyquist_tone", "quiet_s3")):
+    seed0 = int(os.environ.get("FSKD_SWEEP_SEED", "7"))
+    fams = (EM.FAMILIES if os.environ.get("FSKD_SWEEP_ALL") else
+            ("two_tone_equal", "clipped_square", "near_nyquist_tone", "quiet_s3"))
+    for fi, fam in enumerate(fams):
         blocks = -(-((W - 1) * hop + n) // n)
-        x = EM.family(fam, freqs, n, blocks, 7 + fi)[:(W - 1) * hop + n]
+        x = EM.family(fam, freqs, n, blocks, seed0 + fi)[:(W - 1) * hop + n]
         with A.Demodulator(A.make_cfg(n=n, hop=hop, freqs=freqs, method=method)) as d:
             fft = int(d.method) == 2
             sym = d.batch(x, n_windows=W)
