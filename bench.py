@@ -1064,8 +1064,9 @@ def quiet_cost(A, torch, steps, warm, W=1 << 20) -> dict:
                 d.batch_device(d_pcm, n_eval, sym, mag)
                 flagged = float((sym >= 128).sum().item()) / n_eval
             with A.Demodulator(cfg) as d:
+                # past the clock transient of the first ~60 launches (MIN_WARMUP)
                 t = time_steps(torch, lambda: d.batch_async(d_pcm, n_eval, sym, mag),
-                               max(20, steps), max(8, warm))
+                               max(40, steps), max(MIN_WARMUP, warm))
                 if inp == "zeros":
                     zeros_ok = bool((sym == 0).all().item())
             res[inp] = {"ms_per_step": round(t, 4), "flagged_frac": round(flagged, 6)}
