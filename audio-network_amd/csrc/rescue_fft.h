@@ -11,14 +11,16 @@
 // same order as the oracle's, so the rescued powers and symbol are the
 // oracle's bit for bit; only where the values wait between stages differs.
 //
-// The wave that decided the group runs it at once, in a wave-uniform branch,
-// with all 64 lanes on one window: the ten stages in three register passes of
+// After its group loop, each wave reads back the symbol bytes of the groups
+// it decided (fft_quad.hip, step 6) and runs this, in a wave-uniform branch,
+// with all 64 lanes on one flagged window: the ten stages in three register passes of
 // 16 points per lane — positions 16 l + e of the bit-reversed array (stages
 // len 2 .. 16 inside the lane), then (l & 15) + 16 m + 256 (l >> 4) (len 32 ..
 // 256), then l + 64 q + 256 m (len 512, 1024) — with two exchanges through
 // the wave's own 1088-double LDS slab (re, then im). Flagged windows are rare
 // (0.04 % of the hop-256 bench stream), so the cost spreads over the
-// detector's grid: no second launch and no scan of the symbol bytes.
+// detector's grid: no second launch. (Round 4: a first pass by segments,
+// rescue_fft_seg below, takes the tone-only batches' flagged groups first.)
 #pragma once
 
 #include <hip/hip_runtime.h>
