@@ -107,6 +107,33 @@ class DemodReceiverError(ctypes.Structure):
     _fields_ = [("audio_underflow", ctypes.c_int), ("audio_decode_error", ctypes.c_int)]
 
 
+class DemodErrorModel(ctypes.Structure):
+    """demod_error_model_t (include/demod.h): the decision rescue's derived bounds."""
+    _fields_ = [("method", ctypes.c_int32), ("energy", ctypes.c_int32)] + [
+        (f, ctypes.c_double) for f in ("rho_det", "rho_ref", "rho_first", "tau", "tau64", "t2e",
+                                        "t2e64", "amb_d")]
+
+
+class DemodPlanInfo(ctypes.Structure):
+    """demod_plan_info_t (include/demod.h): a configuration's tone plan and constants."""
+    _fields_ = [
+        ("method", ctypes.c_int32), ("log2g", ctypes.c_int32), ("reinsch", ctypes.c_int32),
+        ("f16", ctypes.c_int32), ("dcls", ctypes.c_int32), ("slide", ctypes.c_int32),
+        ("perm", ctypes.c_uint64),
+        ("slot_tone", ctypes.c_int32 * DEMOD_MAX_TONES),
+        ("zcls", ctypes.c_int32 * DEMOD_MAX_TONES),
+        ("fft_bins", ctypes.c_int32 * DEMOD_MAX_TONES),
+        ("coef", ctypes.c_float * DEMOD_MAX_TONES),
+        ("sgn", ctypes.c_float * DEMOD_MAX_TONES),
+        ("rcoef", ctypes.c_double * DEMOD_MAX_TONES),
+        ("rot_len", ctypes.c_uint32),
+        ("rot64_len", ctypes.c_uint32),
+    ]
+
+
+ENERGY_RAW, ENERGY_FOLDED, ENERGY_PARSEVAL = 0, 1, 2
+
+
 class DemodError(RuntimeError):
     def __init__(self, code: int, what: str = ""):
         self.code = code
@@ -137,6 +164,10 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         import torch  # noqa: F401
     except ImportError:
         pass
+    if path != LIB_PATH:
+        import sys
+        print(f"audio_network_amd: FSKD_LIB override active, loading {path} (measurement A/B "
+              "only; entry points that build lacks stay unbound)", file=sys.stderr)
     lib = ctypes.CDLL(path)
     sig = {
         "demod_cfg_default": (None, [ctypes.POINTER(DemodCfg)]),
@@ -150,6 +181,9 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "demod_batch_launches": (ctypes.c_int, [_P, _SZ, ctypes.c_int]),
         "demod_rescue_tau": (ctypes.c_double, [_P]),
         "demod_rescue_tau64": (ctypes.c_double, [_P]),
+        "demod_error_model": (ctypes.c_int, [ctypes.POINTER(DemodCfg), ctypes.POINTER(DemodErrorModel)]),
+        "demod_plan_info": (ctypes.c_int, [ctypes.POINTER(DemodCfg), ctypes.POINTER(DemodPlanInfo),
+                                           _P, _SZ, _P, _SZ]),
         "demodulate": (ctypes.c_int, [_P, _P, _SZ, _P, _SZ]),
         "demodulate_mags": (ctypes.c_int, [_P, _P, _SZ, _P, _P, _SZ]),
         "demod_batch": (ctypes.c_int, [_P, _P, _SZ, _P, _P]),
@@ -241,6 +275,39 @@ def make_cfg(fs: float = 48000.0, n: int = 1024, hop: Optional[int] = None,
     for i in range(DEMOD_MAX_TONES):
         cfg.freqs[i] = float(freqs[i]) if i < len(freqs) else 0.0
     return cfg
+
+
+def error_model(cfg: DemodCfg) -> dict:
+    """demod_error_model: the decision rescue's bounds for cfg's tone plan (no GPU)."""
+    m = DemodErrorModel()
+    rc = load_library().demod_error_model(ctypes.byref(cfg), ctypes.byref(m))
+    if rc != DEMOD_OK:
+        raise DemodError(rc, "demod_error_model")
+    return {f: getattr(m, f) for f, _ in DemodErrorModel._fields_}
+
+
+def plan_info(cfg: DemodCfg) -> dict:
+    """demod_plan_info: the plan cfg runs and its fp32 constants (no GPU); `rot`
+    as float32 [rot_len][4], `rot64` as float64 (empty without a first pass)."""
+    lib = load_library()
+    info = DemodPlanInfo()
+    rc = lib.demod_plan_info(ctypes.byref(cfg), ctypes.byref(info), None, 0, None, 0)
+    if rc != DEMOD_OK:
+        raise DemodError(rc, "demod_plan_info")
+    rot = np.zeros((info.rot_len, 4), np.float32)
+    rot64 = np.zeros(info.rot64_len, np.float64)
+    rc = lib.demod_plan_info(ctypes.byref(cfg), ctypes.byref(info), _ptr(rot), rot.size,
+                             _ptr(rot64), rot64.size)
+    if rc != DEMOD_OK:
+        raise DemodError(rc, "demod_plan_info")
+    out = {f: getattr(info, f) for f, _ in DemodPlanInfo._fields_}
+    for f in ("slot_tone", "zcls", "fft_bins", "coef", "sgn", "rcoef"):
+        out[f] = np.array(out[f][:cfg.k])
+    out["coef"] = out["coef"].astype(np.float32)
+    out["sgn"] = out["sgn"].astype(np.float32)
+    out["rot"] = rot
+    out["rot64"] = rot64
+    return out
 
 
 def _ptr(a) -> int:

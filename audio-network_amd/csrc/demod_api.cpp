@@ -21,6 +21,7 @@
 
 #include "../../include/demod.h"
 #include "demod_internal.h"
+#include "plan.h"
 
 using namespace fskd;
 
@@ -52,7 +53,9 @@ struct demod {
     float amb_t2e = 0.f;        // stage 2: threshold^2 = amb_t2e E P_max
     double rcoef[kMaxTones] = {};  // 2 cos(2 pi f_k / fs) in double, the caller's tone order
     double *d_rot64 = nullptr;  // in-kernel rescue, first step: [k][16][4] segment rotations in double
-    double tau64 = 0.0;         // its threshold factor (rescue_r64 x 12; 0: off)
+    double tau64 = 0.0;         // its threshold factor (error_model; 0: off)
+    double t2e64 = 0.0;         // pass 0's margin test, threshold^2 = t2e64 E P_max
+    float amb_d = 0.f;          // fold detector: the oracle's share of stage 2 (E_eff = (sqrt E + d)^2)
     double *d_rtw = nullptr;    // FFT: radix-2 twiddles (cos, sin)(-2 pi j / len), [n - 1]
     float coef[kMaxTones] = {};
     float sgn[kMaxTones] = {};  // plain detector, Reinsch form: sign of cos(w_k)
@@ -143,117 +146,7 @@ void demod_cfg_default(demod_cfg_t *cfg)
     cfg->freqs[1] = 3000.0;
 }
 
-// Tone i's bin f_i n / fs if it is an integer (within rounding), else -1.
-static long long integer_bin(const demod_cfg_t &c, uint32_t i)
-{
-    const double b = c.freqs[i] * c.n / c.fs;
-    const double r = std::nearbyint(b);
-    if (std::fabs(b - r) > 1e-9 * std::max(1.0, b)) return -1;
-    return (long long)r;
-}
-
-// Every tone on an integer bin (residue.hip's identity).
-static bool residue_eligible(const demod_cfg_t &c)
-{
-    for (uint32_t i = 0; i < c.k; ++i)
-        if (integer_bin(c, i) < 0) return false;
-    return true;
-}
-
-// Every tone on an integer bin that is a multiple of 8 (fold.hip's identity).
-static bool fold_eligible(const demod_cfg_t &c)
-{
-    for (uint32_t i = 0; i < c.k; ++i) {
-        const long long b = integer_bin(c, i);
-        if (b < 0 || b % 8 != 0) return false;
-    }
-    return true;
-}
-
-static int validate(const demod_cfg_t *c)
-{
-    if (!c) return DEMOD_BAD_ARG;
-    if (!(c->fs > 0.0) || !std::isfinite(c->fs)) return DEMOD_BAD_ARG;
-    if (c->k < 1 || c->k > DEMOD_MAX_TONES) return DEMOD_BAD_ARG;
-    // Goertzel tiles: n = 64 * 2^j, 64 <= n <= 4096
-    if (c->n < 64 || c->n > 4096 || (c->n & (c->n - 1))) return DEMOD_BAD_ARG;
-    if (c->hop < 8 || c->hop > c->n || (c->hop % 8)) return DEMOD_BAD_ARG;
-    if (c->channels != 1 && c->channels != 2) return DEMOD_BAD_ARG;
-    if (c->channels == 2 && (c->channel_mode < 0 || c->channel_mode > 2)) return DEMOD_BAD_ARG;
-    if (c->method != DEMOD_METHOD_AUTO && c->method != DEMOD_METHOD_GOERTZEL &&
-        c->method != DEMOD_METHOD_FOLDED && c->method != DEMOD_METHOD_FFT &&
-        c->method != DEMOD_METHOD_RESIDUE)
-        return DEMOD_UNIMPLEMENTED;
-    if (c->method == DEMOD_METHOD_FFT && c->n != 1024) return DEMOD_UNIMPLEMENTED;
-    if (c->lead_in > 0x7FFFFFFFu) return DEMOD_BAD_ARG;
-    if (c->method == DEMOD_METHOD_FOLDED && !fold_eligible(*c)) return DEMOD_BAD_ARG;
-    if (c->method == DEMOD_METHOD_RESIDUE && !residue_eligible(*c)) return DEMOD_BAD_ARG;
-    for (uint32_t i = 0; i < c->k; ++i)
-        if (!std::isfinite(c->freqs[i]) || c->freqs[i] < 0.0 || c->freqs[i] > c->fs / 2)
-            return DEMOD_BAD_ARG;
-    return DEMOD_OK;
-}
-
-// Decision rescue threshold factor tau per detector and tone plan (DESIGN.md
-// §2a). r = the largest fp32 power error a detector showed against the double
-// oracle, as a fraction of sqrt(P_max NE) (NE the energy of the window the
-// detector transforms: n sum x^2, or (n/8) sum xf^2 for the fold detector),
-// over every signal family and kernel path of scripts/precision_probe.py
-// (profiles/round3/precision_probe.log; round 4: tests/test_gpu_error_model.py
-// asserts the model on every window of an adversarial sweep): plain bank
-// (direct, SLIDE, Reinsch, any n) 3.3e-6 at the survey plans' lowest tone
-// (|sin w| = 0.195; round 3 measured 2.67e-6 over ten families, the round-4
-// sweep found up to 1.126x that on pure tones and two equal tones, so r
-// covers the worst observed with 10 % to spare), fold / fold-slide / residue
-// 1.19e-6 (n = 1024), FFT 2.64e-7. A margin carries the errors of two
-// powers: tau = 2 r x 6 (safety).
-// Plan-aware factors (Goertzel family):
-//  * the recurrence's conditioning: the fp32 coefficient 2cos(w) moves the
-//    chain's frequency by d(2cos w) / (2 sin w), and the chain state grows like
-//    1 / sin w, so the error grows like 1 / sin^2 w: r scales with
-//    (0.195 / s_min)^2 for the lowest |sin w| of the plan when that is below
-//    the measured plans' (down to the Reinsch switch at 0.1: x 3.8). Reinsch
-//    plans keep the plain figure (measured 3.0e-7 there: 9x headroom);
-//  * longer windows sum more segments: x sqrt(G / 16) for G = n / 64 > 16
-//    (measured flat from n = 256 to 4096, kept as margin);
-//  * fold and residue at n != 1024 (not probed there) take the plain bank's r.
-static double amb_tau(int detector, int log2g, const demod_cfg_t &c, bool reinsch)
-{
-    if (detector == kDetFft) return 12.0 * 2.64e-7;
-    double r = ((detector == kDetFolded || detector == kDetResidue) && log2g == 4) ? 1.19e-6 : 3.3e-6;
-    constexpr double kSinRef = 0.19509032201612825;  // sin(2 pi 1500 / 48000): bin 32 of 1024
-    if (!reinsch) {
-        double smin = 1.0;
-        for (uint32_t k = 0; k < c.k; ++k)
-            smin = std::min(smin, std::fabs(std::sin(2.0 * M_PI * c.freqs[k] / c.fs)));
-        if (smin < kSinRef) r *= (kSinRef / smin) * (kSinRef / smin);
-    }
-    const double G = (double)(1 << log2g);
-    if (G > 16.0) r *= std::sqrt(G / 16.0);
-    return 12.0 * r;
-}
-
-// The in-kernel rescue's first step (rescue_row_seg, demod_internal.h): the
-// flagged row's powers in double by 64-sample segments. Its error against the
-// oracle's double powers is the oracle's own (one 1024-step chain) plus the
-// segmented sum's; both grow like 1 / sin^2 w at the band edges. Measured
-// (tests/test_rescue_model64.py, numpy restatement vs the oracle, ten signal
-// families x bins 0.3 .. 511.7): at most 1.1e-11 sqrt(P_max NE) at bin 1 /
-// 511, 1e-13 .. 1e-12 elsewhere. r64 = 2^-30 = 9.3e-10, x (sin(2 pi / 1024) /
-// s_min)^2 for plans with a tone below bin 1 (or above 511), keeps ~80x over
-// the worst measured; a plan with a tone at 0 or fs/2 exactly gets none (0:
-// every flagged row takes the exact chain).
-static double rescue_r64(const demod_cfg_t &c)
-{
-    const double s1 = std::sin(2.0 * M_PI / 1024.0);
-    double smin = 1.0;
-    for (uint32_t k = 0; k < c.k; ++k)
-        smin = std::min(smin, std::fabs(std::sin(2.0 * M_PI * c.freqs[k] / c.fs)));
-    if (smin < 1e-6) return 0.0;
-    double r = std::ldexp(1.0, -30);
-    if (smin < s1) r *= (s1 / smin) * (s1 / smin);
-    return r;
-}
+static int validate(const demod_cfg_t *c) { return validate_cfg(c); }
 
 static int init_device_state(demod_t *st)
 {
@@ -277,34 +170,12 @@ static int init_device_state(demod_t *st)
     st->cus = prop.multiProcessorCount;
     HIP_TRY(hipStreamCreateWithFlags(&st->stream, hipStreamNonBlocking));
 
-    int g = (int)(c.n / 64), lg = 0;
-    while ((1 << lg) < g) ++lg;
-    st->log2g = lg;
-    // AUTO: the plain bank is HBM-bound up to K = 2 and within
-    // a few % of it to K = 4; beyond, fold when every tone is a multiple of 8
-    // bins (K >= 3), else fold per residue class when every tone is on an
-    // integer bin (K >= 5: at K = 3, 4 the plain bank measured as fast).
-    // Overlapping windows at n = 1024 with hop a multiple of 64 share their
-    // 64-sample segments: the plain bank computes each segment once (SLIDE,
-    // goertzel.hip) and the fold detector runs its folded sums forward from
-    // window to window (fold_slide_kernel, fold.hip). The
-    // residue detector has no segment-shared form, so AUTO keeps the plain
-    // SLIDE over it up to hop 384 (8-FSK on bins 32 + 9 i: 0.70 vs 0.90 ms at
-    // hop 256, 0.63 vs 0.64 at 384, 0.58 vs 0.52 at 512).
-    // FSKD_NO_SLIDE=1 (measurement switch for probes) runs the direct kernels.
-    const char *no_slide_env = std::getenv("FSKD_NO_SLIDE");
-    const bool slide = lg == 4 && c.hop < c.n && c.hop % 64 == 0 &&
-                       !(no_slide_env && no_slide_env[0] == '1');
-    st->detector = kDetGoertzel;
-    if (c.method == DEMOD_METHOD_FOLDED) st->detector = kDetFolded;
-    else if (c.method == DEMOD_METHOD_RESIDUE) st->detector = kDetResidue;
-    else if (c.method == DEMOD_METHOD_AUTO) {
-        if (c.k >= 3 && fold_eligible(c)) st->detector = kDetFolded;
-        else if (!(slide && c.hop <= 384) && c.k >= 5 && residue_eligible(c))
-            st->detector = kDetResidue;
-    }
-    if (c.method == DEMOD_METHOD_FFT) {
-        st->detector = kDetFft;
+    Plan pl;
+    build_plan(c, pl);
+    st->log2g = pl.log2g;
+    st->detector = pl.detector;
+    const bool slide = pl.slide;
+    if (st->detector == kDetFft) {
         std::vector<float> t1(1024), t2(1024);
         for (int m = 0; m < 512; ++m) {
             t1[2 * m] = (float)std::cos(-2.0 * M_PI * m / 512.0);
@@ -314,10 +185,9 @@ static int init_device_state(demod_t *st)
         }
         std::vector<int> bins(c.k);
         for (uint32_t k = 0; k < c.k; ++k) {
-            long b = std::lround(c.freqs[k] * c.n / c.fs);
-            bins[k] = (int)std::min<long>(std::max<long>(b, 0), c.n / 2);
-            st->fft_bins[k] = bins[k];
-            st->fft_slot[k] = fft_quad_slot(bins[k]);
+            bins[k] = pl.fft_bins[k];
+            st->fft_bins[k] = pl.fft_bins[k];
+            st->fft_slot[k] = pl.fft_slot[k];
         }
         // the rescue's radix-2 twiddles: stage len (2 .. n), j < len / 2 at
         // len / 2 - 1 + j, each the (cos, sin) of (-2 pi / len) j exactly as
@@ -342,159 +212,29 @@ static int init_device_state(demod_t *st)
         HIP_TRY(hipMemcpy(st->d_tw1024, t2.data(), t2.size() * sizeof(float), hipMemcpyHostToDevice));
         HIP_TRY(hipMemcpy(st->d_bins, bins.data(), bins.size() * sizeof(int), hipMemcpyHostToDevice));
     }
-    // Rotation of each lane's piece into window phase, X += A s1 - B s2:
-    //   Goertzel: segment j = samples [64j, 64j+64): A = e^{-jw(64j+63)}, B = e^{-jw(64j+64)}
-    //   Folded:   folded samples [8j, 8j+8):         A = e^{-jw(8j+7)},   B = e^{-jw(8j+8)}
-    //   Residue:  as Folded, with the class input s = (lo, hi) mapped to the
-    //             complex s_c = (alpha lo + beta hi) + i gamma hi, folded into
-    //             X = lo1 C1 + hi1 C2 + lo2 C3 + hi2 C4 (residue.hip):
-    //             C1 = alpha A, C2 = beta A + gamma iA, C3 = -alpha B, C4 = -(beta B + gamma iB)
-    //   Plain bank, Reinsch form (goertzel.hip RS; plans with a tone where
-    //             |sin w| < kReinschSin): coefficient lambda = 2cos w - 2 sgn,
-    //             state (s, d); X += (A - sgn B) s + sgn B d, stored as
-    //             {C1, -C2} so the kernel's A s1 - B s2 form is unchanged.
-    //             fp32 emulation of 64-sample chains: the 2cos(w) form reaches
-    //             4-8e-5 of P at |sin w| ~ 0.01 and ~5e-6 at 0.05-0.08; the
-    //             Reinsch form stays below 1e-6 at every bin.
-    const bool residue = st->detector == kDetResidue;
-    const double span = (st->detector == kDetFolded || residue) ? 8.0 : 64.0;
-    constexpr double kReinschSin = 0.1;
-    st->reinsch = false;
-    if (st->detector == kDetGoertzel)
-        for (uint32_t k = 0; k < c.k; ++k)
-            if (std::fabs(std::sin(2.0 * M_PI * c.freqs[k] / c.fs)) < kReinschSin) st->reinsch = true;
-    // residue rho = bin mod 8 -> (class, alpha, beta, gamma); rho and 8 - rho
-    // share a class (conjugates), class 0 carries (Z0, Z4)
-    static const int kCls[8] = {0, 1, 3, 2, 0, 2, 3, 1};
-    static const double kGam[8] = {0, 1, -1, 1, 0, -1, 1, -1};
-    // Residue detector, compile-time classes (residue.hip DC): at n = 1024 and
-    // K = 8 or 16, kernel tone slot s holds tone slot_tone[s] with a fixed
-    // slot -> class pattern, so the kernel selects classes at compile time (no
-    // LDS class file) and forms only the classes it reads; the window_sum
-    // epilogue maps slots back (perm). Mode 1: K / 4 tones in every class
-    // (class (s / 2) % 4; e.g. 8 tones on an odd bin spacing hit every residue
-    // once); 2: half the tones in class 0 and half in class 3 (slots < K / 2
-    // class 0; even spacings 2 and 6); 3: every tone in class 0; 4: every tone
-    // in class 3. Other plans keep the LDS class file (mode 0).
-    std::vector<uint32_t> slot_tone(c.k);
-    for (uint32_t sl = 0; sl < c.k; ++sl) slot_tone[sl] = sl;
-    st->dcls = 0;
-    st->perm = 0;
-    if (residue && st->log2g == 4 && (c.k == 8 || c.k == 16)) {
-        std::vector<uint32_t> by_cls[4];
-        for (uint32_t k = 0; k < c.k; ++k) by_cls[kCls[integer_bin(c, k) % 8]].push_back(k);
-        size_t cnt[4];
-        for (int cl = 0; cl < 4; ++cl) cnt[cl] = by_cls[cl].size();
-        const size_t K = c.k;
-        if (cnt[0] == K / 4 && cnt[1] == K / 4 && cnt[2] == K / 4 && cnt[3] == K / 4) st->dcls = 1;
-        else if (cnt[0] == K / 2 && cnt[3] == K / 2) st->dcls = 2;
-        else if (cnt[0] == K) st->dcls = 3;
-        else if (cnt[3] == K) st->dcls = 4;
-        if (st->dcls) {
-            size_t next[4] = {0, 0, 0, 0};
-            for (uint32_t sl = 0; sl < c.k; ++sl) {
-                const int cl = st->dcls == 1 ? (int)((sl / 2) % 4)
-                             : st->dcls == 2 ? (sl < K / 2 ? 0 : 3) : st->dcls == 3 ? 0 : 3;
-                slot_tone[sl] = by_cls[cl][next[cl]++];
-                st->perm |= (unsigned long long)slot_tone[sl] << (4 * sl);
-            }
-        }
+    // the tone plan's fp32 constants (error_model.cpp build_plan)
+    st->reinsch = pl.reinsch;
+    st->f16 = pl.f16;
+    st->dcls = pl.dcls;
+    st->perm = pl.perm;
+    for (uint32_t k = 0; k < c.k; ++k) {
+        st->coef[k] = pl.coef[k];
+        st->sgn[k] = pl.sgn[k];
+        st->zcls[k] = pl.zcls[k];
+        st->rcoef[k] = pl.rcoef[k];
     }
-    // Fold detector, F16 (fold.hip): n = 1024, K = 8 on multiples of 8 bins
-    // with four tones on multiples of 16 (read Z0) and four on odd multiples
-    // of 8 (read Z8), e.g. the survey's 8-FSK plan; slots 0-3 hold the Z0
-    // tones, 4-7 the Z8 tones, and lane j of a window covers folded positions
-    // 8 (j & 7) .. +7 of the N/16-sample fold.
-    st->f16 = false;
-    if (st->detector == kDetFolded && st->log2g == 4 && c.k == 8) {
-        std::vector<uint32_t> z0, z8;
-        for (uint32_t k = 0; k < c.k; ++k) ((integer_bin(c, k) / 8) % 2 ? z8 : z0).push_back(k);
-        if (z0.size() == 4 && z8.size() == 4) {
-            for (uint32_t sl = 0; sl < 8; ++sl) {
-                slot_tone[sl] = sl < 4 ? z0[sl] : z8[sl - 4];
-                st->perm |= (unsigned long long)slot_tone[sl] << (4 * sl);
-            }
-            st->f16 = true;
-        }
+    if (!pl.rot.empty()) {
+        HIP_TRY(hipMalloc(&st->d_rot, pl.rot.size() * sizeof(float4)));
+        HIP_TRY(hipMemcpy(st->d_rot, pl.rot.data(), pl.rot.size() * sizeof(float4), hipMemcpyHostToDevice));
     }
-    std::vector<float4> rot((size_t)c.k * g * (residue ? 2 : 1));
-    for (uint32_t sl = 0; sl < c.k; ++sl) {
-        const uint32_t k = slot_tone[sl];  // rows below are kernel slots (= tones unless DCLS)
-        const double w = 2.0 * M_PI * c.freqs[k] / c.fs;
-        const double sg = std::cos(w) >= 0.0 ? 1.0 : -1.0;
-        st->sgn[sl] = (float)sg;
-        st->coef[sl] = (float)(2.0 * std::cos(w));
-        if (st->reinsch) {
-            const double h = std::sin(0.5 * w), q = std::cos(0.5 * w);
-            st->coef[sl] = (float)(sg > 0 ? -4.0 * h * h : 4.0 * q * q);
-        }
-        const int rho = residue ? (int)(integer_bin(c, k) % 8) : 0;
-        const double al = rho == 4 ? 0.0 : 1.0, be = rho == 4 ? 1.0 : 0.0, ga = kGam[rho];
-        st->zcls[sl] = kCls[rho];
-        for (int j = 0; j < g; ++j) {
-            const double pos = st->f16 ? (double)(j & 7) : (double)j;  // F16: lanes j, j + 8 share positions
-            const double a = -w * (span * pos + span - 1.0), b = -w * (span * pos + span);
-            const double Ar = std::cos(a), Ai = std::sin(a), Br = std::cos(b), Bi = std::sin(b);
-            if (!residue && st->reinsch) {
-                const double C1r = Ar - sg * Br, C1i = Ai - sg * Bi;
-                rot[(size_t)sl * g + j] = make_float4((float)C1r, (float)C1i, (float)(-sg * Br),
-                                                      (float)(-sg * Bi));
-                continue;
-            }
-            if (!residue) {
-                rot[(size_t)sl * g + j] = make_float4((float)Ar, (float)Ai, (float)Br, (float)Bi);
-                continue;
-            }
-            // iA = (-Ai, Ar)
-            rot[((size_t)sl * g + j) * 2] =
-                make_float4((float)(al * Ar), (float)(al * Ai), (float)(be * Ar - ga * Ai),
-                            (float)(be * Ai + ga * Ar));
-            rot[((size_t)sl * g + j) * 2 + 1] =
-                make_float4((float)(-al * Br), (float)(-al * Bi), (float)(-(be * Br - ga * Bi)),
-                            (float)(-(be * Bi + ga * Br)));
-        }
-    }
-    HIP_TRY(hipMalloc(&st->d_rot, rot.size() * sizeof(float4)));
-    HIP_TRY(hipMemcpy(st->d_rot, rot.data(), rot.size() * sizeof(float4), hipMemcpyHostToDevice));
-    // Decision rescue: the double coefficients of the
-    // definition's recurrence (the same libm cos of the same rounded argument
-    // as the double oracle), and the detectors' ambiguity threshold
-    // tau sqrt(Q) sqrt(P_max), Q = n^2 2^30 (>= n sum x^2 for int16 input),
-    // plus the floor tau^2 Q / 16 below which the fp32 error's second-order
-    // term could reach the margin.
-    for (uint32_t k = 0; k < c.k; ++k) st->rcoef[k] = 2.0 * std::cos(2.0 * M_PI * c.freqs[k] / c.fs);
-    // the in-kernel rescue's first step (n = 1024): per tone and lane segment
-    // j the rotation of the segment's end state into the window's phase,
-    // X = A s1 - B s2, A = e^{-i w (64 j + 63)}, B = e^{-i w (64 j + 64)}, in
-    // double and in the caller's tone order; FSKD_RESCUE_SEG=0 (measurement
-    // switch) sends every flagged row to the exact chain
-    // (the FFT detector: at its tone bins' frequencies b n / fs, with 2 cos
-    // (2 pi b / n), for its own first pass, rescue_fft_seg)
+    // the in-kernel rescue's first pass (n = 1024): its tables (build_plan);
+    // FSKD_RESCUE_SEG=0 (measurement switch) sends every flagged row to the
+    // exact chain
     const char *seg_env = std::getenv("FSKD_RESCUE_SEG");
-    if (c.n == 1024 && c.k >= 2) {
-        const bool fft = st->detector == kDetFft;
-        std::vector<double> r64((size_t)c.k * 16 * 4 + c.k);
-        demod_cfg_t cb = c;  // the frequencies the first pass evaluates
-        for (uint32_t k = 0; k < c.k; ++k) {
-            if (fft) cb.freqs[k] = (double)st->fft_bins[k] * c.fs / (double)c.n;
-            r64[(size_t)c.k * 64 + k] =
-                fft ? 2.0 * std::cos(2.0 * M_PI * st->fft_bins[k] / (double)c.n) : st->rcoef[k];
-        }
-        for (uint32_t k = 0; k < c.k; ++k) {
-            const double w = fft ? 2.0 * M_PI * st->fft_bins[k] / (double)c.n
-                                 : 2.0 * M_PI * c.freqs[k] / c.fs;
-            for (int j = 0; j < 16; ++j) {
-                const double a = -w * (64.0 * j + 63.0), b = -w * (64.0 * j + 64.0);
-                double *o = &r64[((size_t)k * 16 + j) * 4];
-                o[0] = std::cos(a);
-                o[1] = std::sin(a);
-                o[2] = std::cos(b);
-                o[3] = std::sin(b);
-            }
-        }
-        HIP_TRY(hipMalloc(&st->d_rot64, r64.size() * sizeof(double)));
-        HIP_TRY(hipMemcpy(st->d_rot64, r64.data(), r64.size() * sizeof(double), hipMemcpyHostToDevice));
-        if (!(seg_env && std::strcmp(seg_env, "0") == 0)) st->tau64 = 12.0 * rescue_r64(cb);
+    const bool first_pass = !pl.rot64.empty() && !(seg_env && std::strcmp(seg_env, "0") == 0);
+    if (!pl.rot64.empty()) {
+        HIP_TRY(hipMalloc(&st->d_rot64, pl.rot64.size() * sizeof(double)));
+        HIP_TRY(hipMemcpy(st->d_rot64, pl.rot64.data(), pl.rot64.size() * sizeof(double), hipMemcpyHostToDevice));
     }
     // measurement switches: FSKD_NO_RESCUE=1 turns the rescue off, =flags
     // keeps the detectors' flags but skips the launch (the flagged windows'
@@ -508,19 +248,20 @@ static int init_device_state(demod_t *st)
     st->wb_bursts = !(wb_env && std::strcmp(wb_env, "0") == 0);
     if (wb_env && std::atoi(wb_env) > 0) st->wb_force = std::min(std::atoi(wb_env), 64);
     if (st->rescue) {
-        // stage 1 with Q (1 + 2e-4), so that it flags every window stage 2
-        // flags whatever the fp32 rounding of the energy sum (which the (1 +
-        // 1e-4) of amb_t2e covers); stage 2: amb_t2e E P_max, E the
-        // detector's energy sum (fold: of the N/8-sample folded window; FFT:
-        // Parseval's sum, already n sum x^2)
-        const double q = (double)c.n * (double)c.n * 1073741824.0 * (1.0 + 2e-4);
-        st->tau = amb_tau(st->detector, st->log2g, c, st->reinsch);
-        const double t2 = st->tau * st->tau;
-        st->amb_tq = (float)(st->tau * std::sqrt(q));
-        st->amb_floor = (float)(t2 * q / 16.0);
-        const double ne_per_e = st->detector == kDetFft ? 1.0
-                              : st->detector == kDetFolded ? (double)c.n / 8.0 : (double)c.n;
-        st->amb_t2e = (float)(t2 * ne_per_e * (1.0 + 1e-4));
+        // Decision rescue thresholds, derived from the plan's
+        // constants and the kernels' operation sequences (error_model.cpp):
+        // stage 2 flags (P_1 - P_2)^2 < t2e E_eff P_1, stage 1 the same with
+        // the int16 maximum of E_eff (tq, fl); pass 0 decides a flagged row
+        // where its own margin clears t2e64 E P_max.
+        ErrModel m;
+        error_model(c, pl, first_pass, m);
+        st->tau = m.tau;
+        st->amb_tq = (float)m.tq;
+        st->amb_floor = (float)m.fl;
+        st->amb_t2e = (float)m.t2e;
+        st->amb_d = (float)m.amb_d;
+        st->tau64 = m.tau64;
+        st->t2e64 = m.t2e64;
     }
     st->slide_wt = 0;
     if (slide && st->detector == kDetGoertzel)
@@ -769,7 +510,7 @@ static int enqueue_fft(demod_t *st, const int16_t *d_pcm, size_t n_windows, uint
     // the rescue's first pass (tones only; with the spectrum stored every
     // flagged window takes the double FFT, whose spectrum row is the oracle's)
     p.rot64 = st->d_rot64;
-    p.t2e64 = st->tau64 * st->tau64 * (double)st->cfg.n * (1.0 + 1e-3);
+    p.t2e64 = st->t2e64;
     HIP_TRY(launch_fft_quad(p, s));
     return (int)n_windows;
 }
@@ -816,10 +557,11 @@ static int enqueue_batch(demod_t *st, const int16_t *d_pcm, size_t n_windows, ui
     p.rescue_inline = st->rescue && st->rescue_launch && rescue_in_kernel(st) ? 1 : 0;
     for (uint32_t k = 0; k < st->cfg.k; ++k) p.rcoef[k] = st->rcoef[k];
     // the in-kernel rescue's tables; its first pass's threshold^2 = t2e64 E
-    // P_max, E = sum x^2 (fp32 in the kernel: the (1 + 1e-3) covers its
-    // rounding), 0: the exact chain only
+    // P_max, E = sum x^2 (fp32 in the kernel; error_model's safety factor
+    // covers its rounding), 0: the exact chain only
     p.rot64 = st->d_rot64;
-    p.t2e64 = st->tau64 * st->tau64 * (double)st->cfg.n * (1.0 + 1e-3);
+    p.t2e64 = st->t2e64;
+    p.amb_d = st->amb_d;
     for (size_t w0 = 0; w0 < n_windows; w0 += per) {
         const size_t cnt = std::min(per, n_windows - w0);
         p.pcm = d_pcm + w0 * st->cfg.hop;

@@ -69,6 +69,10 @@ struct GoertzelParams {
     float amb_tq;
     float amb_floor;         // stage 1: 0 < P_max < amb_floor is ambiguous
     float amb_t2e;
+    // fold detector: stage 2's energy is E_eff = (sqrt(sum xf^2) + amb_d)^2,
+    // amb_d the double oracle's own error (which scales with the RAW window)
+    // in units of the folded window's norm (error_model.cpp)
+    float amb_d;
 };
 
 // Decision rescue. A detector's fp32 powers carry an error

@@ -49,14 +49,19 @@ __device__ __forceinline__ float group_sum_f(float v, int log2g)
 // == 0) returns the raw window's sum x^2, which the P_max == 0 test of
 // demod_internal.h amb_energy then reads (> 0: ambiguous). A window with
 // E_f > 0 has raw energy too, so only its threshold scale matters.
+// Round 5: the threshold carries the double oracle's own error too, which
+// scales with the raw window (error_model.cpp): E_eff = (sqrt(E_f) + d)^2,
+// d = p.amb_d in units of sqrt(E_f); a row with E_f == 0 gets d^2 (> 0: a
+// candidate) unless its raw window is digital silence.
 template <typename RawFn>
-__device__ __forceinline__ float fold_energy(float ef, bool live, RawFn rawfn)
+__device__ __forceinline__ float fold_energy(float ef, bool live, float d, RawFn rawfn)
 {
     if (__ballot(live && ef == 0.f) != 0) {
         const float er = rawfn();
-        if (ef == 0.f) ef = er;
+        if (ef == 0.f) return er > 0.f ? fmaxf(d * d, 1e-30f) : 0.f;
     }
-    return ef;
+    const float s = __builtin_amdgcn_sqrtf(ef) + d;
+    return s * s;
 }
 
 // The decision of one window at n = 1024 from this lane's folded integer sums
@@ -86,7 +91,7 @@ __device__ __forceinline__ bool fold_decide(const int (&acc)[8], const float4 *r
 #pragma unroll
         for (int q = 0; q < 8; q += 2)
             a = __builtin_elementwise_fma(f32x2f{xf[q], xf[q + 1]}, f32x2f{xf[q], xf[q + 1]}, a);
-        return fold_energy(row_sum16(a.x + a.y), live, rawfn);
+        return fold_energy(row_sum16(a.x + a.y), live, p.amb_d, rawfn);
     };
     const AmbTest at{p.amb_tq, p.amb_floor, p.amb_t2e, defer};
     if constexpr (F16) {
@@ -333,7 +338,7 @@ __global__ __launch_bounds__(64 * WPB) void fold_tile_kernel(GoertzelParams p)
                 float e = 0.f;
 #pragma unroll
                 for (int q = 0; q < 8; ++q) e = fmaf(xf[q], xf[q], e);
-                return fold_energy(row_sum16(e), w < p.n_windows, rawfn);
+                return fold_energy(row_sum16(e), w < p.n_windows, p.amb_d, rawfn);
             };
             window_sum_decide<K, false, MST>(xr, xi, lane, w, w < p.n_windows, p.sym, p.mag, 0,
                                              AmbTest{p.amb_tq, p.amb_floor, p.amb_t2e, false}, efn);
@@ -362,7 +367,7 @@ __global__ __launch_bounds__(64 * WPB) void fold_tile_kernel(GoertzelParams p)
             float e = 0.f;
 #pragma unroll
             for (int q = 0; q < 8; ++q) e = fmaf(xf[q], xf[q], e);
-            return fold_energy(group_sum_f(e, log2g), w < p.n_windows, rawfn);
+            return fold_energy(group_sum_f(e, log2g), w < p.n_windows, p.amb_d, rawfn);
         };
         bool amb;
         const int arg = chain_decide<K>(P, w < p.n_windows, p.amb_tq, p.amb_floor, p.amb_t2e, efn, amb);

@@ -165,19 +165,77 @@ int demod_batch_launches(const demod_t *st, size_t n_windows, int with_mags);
  * rescue is off, K = 1 or FSKD_NO_RESCUE=1): a window is re-decided in double
  * when its fp32 top-2 margin is below tau sqrt(NE P_max), NE the energy scale
  * of the window the detector transforms (n sum x^2; fold detector: (n/8)
- * sum xf^2 of the N/8-folded window). tau = 12 r, r the detector's fp32 power
- * error bound |dP| <= r sqrt(NE P_max), scaled for the tone plan (DESIGN.md
- * §2a). For tests and diagnostics. */
+ * sum xf^2 of the N/8-folded window, plus the oracle's share, see
+ * demod_error_model_t.amb_d). tau = 4 (rho_det + rho_ref) / sqrt(n_eff) with
+ * the bounds derived for the handle's tone plan and kernel (demod_error_model,
+ * DESIGN.md §2a); no measured constant. For tests and diagnostics. */
 double demod_rescue_tau(const demod_t *st);
 
 /* The in-kernel rescue's first pass (n = 1024 Goertzel-family detectors, and
- * the FFT detector's tones-only batches at its tone bins): a flagged
- * window's powers in double by 64-sample segments decide it when their
- * top-2 margin clears tau64 sqrt(NE P_max); windows inside that band take
- * the exact double chain (or double FFT). Returns tau64 (0: every flagged
- * window takes the exact path — rescue launches, FSKD_RESCUE_SEG=0, plans
- * with a tone at 0 or fs/2). For tests and diagnostics. */
+ * the FFT detector's TONES-ONLY batches at its tone bins; a spectrum batch's
+ * flagged windows always take the double FFT): a flagged window's powers in
+ * double by 64-sample segments decide it when their top-2 margin clears
+ * tau64 sqrt(n sum x^2 P_max); windows inside that band take the exact double
+ * chain (or double FFT). Returns tau64 = 4 rho_first / sqrt(n) (0: every
+ * flagged window takes the exact path — rescue launches, FSKD_RESCUE_SEG=0).
+ * For tests and diagnostics. */
 double demod_rescue_tau64(const demod_t *st);
+
+/* The error bounds behind the decision rescue, derived for a
+ * configuration's tone plan from the kernel's operation sequence and fp32
+ * constants by a forward rounding-error analysis; no device needed. For every
+ * window x and tone k, with X_k the exact DFT of x at the tone (the fold /
+ * residue / FFT detectors: at its bin):
+ *   |sqrt(P_gpu,k) - |X_k||      <= rho_det sqrt(E_det)
+ *   |sigma(P_oracle,k) - |X_k||  <= rho_ref sqrt(sum x^2)   sigma(P) = sign(P) sqrt|P|
+ *   |sqrt(P_first,k) - sigma(P_oracle,k)| <= rho_first sqrt(sum x^2)  (pass 0)
+ * E_det = sum x^2 of the window (plain bank, residue, FFT) or sum xf^2 of the
+ * window folded to n/8 samples (energy = DEMOD_ENERGY_FOLDED). The kernels
+ * flag a window when (P_1 - P_2)^2 < t2e E_eff P_1 (E_eff: the kernel's energy
+ * E, Parseval's 2 sum_b P_b for the FFT, (sqrt E + amb_d)^2 for the fold
+ * detector), which leaves unflagged only windows whose sqrt-power margin
+ * exceeds twice the two bounds: their symbol is the oracle's. */
+#define DEMOD_ENERGY_RAW      0
+#define DEMOD_ENERGY_FOLDED   1
+#define DEMOD_ENERGY_PARSEVAL 2
+typedef struct demod_error_model {
+    int32_t method;      /* the detector the configuration runs (DEMOD_METHOD_*) */
+    int32_t energy;      /* DEMOD_ENERGY_*: the energy the kernel's flag test sums */
+    double  rho_det;
+    double  rho_ref;
+    double  rho_first;   /* 0 when the configuration has no pass 0 (n != 1024, K = 1) */
+    double  tau;         /* as demod_rescue_tau (0 for K = 1) */
+    double  tau64;       /* as demod_rescue_tau64, before the handle's switches */
+    double  t2e;         /* the stage-2 threshold factor the kernels read */
+    double  t2e64;       /* pass 0's, with E its sum x^2 */
+    double  amb_d;       /* fold detector: the oracle's share in units of sqrt(sum xf^2) */
+} demod_error_model_t;
+int demod_error_model(const demod_cfg_t *cfg, demod_error_model_t *model);
+
+/* The tone plan a configuration runs and the fp32 constants its kernels read
+ * (the arrays demod_create uploads), for operation-for-operation emulation in
+ * tests; no device needed. rot receives rot_len float4 entries ([slot][g],
+ * residue [slot][g][2]) when rot_cap (floats) allows, rot64 the first pass's
+ * double tables ([k][16][4] then c[k]) when rot64_cap allows. */
+typedef struct demod_plan_info {
+    int32_t  method;        /* DEMOD_METHOD_* the configuration runs */
+    int32_t  log2g;         /* lanes per window = 2^log2g = n / 64 */
+    int32_t  reinsch;       /* plain bank: Reinsch-modified recurrence */
+    int32_t  f16;           /* fold detector: fold by 16 (K = 8) */
+    int32_t  dcls;          /* residue detector: compile-time class pattern */
+    int32_t  slide;         /* segment-shared kernels (n = 1024, hop = 64 H < n) */
+    uint64_t perm;          /* nibble s = the tone of kernel slot s (DCLS / F16) */
+    int32_t  slot_tone[DEMOD_MAX_TONES];
+    int32_t  zcls[DEMOD_MAX_TONES];
+    int32_t  fft_bins[DEMOD_MAX_TONES];
+    float    coef[DEMOD_MAX_TONES];
+    float    sgn[DEMOD_MAX_TONES];
+    double   rcoef[DEMOD_MAX_TONES];
+    uint32_t rot_len;       /* float4 entries of rot */
+    uint32_t rot64_len;     /* doubles of rot64 */
+} demod_plan_info_t;
+int demod_plan_info(const demod_cfg_t *cfg, demod_plan_info_t *info, float *rot, size_t rot_cap,
+                    double *rot64, size_t rot64_cap);
 
 /*
  * Streaming entry point: demodulate(pcm, n) -> symbols.
