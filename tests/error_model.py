@@ -1,26 +1,28 @@
-"""The fp32 error model behind the decision rescue, measured window by window.
+"""The decision rescue's derived error bounds, checked window by window on
+the GPU.
 
-DESIGN.md §2a: a detector's fp32 tone power carries an error
-    |P_gpu - P_ref| <= r sqrt(P_max NE) + r^2 NE              (*)
-with NE the energy scale of the window the detector transforms (n sum x^2;
-the fold detector: (n/8) sum xf^2 of the N/8-folded window) and r the
-detector's bound for the tone plan; the kernels flag a window when its fp32
-top-2 margin is below tau sqrt(NE P_max), tau = 12 r (a margin carries two
-powers' errors, x 6 safety), or P_max < tau^2 NE / 16, and the rescue
-re-decides flagged windows in double. r = tau / 12 comes from the handle
-(demod_rescue_tau), so what is checked is the constant the shipped kernels
-use, for the plan they run.
+DESIGN.md §2a (round 5): for each tone plan, audio-network_amd/csrc/
+error_model.cpp derives from the kernels' operation sequences and fp32
+constants (no measured constant; demod_error_model)
+    |sqrt(P_gpu,k) - |X_k||      <= rho_det sqrt(E_det)
+    |sigma(P_oracle,k) - |X_k||  <= rho_ref sqrt(sum x^2)
+so on every window and tone
+    |sqrt(P_gpu,k) - sigma(P_oracle,k)| <= rho_det sqrt(E_det) + rho_ref sqrt(sum x^2)   (*)
+with E_det the energy the kernel sums (raw sum x^2; fold detector: sum xf^2
+of the n/8 fold; FFT: raw, the kernel's own Parseval sum covering it). The
+kernels flag a window when (P_1 - P_2)^2 < t2e E_eff P_1 (E_eff: raw sum x^2,
+(sqrt(sum xf^2) + amb_d)^2 for the fold detector, Parseval's 2 sum_b P_b for
+the FFT), or P_1 == 0 with E_eff > 0; the rescue re-decides flagged windows
+in double.
 
 evaluate() runs one detector configuration on one signal family with the
 rescue's flags kept but the rescue itself off (FSKD_NO_RESCUE=flags: every
 magnitude is the kernel's fp32 value) and checks, on every window:
-  1. the model (*) with the handle's r (reports the worst ratio, and the
-     worst error as a fraction of tau);
+  1. (*) (reports the worst ratio, and the worst sqrt-power error as a fraction
+     of the flag threshold's sqrt margin);
   2. the kernel flags exactly the windows the stated threshold selects
      (within 1e-3 of it, the fp32 rounding of the test itself; the FFT's
-     stage-2 energy is Parseval's 2 sum_{b<=512} P_b, between NE and 2 NE),
-     and every window whose fp32 tone powers are all exactly 0 unless it is
-     digital silence;
+     stage-2 energy lies between n sum x^2 and 2 n sum x^2);
   3. every window it leaves unflagged carries the oracle's symbol.
 Test infrastructure: only tests/ and bench.py's checker legs import this.
 """
@@ -99,14 +101,16 @@ def family(name, freqs, n, blocks, seed):
     return np.clip(np.round(v), -32768, 32767).astype(np.int16).reshape(-1)
 
 
-def window_energy(x, n, hop, W, fold):
-    """NE per window: n sum x^2, or (n/8) sum xf^2 of the N/8-folded window."""
+def window_energies(x, n, hop, W):
+    """(raw sum x^2, folded sum xf^2) per window, exact."""
     idx = np.arange(W)[:, None] * hop + np.arange(n)[None, :]
-    xw = x[idx].astype(np.float64)
-    if fold:
-        xf = xw.reshape(W, 8, n // 8).sum(axis=1)
-        return (n / 8) * (xf * xf).sum(axis=1)
-    return n * (xw * xw).sum(axis=1)
+    xw = x[idx].astype(np.int64)
+    xf = xw.reshape(W, 8, n // 8).sum(axis=1)
+    return (xw * xw).sum(axis=1).astype(np.float64), (xf * xf).sum(axis=1).astype(np.float64)
+
+
+def sigma(P):
+    return np.sign(P) * np.sqrt(np.abs(P))
 
 
 def evaluate(A, O, case, fam, W=4096, threads=16, seed=1):
@@ -116,7 +120,8 @@ def evaluate(A, O, case, fam, W=4096, threads=16, seed=1):
     old = os.environ.get("FSKD_NO_RESCUE")
     os.environ["FSKD_NO_RESCUE"] = "flags"
     try:
-        d = A.Demodulator(A.make_cfg(n=n, hop=hop, freqs=freqs, method=method))
+        cfg = A.make_cfg(n=n, hop=hop, freqs=freqs, method=method)
+        d = A.Demodulator(cfg)
     finally:
         if old is None:
             del os.environ["FSKD_NO_RESCUE"]
@@ -126,41 +131,46 @@ def evaluate(A, O, case, fam, W=4096, threads=16, seed=1):
         got = int(d.method)
         tau = d.rescue_tau
         sym, mag = d.batch(x, n_windows=W, mags=True)
+    m = A.error_model(cfg)
     fft = got == 2
+    fold = got == 3
     rs, rP = (O.fft_demod if fft else O.goertzel)(x, freqs, n, hop=hop, fs=FS, threads=threads)
     rs, rP = rs[:W], rP[:W]
-    fold = got == 3
-    NE = window_energy(x, n, hop, W, fold)
-    r = tau / 12.0
+    e_raw, e_fold = window_energies(x, n, hop, W)
+    e_det = e_fold if fold else e_raw
     g = mag.astype(np.float64)
-    dP = np.abs(g - rP).max(axis=1)
-    Pm = rP.max(axis=1)
-    bound = r * np.sqrt(Pm * NE) + r * r * NE
+    bound = m["rho_det"] * np.sqrt(e_det) + m["rho_ref"] * np.sqrt(e_raw)
+    err = np.abs(np.sqrt(g) - sigma(rP)).max(axis=1)
     ok = bound > 0
     ratio = np.zeros(W)
-    ratio[ok] = dP[ok] / bound[ok]
-    # the error as a fraction of tau's model (tau = 12 r): what fraction of
-    # the margin threshold tau sqrt(P_max NE) (+ its second-order term) one
-    # power's error uses
-    frac_tau = ratio / 12.0
-    zero_ne = ~ok
-    # 2. the flags against the stated threshold, from the kernel's own powers
+    ratio[ok] = err[ok] / bound[ok]
+    zero_e = ~ok
+    assert (err[zero_e] == 0).all() if zero_e.any() else True
+    # the flag test's sqrt margin is sqrt(t2e E_eff) / 2 = 2 bound (x safety):
+    # one power's error as a fraction of it
+    frac_tau = ratio / 2.0
     flag = (sym & 0x80) != 0
     gs = np.sort(g, axis=1)
     p1 = gs[:, -1]
     p2 = gs[:, -2] if g.shape[1] > 1 else np.zeros(W)
-    m = p1 - p2
-    lo_ne, hi_ne = (NE, 2 * NE) if fft else (NE, NE)
+    mm = p1 - p2
+    if fft:
+        lo_e, hi_e = n * e_raw, 2 * n * e_raw
+    elif fold:
+        d_ = m["amb_d"]
+        eff = np.where(e_fold > 0, (np.sqrt(e_fold) + d_) ** 2, np.where(e_raw > 0, d_ * d_, 0.0))
+        lo_e = hi_e = eff
+    else:
+        lo_e = hi_e = e_raw
 
-    def sel(ne, s):
-        c = tau * tau * ne * s
-        return (p1 > 0) & ((m * m < c * p1) | (16 * p1 < c))
-    must = sel(lo_ne, 0.999)     # below the threshold: flagged
-    may = sel(hi_ne, 1.001)      # above it: not flagged
+    def sel(e, s):
+        c = m["t2e"] * e * s
+        return (p1 > 0) & ((mm * mm < c * p1) | (16 * p1 < c))
+    must = sel(lo_e, 0.999)     # below the threshold: flagged
+    may = sel(hi_e, 1.001)      # above it: not flagged
     # every fp32 tone power exactly 0: flagged unless the window is digital
     # silence (the oracle's powers are then its own rounding noise)
-    raw = window_energy(x, n, hop, W, False)
-    zero = (p1 == 0) & (raw > 0)
+    zero = (p1 == 0) & (e_raw > 0)
     must |= zero
     may |= zero
     if g.shape[1] < 2:
@@ -169,12 +179,13 @@ def evaluate(A, O, case, fam, W=4096, threads=16, seed=1):
     extra = np.flatnonzero(flag & ~may)
     # 3. unflagged decisions equal the oracle's (digital silence: all powers 0
     # in fp32 and in double -> tone 0)
-    silent = (g == 0).all(axis=1) & (raw == 0)
+    silent = (g == 0).all(axis=1) & (e_raw == 0)
     wrong = np.flatnonzero(~flag & ~silent & ((sym & 0x7F) != rs))
     return {"case": name, "family": fam, "method": got, "windows": W, "tau": tau,
-            "r": r, "worst_ratio_to_model": float(ratio.max()),
+            "rho_det": m["rho_det"], "rho_ref": m["rho_ref"],
+            "worst_ratio_to_model": float(ratio.max()),
             "worst_err_frac_of_tau": float(frac_tau.max()),
-            "windows_zero_energy": int(zero_ne.sum()),
+            "windows_zero_energy": int(zero_e.sum()),
             "flagged": int(flag.sum()), "flag_missed": int(missed.size), "flag_extra": int(extra.size),
             "unflagged_wrong": int(wrong.size),
             "_detail": (missed[:4].tolist(), extra[:4].tolist(), wrong[:4].tolist())}

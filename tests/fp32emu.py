@@ -31,6 +31,7 @@ import numpy as np
 
 F32 = np.float32
 F64 = np.float64
+PI_L = np.longdouble("3.14159265358979323846264338327950288")  # pi to long double precision
 
 
 def fma32(a, b, c):
@@ -279,8 +280,177 @@ def exact_dft_mag(x, n, hop, W, omegas):
     t = np.arange(n, dtype=np.longdouble)
     out = np.zeros((W, len(omegas)), F64)
     for k, w in enumerate(omegas):
-        ph = np.longdouble(w) * t
+        ph = np.asarray(w, np.longdouble) * t
         re = xw @ np.cos(ph)
         im = xw @ np.sin(ph)
         out[:, k] = np.sqrt(re * re + im * im).astype(F64)
     return out
+
+
+# ---------------------------------------------------------------------------
+# fft_quad.hip (the shipped FUSED 4 kernel), operation for operation: complex
+# values as (re, im) pairs of float32 arrays.
+
+def _c(re, im):
+    return (np.asarray(re, F32), np.asarray(im, F32))
+
+
+def _add(a, b):
+    return ((a[0] + b[0]).astype(F32), (a[1] + b[1]).astype(F32))
+
+
+def _sub(a, b):
+    return ((a[0] - b[0]).astype(F32), (a[1] - b[1]).astype(F32))
+
+
+def _add_mj(x, y):   # x + (-j) y
+    return ((x[0] + y[1]).astype(F32), (x[1] - y[0]).astype(F32))
+
+
+def _sub_mj(x, y):   # x - (-j) y
+    return ((x[0] - y[1]).astype(F32), (x[1] + y[0]).astype(F32))
+
+
+def _bfly(x, y, w):
+    """QTB_T / QTB_U / QTB_V: t = fma(y, w.x, x); u = x + w y by
+    fma(y.yx, (-w.y, w.y), t); v = fma(x, 2, -u)."""
+    wr, wi = w
+    t = (fma32(y[0], wr, x[0]), fma32(y[1], wr, x[1]))
+    u = (fma32(y[1], -wi, t[0]), fma32(y[0], wi, t[1]))
+    v = (fma32(x[0], F32(2), -u[0]), fma32(x[1], F32(2), -u[1]))
+    return u, v
+
+
+def _mjw(w):          # -j w, as the QTB_TM / QTB_UM operand modifiers read it
+    return (w[1], -w[0])
+
+
+_W32 = [(F32(np.cos(2 * np.pi * j / 32)), F32(-np.sin(2 * np.pi * j / 32))) for j in range(32)]
+
+
+def _w32(e):
+    return _W32[e % 32]
+
+
+def _dft4_triv(x):
+    a0, a1 = _add(x[0], x[2]), _sub(x[0], x[2])
+    c0, c1 = _add(x[1], x[3]), _sub(x[1], x[3])
+    return [_add(a0, c0), _add_mj(a1, c1), _sub(a0, c0), _sub_mj(a1, c1)]
+
+
+def _dft4_geo(x, w, w2):
+    """Geometric DFT-4 of (x0, w x1, w^2 x2, w^3 x3) in two fused stages
+    (dft4_fused_k / dft4_fused_v / dft4x2_fused_v): a = x0 +- w^2 x2,
+    c = x1 +- w^2 x3, X0 / X2 = a0 +- w c0, X1 / X3 = a1 +- (-j w) c1."""
+    a0, a1 = _bfly(x[0], x[2], w2)
+    c0, c1 = _bfly(x[1], x[3], w2)
+    X0, X2 = _bfly(a0, c0, w)
+    X1, X3 = _bfly(a1, c1, _mjw(w))
+    return [X0, X1, X2, X3]
+
+
+def _dft8(x):
+    """dftf<8, ., 4>: two DFT-4 (even / odd i1), then dft8_last."""
+    e = _dft4_triv([x[0], x[2], x[4], x[6]])
+    o = _dft4_triv([x[1], x[3], x[5], x[7]])
+    u0, v0 = _add(e[0], o[0]), _sub(e[0], o[0])
+    u1, v1 = _bfly(e[1], o[1], _w32(4))
+    u2, v2 = _add_mj(e[2], o[2]), _sub_mj(e[2], o[2])
+    u3, v3 = _bfly(e[3], o[3], _w32(12))
+    return [u0, u1, u2, u3, v0, v1, v2, v3]
+
+
+def _dft32(a):
+    """dftf<32, 1, 4> over a[0..31]: a DFT-8 over i1 per column i2 < 4, then per
+    k1 the geometric DFT-4 over i2 with ratio W32^k1; natural order out."""
+    cols = [_dft8([a[i2 + 4 * i1] for i1 in range(8)]) for i2 in range(4)]
+    out = [None] * 32
+    for k1 in range(8):
+        y = [cols[i2][k1] for i2 in range(4)]
+        if k1 == 0:
+            X = _dft4_triv(y)
+        elif k1 == 4:   # w^2 = -j: dft4_fused_kq
+            a0, a1 = _add_mj(y[0], y[2]), _sub_mj(y[0], y[2])
+            c0, c1 = _add_mj(y[1], y[3]), _sub_mj(y[1], y[3])
+            X0, X2 = _bfly(a0, c0, _w32(4))
+            X1, X3 = _bfly(a1, c1, _w32(12))
+            X = [X0, X1, X2, X3]
+        else:           # dft4_fused_k: w^2 = W32^{2 k1}, w = W32^k1, -j w = W32^{k1 + 8}
+            a0, a1 = _bfly(y[0], y[2], _w32(2 * k1))
+            c0, c1 = _bfly(y[1], y[3], _w32(2 * k1))
+            X0, X2 = _bfly(a0, c0, _w32(k1))
+            X1, X3 = _bfly(a1, c1, _w32(k1 + 8))
+            X = [X0, X1, X2, X3]
+        for k2 in range(4):
+            out[k1 + 8 * k2] = X[k2]
+    return out
+
+
+def _tw512(e):
+    e = np.asarray(e) & 511
+    ang = -2.0 * np.pi * e / 512.0
+    return (np.cos(ang).astype(F32), np.sin(ang).astype(F32))
+
+
+def fft_spectrum(x, hop, W):
+    """|X_b|^2, b = 0..512, of W 1024-sample windows as fft1024_quad_kernel
+    computes them (float32 [W, 513])."""
+    xw = _windows(np.asarray(x), 1024, hop, W).astype(F32)
+    z = (xw[:, 0::2], xw[:, 1::2])                      # z[n] = x[2n] + i x[2n+1]
+    # lane t: a[n1] = z[t + 16 n1]; arrays [W, 16] per n1
+    a = [(z[0][:, n1 * 16:(n1 + 1) * 16], z[1][:, n1 * 16:(n1 + 1) * 16]) for n1 in range(32)]
+    A = _dft32(a)                                        # A[k1][:, t] = DFT-32 of lane t at k1
+    t = np.arange(16)
+    cols = [t, np.where(t == 0, 16, 32 - t)]             # lane t': columns t' and k1b
+    Z = []
+    for col in cols:
+        # b[n2] = A_{n2}[col] for lane t': the transpose
+        Ak_re = np.stack([A[k][0] for k in range(32)], axis=1)   # [W, 32 (k1), 16 (t)]
+        Ak_im = np.stack([A[k][1] for k in range(32)], axis=1)
+        b = [(Ak_re[:, col, n2], Ak_im[:, col, n2]) for n2 in range(16)]  # [W, 16 lanes t']
+        v, v2 = _tw512(4 * col), _tw512(8 * col)
+        y = [None] * 16
+        for i2 in range(4):       # inner geometric DFT-4 over i1 (rows i2 + 4 i1), ratio v
+            X = _dft4_geo([b[i2 + 4 * i1] for i1 in range(4)], v, v2)
+            for k1 in range(4):
+                y[i2 + 4 * k1] = X[k1]
+        out = [None] * 16
+        for k1 in range(4):       # outer over i2, ratio g = W512^{col + 32 k1}
+            g, g2 = _tw512(col + 32 * k1), _tw512(2 * (col + 32 * k1))
+            X = _dft4_geo([y[4 * k1 + i2] for i2 in range(4)], g, g2)
+            for k2 in range(4):
+                out[k1 + 4 * k2] = X[k2]
+        Z.append(out)             # Z[sl][k2] = Z[col + 32 k2]
+    # real post-pass: pair j of lane t: P = Z[kP], Q = Z[512 - kP]
+    P_out = np.zeros((W, 513), F32)
+    ang = -2.0 * np.pi * np.arange(512) / 1024.0
+    t1024 = (np.cos(ang).astype(F32), np.sin(ang).astype(F32))
+    l0 = t == 0
+    for j in range(16):
+        Pr, Pi = Z[0][j]
+        Qr, Qi = Z[1][15 - j]
+        if j < 8:   # lane 0: column 16's Z[16 + 32 j]
+            Pr = np.where(l0, Z[1][j][0], Pr)
+            Pi = np.where(l0, Z[1][j][1], Pi)
+        else:       # lane 0: Z[32 (16 - j)]
+            Qr = np.where(l0, Z[0][16 - j][0], Qr)
+            Qi = np.where(l0, Z[0][16 - j][1], Qi)
+        kP = np.where(l0 & (j < 8), 16 + 32 * j, t + 32 * j)
+        Wr = (F32(0.5) * t1024[0][kP]).astype(F32)
+        Wi = (F32(0.5) * t1024[1][kP]).astype(F32)
+        S = ((Pr + Qr).astype(F32), (Pi - Qi).astype(F32))
+        D = ((Pi + Qi).astype(F32), (Qr - Pr).astype(F32))
+        tt = ((D[1] * Wi).astype(F32), (D[1] * Wr).astype(F32))
+        T = (fma32(D[0], Wr, -tt[0]), fma32(D[0], Wi, tt[1]))
+        R0 = (fma32(S[0], F32(0.5), T[0]), fma32(S[0], F32(0.5), -T[0]))
+        R1 = (fma32(S[1], F32(0.5), T[1]), fma32(S[1], F32(0.5), -T[1]))
+        sq = ((R1[0] * R1[0]).astype(F32), (R1[1] * R1[1]).astype(F32))
+        pw = (fma32(R0[0], R0[0], sq[0]), fma32(R0[1], R0[1], sq[1]))
+        rows = np.arange(W)[:, None]
+        P_out[rows, kP[None, :].repeat(W, 0)] = pw[0]
+        P_out[rows, (512 - kP)[None, :].repeat(W, 0)] = pw[1]
+    z0 = Z[0][0]                  # lane 0: Z[0]
+    px = ((z0[0] + z0[1]).astype(F32), (z0[0] - z0[1]).astype(F32))
+    P_out[:, 0] = (px[0][:, 0] * px[0][:, 0]).astype(F32)
+    P_out[:, 512] = (px[1][:, 0] * px[1][:, 0]).astype(F32)
+    return P_out

@@ -72,7 +72,7 @@ def test_derived_bounds_dominate(A, O, case):
     bins = got in (3, 4)
     rc = np.asarray(info["rcoef"], np.float64)
     w_or = np.arccos(rc.astype(np.longdouble) / 2)
-    w_b = 2 * np.pi * np.round(np.asarray(freqs) * n / FS) / n
+    w_b = 2 * E.PI_L * np.round(np.asarray(freqs) * n / FS).astype(np.longdouble) / n
     w_det = w_b if bins else w_or
     worst1 = worst2 = (0.0, None)
     for fi, fam in enumerate(FAMILIES):
@@ -134,3 +134,56 @@ def test_error_model_abi(A):
     for f, meth in (((0.0, 8 * BIN, 512 * BIN), 3), ((0.0, 512 * BIN), 1), ((BIN * 0.01, 3000.0), 1)):
         mm = A.error_model(A.make_cfg(freqs=f, method=meth))
         assert np.isfinite(mm["tau"]) and mm["tau"] > 0, (f, mm)
+
+
+def _exact_spectrum(xw):
+    """|X_b|, b = 0..512, in long double (direct DFT)."""
+    n = xw.shape[1]
+    tb = np.outer(np.arange(n), np.arange(n // 2 + 1)) % n        # exact phase index
+    ph = (2 * E.PI_L / n) * tb.astype(np.longdouble)
+    xl = xw.astype(np.longdouble)
+    re = xl @ np.cos(ph)
+    im = xl @ np.sin(ph)
+    return np.sqrt(re * re + im * im).astype(np.float64)
+
+
+@pytest.mark.parametrize("plan", ["fsk2", "fsk8"])
+def test_fft_bounds_dominate(A, O, plan):
+    """The FFT detector (fft_quad.hip, emulated operation for operation by
+    fp32emu.fft_spectrum): its structural bound on EVERY bin of the 513, and
+    the double radix-2 oracle's (oracle_fft_power) against a long-double DFT."""
+    freqs = A.FSK2_FREQS if plan == "fsk2" else A.FSK8_FREQS
+    n = 1024
+    m = A.error_model(A.make_cfg(freqs=freqs, method=A.METHOD_FFT))
+    assert m["energy"] == A.ENERGY_PARSEVAL
+    bins = np.round(np.asarray(freqs) * n / FS).astype(int)
+    worst1 = worst2 = (0.0, None)
+    for fi, fam in enumerate(FAMILIES):
+        W = 24
+        x = family(fam, freqs, n, W, 2000 + fi)[:W * n]
+        xw = x.reshape(W, n)
+        P = E.fft_spectrum(x, n, W).astype(np.float64)
+        Pr = np.stack([O.fft_power(xw[i]) for i in range(W)])
+        X = _exact_spectrum(xw)
+        nrm = np.sqrt((xw.astype(np.float64) ** 2).sum(axis=1))[:, None]
+        d1 = np.abs(np.sqrt(P) - X)
+        d2 = np.abs(sigma(Pr) - X)
+        b1, b2 = m["rho_det"] * nrm, m["rho_ref"] * nrm
+        assert (d1 <= b1).all(), (fam, float((d1 / np.maximum(b1, 1e-300)).max()))
+        assert (d2 <= b2).all(), (fam, float((d2 / np.maximum(b2, 1e-300)).max()))
+        live = nrm[:, 0] > 0
+        if live.any():
+            r1 = float((d1[live] / b1[live]).max())
+            r2 = float((d2[live] / b2[live]).max())
+            worst1 = max(worst1, (r1, fam))
+            worst2 = max(worst2, (r2, fam))
+        # the kernel's test on its own powers (E = Parseval's 2 sum P): what
+        # it leaves unflagged is the oracle's symbol
+        Pt = P[:, bins]
+        Ps = np.sort(Pt, axis=1)
+        p1, p2 = Ps[:, -1], Ps[:, -2]
+        epar = 2 * P.sum(axis=1)
+        flag = ((p1 == 0) & (epar > 0)) | ((p1 > 0) & ((p1 - p2) ** 2 < m["t2e"] * epar * p1))
+        assert (np.argmax(Pt, 1)[~flag] == np.argmax(Pr[:, bins], 1)[~flag]).all(), fam
+    print(f"\nfft {plan}: rho_det {m['rho_det']:.3g} worst {worst1[0]:.3g} ({worst1[1]}); "
+          f"rho_ref {m['rho_ref']:.3g} worst {worst2[0]:.3g} ({worst2[1]})")

@@ -120,15 +120,17 @@ def test_near_ties_follow_exact_argmax(A, O, torch, plan, method):
     assert sure.sum() >= 20
     ref32 = ref_P[sure].astype(np.float32).view(np.int32)
     # the in-kernel rescue's first pass decides most of them from its own
-    # double powers: each within r64 sqrt(P_max NE) + r64^2 NE of the
-    # oracle's (its error model, tests/test_rescue_model64.py; ~1e-9 of P_max,
-    # so the top powers agree to an ulp of fp32 and a leakage bin at 1e-16 of
-    # P_max may not), then rounded to fp32
-    r64 = tau64 / 12.0
-    Pm = ref_P[sure].max(axis=1, keepdims=True)
-    ne = 1024.0 * (xw[sure] * xw[sure]).sum(axis=1)[:, None]   # the raw window's (fold too)
-    bound = r64 * np.sqrt(Pm * ne) + r64 * r64 * ne + 2.0 ** -23 * np.abs(ref_P[sure])
-    assert (np.abs(mag[sure].astype(np.float64) - ref_P[sure]) <= bound).all()
+    # double powers: each within its derived bound of the oracle's,
+    # |sqrt P_0 - sigma P_oracle| <= rho_first sqrt(sum x^2) (tests/
+    # test_rescue_model64.py), then rounded to fp32 (half an ulp: 2^-24
+    # relative in P, 2^-25 in sqrt P)
+    m = A.error_model(A.make_cfg(freqs=freqs, method=method))
+    assert m["tau64"] == pytest.approx(tau64, rel=1e-12)
+    e_raw = (xw[sure] * xw[sure]).sum(axis=1)[:, None]   # the raw window's (fold too)
+    g = mag[sure].astype(np.float64)
+    sig = np.sign(ref_P[sure]) * np.sqrt(np.abs(ref_P[sure]))
+    bound = m["rho_first"] * np.sqrt(e_raw) + 2.0 ** -24 * np.sqrt(g)
+    assert (np.abs(np.sqrt(g) - sig) <= bound).all()
     # with that pass off every rescued window takes the exact chain (the
     # double FFT for the FFT detector): the oracle's powers rounded to fp32,
     # bit for bit, and the same symbols
@@ -191,25 +193,25 @@ def test_rescue_double_ties_take_the_exact_chain(A, O, torch, plan, method):
     ((1500.0, 3000.0), GOERTZEL, 1024, 1024, True),
     (tuple(1500.0 + 375.0 * i for i in range(8)), FOLDED, 1024, 1024, True),
     (FSK8_ODD, RESIDUE, 1024, 1024, True),
-    ((46.875 * 1, 46.875 * 2), GOERTZEL, 1024, 1024, True),      # bin 1: r64 x 1
-    ((46.875 * 0.3, 1500.0), GOERTZEL, 1024, 1024, True),        # below bin 1: scaled
+    ((46.875 * 1, 46.875 * 2), GOERTZEL, 1024, 1024, True),      # bin 1
+    ((46.875 * 0.3, 1500.0), GOERTZEL, 1024, 1024, True),        # below bin 1
     ((1500.0, 3000.0), GOERTZEL, 1024, 256, False),              # SLIDE: rescue launch
     ((1500.0, 3000.0), GOERTZEL, 4096, 4096, False),             # n != 1024
     ((1500.0, 3000.0), FFT, 1024, 1024, True),                   # FFT: at its bins
     ((1500.0, 3000.0), FFT, 1024, 256, True),
-    ((0.0, 3000.0), FFT, 1024, 1024, False),                     # a bin at DC: none
+    ((0.0, 3000.0), FFT, 1024, 1024, True),                      # a bin at DC: finite now
 ])
 def test_rescue_tau64_is_the_stated_model(A, torch, freqs, method, n, hop, expect):
-    """The handle's tau64 is 12 x tests/test_rescue_model64.r64 (the constant
-    the CPU test checks the first pass's error model with; the FFT detector's
-    at its tone bins' frequencies), and 0 where no first pass runs."""
-    import test_rescue_model64 as M
-    with A.Demodulator(A.make_cfg(n=n, hop=hop, freqs=freqs, method=method)) as d:
+    """The handle's tau64 is the derived bound's (demod_error_model: 4
+    rho_first / sqrt(n), rho_first checked by tests/test_rescue_model64.py),
+    and 0 where no first pass runs (the rescue launch, n != 1024)."""
+    cfg = A.make_cfg(n=n, hop=hop, freqs=freqs, method=method)
+    with A.Demodulator(cfg) as d:
         t = d.rescue_tau64
-    if method == FFT:
-        freqs = tuple(round(f * 1024 / 48000.0) * 48000.0 / 1024 for f in freqs)
     if expect:
-        assert t == pytest.approx(12.0 * M.r64(freqs), rel=1e-12)
+        m = A.error_model(cfg)
+        assert t > 0 and t == pytest.approx(m["tau64"], rel=1e-12)
+        assert t == pytest.approx(4.0 * m["rho_first"] / 32.0, rel=1e-12)
     else:
         assert t == 0.0
 

@@ -1,19 +1,22 @@
-"""The decision rescue's error model, asserted on every window (VERDICT r3
-item 2; tests/error_model.py): for every detector path and tone plan of
-error_model.CASES (plain bank at the Reinsch edge, near Nyquist, n = 256 /
-4096, segment-shared; fold incl. F16, edge bins, n = 256 / 4096, fold-slide;
-residue with compile-time and LDS classes, n = 256 / 4096; FFT at hop 1024 /
-256) and every adversarial signal family (FSK at sigma 0 / 400, full scale
-with clipping, full-scale clipped square waves, DC offset + tone, uniform
-full-scale int16, dithered silence, two tones at equal power, a tone
+"""The decision rescue's derived error bounds, asserted on every window
+(tests/error_model.py): for every detector path and tone
+plan of error_model.CASES (plain bank at the Reinsch edge, near Nyquist,
+n = 256 / 4096, segment-shared; fold incl. F16, edge bins, n = 256 / 4096,
+fold-slide; residue with compile-time and LDS classes, n = 256 / 4096; FFT at
+hop 1024 / 256) and every adversarial signal family (FSK at sigma 0 / 400,
+full scale with clipping, full-scale clipped square waves, DC offset + tone,
+uniform full-scale int16, dithered silence, two tones at equal power, a tone
 cancelling itself, a near-Nyquist tone beside a plan tone):
-  * every fp32 tone power is within the model r sqrt(P_max NE) + r^2 NE, r =
-    tau / 12 the handle's own constant;
+  * every fp32 tone power is within the derived bound of the oracle's
+    (|sqrt P_gpu - sigma P_oracle| <= rho_det sqrt E_det + rho_ref sqrt E);
   * the kernel flags exactly the windows the stated threshold selects;
   * every window it leaves unflagged already carries the oracle's symbol;
   * quiet input is not flagged wholesale (the round-3 threshold
     used the int16 worst-case energy and flagged every window of dithered
     silence).
+And the kernels' fp32 powers equal tests/fp32emu.py's operation-for-operation
+emulation bit for bit (test_kernels_equal_emulation), which ties the CPU
+check of the bounds (tests/test_error_bound.py) to the shipped code.
 """
 import json
 import os
@@ -80,3 +83,72 @@ def test_rescued_decisions_every_window(A, O, torch, case):
         assert not (sym & 0x80).any(), (name, fam)
         bad = np.flatnonzero(sym != rs[:W])
         assert bad.size == 0, (name, fam, bad[:8].tolist())
+
+
+# the direct kernels of each path (the segment-shared ones are bit-identical
+# to them: test_gpu_slide.py, test_gpu_fold_slide.py)
+EMU_CASES = [c for c in EM.CASES if c[2] == c[3] and c[4] != 2] + [
+    ("plain_k16_n4096", tuple(700.0 + 1234.5 * i for i in range(16)), 4096, 4096, 1),
+    ("residue_k16", tuple(EM.BIN * (20 + 7 * i) for i in range(16)), 1024, 1024, 4),
+    ("plain_k3_ws", (1500.0, 2250.0, 3000.0), 1024, 1024, 1),
+]
+
+
+@pytest.mark.parametrize("case", EMU_CASES, ids=[c[0] for c in EMU_CASES])
+def test_kernels_equal_emulation(A, O, torch, case):
+    """The detector's fp32 tone powers (rescue off: FSKD_NO_RESCUE=1) equal
+    fp32emu.detector_powers bit for bit on adversarial families."""
+    import numpy as np
+    import fp32emu as E
+    name, freqs, n, hop, method = case
+    W = 512
+    cfg = A.make_cfg(n=n, hop=hop, freqs=freqs, method=method)
+    info = A.plan_info(cfg)
+    old = os.environ.get("FSKD_NO_RESCUE")
+    os.environ["FSKD_NO_RESCUE"] = "1"
+    try:
+        d = A.Demodulator(cfg)
+    finally:
+        if old is None:
+            del os.environ["FSKD_NO_RESCUE"]
+        else:
+            os.environ["FSKD_NO_RESCUE"] = old
+    with d:
+        for fi, fam in enumerate(("fsk_s400", "two_tone_equal", "random_full", "near_nyquist_tone")):
+            x = EM.family(fam, freqs, n, W, 300 + fi)[:W * n]
+            _, mag = d.batch(x, n_windows=W, mags=True)
+            emu = E.detector_powers(info, x, n, n, W, len(freqs))
+            diff = np.flatnonzero((mag != emu).any(axis=1))
+            assert diff.size == 0, (name, fam, diff.size, diff[:4].tolist(),
+                                    mag[diff[:1]].tolist(), emu[diff[:1]].tolist())
+
+
+def test_fft_kernel_equals_emulation(A, O, torch):
+    """The FFT detector's full 513-bin spectrum equals fp32emu.fft_spectrum bit
+    for bit (rescue off), at hop 1024 and hop 256."""
+    import numpy as np
+    import fp32emu as E
+    old = os.environ.get("FSKD_NO_RESCUE")
+    os.environ["FSKD_NO_RESCUE"] = "1"
+    try:
+        for hop in (1024, 256):
+            d = A.Demodulator(A.make_cfg(hop=hop, freqs=A.FSK8_FREQS, method=A.METHOD_FFT))
+            with d:
+                for fi, fam in enumerate(("fsk_s400", "random_full", "near_nyquist_tone")):
+                    W = 256
+                    blocks = -(-((W - 1) * hop + 1024) // 1024)
+                    x = EM.family(fam, A.FSK8_FREQS, 1024, blocks, 400 + fi)[:(W - 1) * hop + 1024]
+                    xt = torch.from_numpy(x).cuda()
+                    sym = torch.empty(W, dtype=torch.uint8, device="cuda")
+                    spec = torch.empty(W * 513, dtype=torch.float32, device="cuda")
+                    d.batch_spectrum_async(xt, W, sym, None, spec)
+                    torch.cuda.synchronize()
+                    got = spec.cpu().numpy().reshape(W, 513)
+                    emu = E.fft_spectrum(x, hop, W)
+                    diff = np.flatnonzero((got != emu).any(axis=1))
+                    assert diff.size == 0, (hop, fam, diff.size, diff[:4].tolist())
+    finally:
+        if old is None:
+            del os.environ["FSKD_NO_RESCUE"]
+        else:
+            os.environ["FSKD_NO_RESCUE"] = old
