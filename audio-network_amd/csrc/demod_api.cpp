@@ -47,7 +47,7 @@ struct demod {
     bool wb_bursts = true;
     bool rescue_kernel_forced = false;  // FSKD_RESCUE_LAUNCH=1: the rescue launch everywhere (measurement)
     int wb_force = 0;  // FSKD_WB_BURSTS=<n >= 1>: n bursts on every hop = n batch (measurement)
-    double tau = 0.0;           // decision rescue threshold factor (amb_tau)
+    double tau = 0.0;           // decision rescue threshold factor (error_model.cpp)
     float amb_tq = 0.f;         // stage 1: amb_tq sqrt(P_max), the int16 worst-case energy
     float amb_floor = 0.f;
     float amb_t2e = 0.f;        // stage 2: threshold^2 = amb_t2e E P_max

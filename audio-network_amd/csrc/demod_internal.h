@@ -75,21 +75,22 @@ struct GoertzelParams {
     float amb_d;
 };
 
-// Decision rescue. A detector's fp32 powers carry an error
-// |dP_k| <= r sqrt(P_max NE), NE the window's energy scale (n sum x^2; for
-// the fold detector (n/8) sum xf^2 of the folded window it transforms; r per
-// detector and tone plan, demod_api.cpp amb_tau, checked by
-// tests/test_gpu_error_model.py). Where the fp32 top-2 margin is below
-// tau sqrt(NE P_max) (tau = 12 r: two powers' errors, x 6), or P_max is so
-// small that the second-order term could dominate, the fp32 argmax may
-// differ from the exact one: the detector marks the window ambiguous and the
-// rescue (rescue_rows in the detector, or rescue_kernel) re-decides it with
-// the definition's double-precision arithmetic (bit-identical to
-// oracle/fsk_oracle.c). The test runs in two stages: NE <= Q = n^2 2^30 for
-// int16 input, so a window whose margin clears tau sqrt(Q P_max) clears the
-// exact test too and no per-sample work is spent on it (stage 1); only rows
-// stage 1 flags compute their energy (stage 2), so quiet input (dithered
-// silence, idle-channel noise) is not flagged wholesale.
+// Decision rescue. A detector's fp32 tone powers carry an
+// error that error_model.cpp BOUNDS, from the kernel's own operation sequence
+// and fp32 constants (round 5; no measured constant):
+// |sqrt(P_k) - |X_k|| <= rho_det sqrt(E), and the double oracle's
+// |sigma(P_ref,k) - |X_k|| <= rho_ref sqrt(sum x^2). A window whose fp32
+// top-2 margin satisfies (P_max - P_2nd)^2 >= t2e E_eff P_max (t2e = 16
+// (bound)^2) has sqrt P_max - sqrt P_2nd above twice both bounds, so its fp32
+// argmax is the oracle's; every other window (and P_max == 0 with energy) is
+// marked ambiguous and the rescue (rescue_rows in the detector, or
+// rescue_kernel) re-decides it with the definition's double-precision
+// arithmetic (bit-identical to oracle/fsk_oracle.c). The test runs in two
+// stages: E_eff <= E_max for int16 input, so a window whose margin clears
+// the threshold at E_max clears the exact test too and no per-sample work is
+// spent on it (stage 1, amb_tq / amb_floor); only rows stage 1 flags compute
+// their energy (stage 2), so quiet input (dithered silence, idle-channel
+// noise) is not flagged wholesale.
 // P_max == 0 (every fp32 tone power exactly zero) is a stage-1 candidate and
 // ambiguous when the window's energy is not zero: input with no energy at the
 // tones (a fold detector's folded window that cancels to a constant, say)
@@ -164,7 +165,8 @@ __device__ __forceinline__ int chain_decide(const float (&P)[K], bool live, floa
 
 // Sum of squares of the 64 int16 samples of one lane segment, 16-byte chunks
 // read by `chunk(i)` (i < 8), as fp32 (each square and partial sum rounded:
-// relative error < 1e-5, covered by the host's (1 + 1e-4) in amb_t2e).
+// relative error < 100 u, covered by error_model.cpp's safety factor in
+// amb_t2e).
 typedef unsigned int u32x4e __attribute__((ext_vector_type(4)));
 typedef float f32x2e __attribute__((ext_vector_type(2)));
 template <typename Chunk>
@@ -254,13 +256,14 @@ __device__ __forceinline__ long long tile_block(int swz)
 //    window's phase (rot64) and the row sums — K x 64 double steps per lane
 //    on all 16 lanes, instead of one 1024-step chain per tone on K lanes
 //    (~10x fewer wave instructions at K = 2). These powers are not the
-//    oracle's bits, but they are within |dP| <= r64 sqrt(P_max NE) of them
-//    (r64 ~1e-9: their error plus the oracle's own; demod_api.cpp
-//    rescue_r64, checked by tests/test_rescue_model64.py), so where their
-//    top-2 margin clears tau64 sqrt(NE P_max) (tau64 = 12 r64) the argmax is
-//    the oracle's and the row is decided here (its magnitudes: these powers
-//    rounded to fp32, within the model of the oracle's). Rows inside that band
-//    (exact ties; margins within ~1e-8 of P_max) go on to
+//    oracle's bits, but |sqrt P_0 - sigma P_ref| <= rho_first sqrt(E) (its own
+//    rounding and the oracle's, derived by error_model.cpp from both
+//    operation sequences; checked by tests/test_rescue_model64.py), so where
+//    their top-2 margin satisfies margin^2 >= t2e64 E P_max (t2e64 = 16
+//    rho_first^2) the argmax is the oracle's and the row is decided here (its
+//    magnitudes: these powers rounded to fp32, within the bound of the
+//    oracle's). Rows inside that band (exact ties; margins within ~1e-10 of
+//    P_max) go on to
 //  pass 1: lane seg < K runs tone seg's recurrence in double over the
 //    window's 1024 samples with exactly rescue_kernel's operations and order
 //    (so exactly oracle/fsk_oracle.c's: contraction off); the row's argmax

@@ -137,10 +137,12 @@ __device__ __forceinline__ bool fold_decide(const int (&acc)[8], const float4 *r
                 a2 = a1;
                 a1 = a;
             }
-            xr[2 * h] = r[2 * h].x * a1.x - r[2 * h].z * a2.x;
-            xi[2 * h] = r[2 * h].y * a1.x - r[2 * h].w * a2.x;
-            xr[2 * h + 1] = r[2 * h + 1].x * a1.y - r[2 * h + 1].z * a2.y;
-            xi[2 * h + 1] = r[2 * h + 1].y * a1.y - r[2 * h + 1].w * a2.y;
+            // explicit fma: the rounding does not depend on the compiler's
+            // contraction (error_model.cpp, tests/fp32emu.py)
+            xr[2 * h] = fmaf(r[2 * h].x, a1.x, -(r[2 * h].z * a2.x));
+            xi[2 * h] = fmaf(r[2 * h].y, a1.x, -(r[2 * h].w * a2.x));
+            xr[2 * h + 1] = fmaf(r[2 * h + 1].x, a1.y, -(r[2 * h + 1].z * a2.y));
+            xi[2 * h + 1] = fmaf(r[2 * h + 1].y, a1.y, -(r[2 * h + 1].w * a2.y));
         }
         if constexpr (K & 1) {
             float s1 = 0.f, s2 = 0.f;
@@ -150,8 +152,8 @@ __device__ __forceinline__ bool fold_decide(const int (&acc)[8], const float4 *r
                 s2 = s1;
                 s1 = a;
             }
-            xr[K - 1] = r[K - 1].x * s1 - r[K - 1].z * s2;
-            xi[K - 1] = r[K - 1].y * s1 - r[K - 1].w * s2;
+            xr[K - 1] = fmaf(r[K - 1].x, s1, -(r[K - 1].z * s2));
+            xi[K - 1] = fmaf(r[K - 1].y, s1, -(r[K - 1].w * s2));
         }
         return window_sum_decide<K, false, MST>(xr, xi, lane, w, live, p.sym, p.mag, 0, at, efn);
     }
@@ -330,8 +332,8 @@ __global__ __launch_bounds__(64 * WPB) void fold_tile_kernel(GoertzelParams p)
 #pragma unroll
             for (int k = 0; k < K; ++k) {
                 const float4 rk = ROTLDS ? rot_lds[k * g + j] : r[ROTLDS ? 0 : k];
-                xr[k] = rk.x * t1[k] - rk.z * t2[k];
-                xi[k] = rk.y * t1[k] - rk.w * t2[k];
+                xr[k] = fmaf(rk.x, t1[k], -(rk.z * t2[k]));
+                xi[k] = fmaf(rk.y, t1[k], -(rk.w * t2[k]));
             }
             const long long w = wbase + win_in_tile;
             auto efn = [&]() {
@@ -355,8 +357,8 @@ __global__ __launch_bounds__(64 * WPB) void fold_tile_kernel(GoertzelParams p)
                 s1 = a;
             }
             const float4 rk = ROTLDS ? rot_lds[k * g + j] : r[ROTLDS ? 0 : k];
-            float re = rk.x * s1 - rk.z * s2;
-            float im = rk.y * s1 - rk.w * s2;
+            float re = fmaf(rk.x, s1, -(rk.z * s2));  // explicit, as fold_decide
+            float im = fmaf(rk.y, s1, -(rk.w * s2));
             re = group_sum_f(re, log2g);
             im = group_sum_f(im, log2g);
             P[k] = fmaf(re, re, im * im);

@@ -188,10 +188,10 @@ __device__ __attribute__((always_inline)) inline void rescue_fft_window(const in
 // lane seg runs each tone bin's recurrence in double over its own 64 samples
 // (read once from global memory / L2 into 32 VGPRs: the group loop's
 // registers are dead here), rotates its end state into the window's phase
-// and the row sums. The bins' powers come within r64 sqrt(P_max NE) of the
-// oracle's double FFT (the recurrence's error; the FFT's own is ~1e-15), so
-// where their top-2 margin clears tau64 sqrt(NE P_max) the row is decided
-// here (symbol; tone powers rounded to fp32, within the model of the oracle's).
+// and the row sums. The bins' sqrt powers come within rho_first sqrt(E) of the
+// oracle's double FFT's (both errors, derived by error_model.cpp), so where
+// their top-2 margin satisfies margin^2 >= t2e64 E P_max the row is decided
+// here (symbol; tone powers rounded to fp32, within that bound of the oracle's).
 // Returns the lane's row verdict: still ambiguous (for rescue_fft_window).
 // x: the row's window (valid where amb_row); k tones at runtime.
 __device__ __forceinline__ bool rescue_fft_seg(const int16_t *__restrict__ x, const double *__restrict__ rot64,

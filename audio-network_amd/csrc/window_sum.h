@@ -237,12 +237,15 @@ __device__ __forceinline__ bool window_sum_decide(const float (&re)[K], const fl
     const int idx = j & (VS - 1);
     const bool re_lane = (idx & 1) == 0 && j < VS;
     const int t0 = idx >> 1;
+    // re^2 + im^2 in the re lane as fma(re, re, im^2): explicit, so the
+    // rounding does not depend on the compiler's contraction (the error
+    // bound and tests/fp32emu.py follow this operation sequence)
     float sq = v[0] * v[0];
-    const float P0 = sq + ws_dpp<0xB1>(sq);  // re^2 + im^2 in the re lane
+    const float P0 = __builtin_fmaf(v[0], v[0], ws_dpp<0xB1>(sq));
     float P1 = 0.f;
     if constexpr (V > 16) {
         sq = v[16] * v[16];
-        P1 = sq + ws_dpp<0xB1>(sq);
+        P1 = __builtin_fmaf(v[16], v[16], ws_dpp<0xB1>(sq));
     }
     const bool ok0 = re_lane && t0 < K;
     const bool ok1 = V > 16 && re_lane && t0 + 8 < K;
@@ -290,7 +293,7 @@ __device__ __forceinline__ bool window_sum_decide_split8(const float (&re)[4], c
     const bool re_lane = (j & 1) == 0;
     const int t0 = j >> 1;
     const float sq = v[0] * v[0];
-    const float P0 = sq + ws_dpp<0xB1>(sq);
+    const float P0 = __builtin_fmaf(v[0], v[0], ws_dpp<0xB1>(sq));  // as window_sum_decide
     const int o0 = PERM ? (int)((perm >> (4 * t0)) & 15u) : t0;
     float mx;
     const unsigned arg = ws_argmax_m<false>(__float_as_uint(P0), re_lane, o0, 0u, false, 0, mx);

@@ -14,6 +14,7 @@
 #   sq[:<args>]      one SQ pass (issue counts) of the tones-only FFT kernel
 #   sqw[:<ENV=V|-> <args>]  one SQ pass of its wait states (SQ_WAIT_ANY / _INST_ANY / _INST_LDS)
 #   testsall[:<args>] pytest -m gpu without -x (all failures in one call)
+#   testsk:<expr>    pytest -m gpu -k <expr> without -x
 #   precision        scripts/precision_probe.py
 #   py:<script args> python3 <script args> (probes under scripts/)
 #   pyt:<secs>:<args> the same under a time limit of its own
@@ -70,6 +71,9 @@ for st in "$@"; do
       ev=${arg%% *}; rest=${arg#* }; [ "$rest" = "$arg" ] && rest=""
       [ -z "$ev" ] || [ "$ev" = "-" ] && ev="X=1"
       (cd /tmp && export $ev && timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE --output-format csv -d "$O/sqw_$i" -o run -- python3 "$R/bench.py" --config fft --no-cpu-baseline --no-rescue-ab --warmup 2 --steps 5 $rest) > "$log" 2>&1 || exit $? ;;
+    testsk)
+      # pytest -m gpu -k <expr> without -x (the expression stays one argument)
+      timeout -k 10 1100 python -u -m pytest -v --timeout 300 --timeout-method thread -m gpu tests -k "$arg" > "$log" 2>&1 || exit $? ;;
     testsall)
       # the GPU suite without -x (every failure of a change set in one call)
       timeout -k 10 1100 python -u -m pytest -v --timeout 300 --timeout-method thread -m gpu tests $arg > "$log" 2>&1 || exit $? ;;

@@ -11,16 +11,15 @@ kernel issues, in the kernel's order:
                 d = fma(lam, s, t), s = fma(sg, s, d)); rotation
                 'ws'   (re, im) = fma(-(Bx, By), s2, (Ax, Ay) * s1)   (K >= 3, n = 1024)
                 'fmaf' re = fma(Ax, s1, -(Bx * s2))                    (K <= 2, n != 1024)
-  fold.hip      the same chain over the folded window; F16 combines the two
-                fold halves exactly (Z0 = E + O, Z8 = E - O) and sums over 8
-                lanes; the C rotation `Ax * s1 - Bx * s2` is emulated as the
-                compiler contracts it ('c': fma(Ax, s1, -(Bx * s2)))
+  fold.hip      the same chain over the folded window, rotation 'fmaf'; F16
+                combines the two fold halves exactly (Z0 = E + O, Z8 = E - O),
+                rotation 'ws', and sums over 8 lanes
   residue.hip   the 8-point class butterflies (exact integer adds, the 1/sqrt 2
                 products as FMAs), the chain on both components, the 4-term
                 rotation by FMAs
   window_sum.h  the reduce-scatter over the 16 lanes of a row (row_mirror,
                 row_half_mirror, quad_perm [2,3,0,1], [1,0,3,2]), then
-                P = re^2 + im^2 as sq + dpp(sq)
+                P = fma(re, re, im^2) (im^2 from the partner lane)
   group_sum     v += dpp(v) over xor 1, xor 2, half mirror, mirror, xor 16,
                 xor 32; P = fma(re, re, im * im)
 
@@ -83,7 +82,7 @@ def rotate(s1, s2, r, mode):
     if mode == "ws":
         re = fma32(-bx, s2, (ax * s1).astype(F32))
         im = fma32(-by, s2, (ay * s1).astype(F32))
-    elif mode in ("fmaf", "c"):
+    elif mode == "fmaf":
         re = fma32(ax, s1, -((bx * s2).astype(F32)))
         im = fma32(ay, s1, -((by * s2).astype(F32)))
     else:
@@ -131,8 +130,9 @@ def ws_powers(re, im):
     v = ws_reduce(v)
     P = np.zeros((W, K), F32)
     for lst in (0, 16) if 2 * KP > 16 else (0,):
-        sq = (v[:, :, lst] * v[:, :, lst]).astype(F32)
-        p = (sq + sq[:, _LANES ^ 1]).astype(F32)
+        a = v[:, :, lst]
+        sq = (a * a).astype(F32)
+        p = fma32(a, a, sq[:, _LANES ^ 1])
         VS = min(2 * KP, 16)
         for j in range(0, VS, 2):
             t = j // 2 + (8 if lst else 0)
@@ -209,7 +209,7 @@ def detector_powers(info, x, n, hop, W, K):
             v[:, :, 1::2] = im
             v = ws_reduce(v, stages=(2, 1, 0))
             sq = (v[:, :, 0] * v[:, :, 0]).astype(F32)
-            p = (sq + sq[:, _LANES ^ 1]).astype(F32)
+            p = fma32(v[:, :, 0], v[:, :, 0], sq[:, _LANES ^ 1])
             for j in range(0, 16, 2):
                 P[:, slot_tone[j // 2]] = p[:, j]
             return P
@@ -219,7 +219,7 @@ def detector_powers(info, x, n, hop, W, K):
         for k in range(K):
             s1, s2 = chain_plain(seg, coef[k])
             r = rot[k * G:(k + 1) * G][None, :, :]
-            re[:, :, k], im[:, :, k] = rotate(s1, s2, r, "c")
+            re[:, :, k], im[:, :, k] = rotate(s1, s2, r, "fmaf")
         if log2g == 4:
             return ws_powers(re, im)
         for k in range(K):
