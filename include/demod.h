@@ -25,9 +25,14 @@
  * Decisions: every symbol is the argmax of the tone powers as the double-
  * precision definition computes them (ties to the lowest tone). The kernels
  * decide in fp32; a window whose fp32 top-2 margin lies within the powers'
- * error bound is flagged, and the decision rescue decides it
- * again in double with the definition's own arithmetic and rewrites its
- * symbol and powers. The flag test runs in two stages: the int16 worst-case
+ * error bound (derived from the kernel's operation sequence and constants,
+ * demod_error_model) is flagged, and the decision rescue
+ * decides it again in double and rewrites its symbol and powers: first by
+ * 64-sample segments (n = 1024; its own derived bound against the
+ * definition's, so the rewritten powers are within that bound of the
+ * definition's, not its bits), and where that pass cannot decide, with the
+ * definition's own arithmetic (powers bit-identical to it; every rescued
+ * window with FSKD_RESCUE_SEG=0). The flag test runs in two stages: the int16 worst-case
  * energy first (no per-sample work), then, only for windows that test
  * flags, the window's own energy, so quiet input is not flagged wholesale.
  * The rescue runs inside the detector's own launch for every detector at
