@@ -221,6 +221,21 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
                                            ctypes.c_uint64, _SZ, ctypes.c_int, ctypes.c_int,
                                            _P, _P, _P]),
         "demod_read_ceiling_async": (ctypes.c_int, [_P, _SZ, _P]),
+        "demod_group_unique_id": (ctypes.c_int, [_P]),
+        "demod_group_shard": (ctypes.c_int, [_SZ, ctypes.c_int, ctypes.c_int, ctypes.POINTER(_SZ),
+                                             ctypes.POINTER(_SZ)]),
+        "demod_group_block_bytes": (ctypes.c_longlong, [_SZ, ctypes.c_int, _SZ, _SZ, ctypes.c_int]),
+        "demod_group_create": (_P, [ctypes.POINTER(DemodCfg), _SZ, ctypes.c_int, ctypes.c_int, _P,
+                                    ctypes.POINTER(ctypes.c_int)]),
+        "demod_group_create_local": (_P, [ctypes.POINTER(DemodCfg), _SZ, ctypes.c_int, _P,
+                                          ctypes.POINTER(ctypes.c_int)]),
+        "demod_group_destroy": (None, [_P]),
+        "demod_group_world": (ctypes.c_int, [_P]),
+        "demod_group_local_ranks": (ctypes.c_int, [_P]),
+        "demod_group_rank_shard": (ctypes.c_int, [_P, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
+                                                  ctypes.POINTER(_SZ), ctypes.POINTER(_SZ)]),
+        "demod_group_push": (ctypes.c_int, [_P, _P, _P, _P, _SZ, _P]),
+        "demod_group_bucket_async": (ctypes.c_longlong, [_P, _P, _SZ, _SZ, _SZ, _P, _P]),
         "demod_strerror": (ctypes.c_char_p, [ctypes.c_int]),
         "demod_version_string": (ctypes.c_char_p, []),
     }
@@ -814,3 +829,110 @@ def iter_frames(stream: bytes):
         payload, used = frame_decode(stream[pos:])
         yield payload
         pos += used
+
+
+# ---- many streams over many GPUs (demod_group_*, RCCL) -----------------------
+
+DEMOD_GROUP_ID_BYTES = 128
+
+
+def group_unique_id() -> bytes:
+    """demod_group_unique_id: a fresh RCCL group id (rank 0 shares it)."""
+    buf = (ctypes.c_uint8 * DEMOD_GROUP_ID_BYTES)()
+    rc = load_library().demod_group_unique_id(buf)
+    if rc != DEMOD_OK:
+        raise DemodError(rc, "demod_group_unique_id")
+    return bytes(buf)
+
+
+def group_shard(n_streams: int, rank: int, world: int) -> Tuple[int, int]:
+    f, c = _SZ(), _SZ()
+    rc = load_library().demod_group_shard(n_streams, rank, world, ctypes.byref(f), ctypes.byref(c))
+    if rc != DEMOD_OK:
+        raise DemodError(rc, "demod_group_shard")
+    return f.value, c.value
+
+
+def group_block_bytes(n_streams: int, world: int, steps: int, symbols_per_stream: int, bits: int) -> int:
+    rc = load_library().demod_group_block_bytes(n_streams, world, steps, symbols_per_stream, bits)
+    if rc < 0:
+        raise DemodError(int(rc), "demod_group_block_bytes")
+    return int(rc)
+
+
+class Group:
+    """demod_group_t: n_streams streams sharded over `world` GPUs, RCCL gathers.
+    Group(cfg, n, rank=r, world=w, uid=...) is one rank of a multi-process
+    group; Group(cfg, n, devices=[...]) drives every rank in this process."""
+
+    def __init__(self, cfg: DemodCfg, n_streams: int, rank: int = 0, world: int = 1,
+                 uid: Optional[bytes] = None, devices: Optional[Sequence[int]] = None):
+        self._lib = load_library()
+        err = ctypes.c_int(0)
+        if devices is not None:
+            arr = (ctypes.c_int * len(devices))(*devices)
+            self._h = self._lib.demod_group_create_local(ctypes.byref(cfg), n_streams, len(devices), arr,
+                                                         ctypes.byref(err))
+        else:
+            if uid is None:
+                uid = group_unique_id()
+            buf = (ctypes.c_uint8 * DEMOD_GROUP_ID_BYTES).from_buffer_copy(uid)
+            self._h = self._lib.demod_group_create(ctypes.byref(cfg), n_streams, rank, world, buf,
+                                                   ctypes.byref(err))
+        if not self._h:
+            raise DemodError(err.value, "demod_group_create")
+        self.n_streams = n_streams
+        self.k = cfg.k
+        self.channels = int(cfg.channels)
+        self.world = self._lib.demod_group_world(self._h)
+        self.local_ranks = self._lib.demod_group_local_ranks(self._h)
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._lib.demod_group_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        self.close()
+
+    def shard(self, local: int = 0) -> Tuple[int, int, int]:
+        """(rank, first stream, count) of the local-th rank this process drives."""
+        r, f, c = ctypes.c_int(), _SZ(), _SZ()
+        rc = self._lib.demod_group_rank_shard(self._h, local, ctypes.byref(r), ctypes.byref(f),
+                                              ctypes.byref(c))
+        if rc != DEMOD_OK:
+            raise DemodError(rc, "demod_group_rank_shard")
+        return r.value, f.value, c.value
+
+    def push(self, packets: Sequence[np.ndarray], cap: Optional[int] = None):
+        """One packet per stream this process owns -> (symbols of every stream,
+        counts per stream)."""
+        packets = [np.ascontiguousarray(p, dtype=np.int16) for p in packets]
+        nf = (_SZ * len(packets))(*[p.size // self.channels for p in packets])
+        ptrs = (ctypes.c_void_p * len(packets))(*[p.ctypes.data if p.size else None for p in packets])
+        if cap is None:
+            cap = sum(p.size for p in packets) * max(self.world, 1) + 64 * self.n_streams
+        sym = np.zeros(max(cap, 1), np.uint8)
+        counts = np.zeros(self.n_streams, np.uint32)
+        rc = self._lib.demod_group_push(self._h, ptrs, nf, sym.ctypes.data, cap, counts.ctypes.data)
+        if rc < 0:
+            raise DemodError(rc, "demod_group_push")
+        return sym[:rc], counts
+
+    def bucket_async(self, d_pcm: Sequence, ring: int, wps: int, steps: int, d_all: Sequence,
+                     streams: Optional[Sequence[int]] = None) -> int:
+        """demod_group_bucket_async over the ranks this process drives."""
+        n = len(d_all)
+        pc = (ctypes.c_void_p * n)(*[_ptr(t) for t in d_pcm])
+        pa = (ctypes.c_void_p * n)(*[_ptr(t) for t in d_all])
+        ps = (ctypes.c_void_p * n)(*(streams or [0] * n))
+        rc = self._lib.demod_group_bucket_async(self._h, pc, ring, wps, steps, pa, ps)
+        if rc < 0:
+            raise DemodError(int(rc), "demod_group_bucket_async")
+        return int(rc)

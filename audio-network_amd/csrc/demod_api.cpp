@@ -1072,6 +1072,26 @@ static size_t streams_windows(const demod_streams_t *ms, size_t s, size_t n_fram
     return total < ms->cfg.n ? 0 : (total - ms->cfg.n) / ms->cfg.hop + 1;
 }
 
+}  // extern "C"
+
+// The symbols each stream emits on a push of these packet sizes (exactly what
+// demod_streams_push will write to counts; demod_group.cpp gathers them
+// before the push). Returns the total.
+long long fskd::streams_counts(const demod_streams_t *ms, const size_t *n_frames, uint32_t *counts)
+{
+    if (!ms || !n_frames || !counts) return DEMOD_BAD_ARG;
+    long long w = 0;
+    for (size_t s = 0; s < ms->carry.size(); ++s) {
+        counts[s] = (uint32_t)streams_windows(ms, s, n_frames[s]);
+        w += counts[s];
+    }
+    return w;
+}
+
+int fskd::streams_device(const demod_streams_t *ms) { return ms ? ms->st->device : -1; }
+
+extern "C" {
+
 long long demod_streams_max_symbols(const demod_streams_t *ms, const size_t *n_frames)
 {
     if (!ms || !n_frames) return DEMOD_BAD_ARG;

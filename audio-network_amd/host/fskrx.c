@@ -9,6 +9,7 @@
  *   fskrx [-c 1|2] [-m left|right|downmix] [-f f1,f2,...] [-n N] [-H hop]
  *         [-M auto|goertzel|folded|fft] [-L lead_in] [-p frames_per_read] [-b] < pcm > frames
  *   fskrx [same options] -l tcp_port -r [-u udp_port] [-a addr] [-N name] [-1] > frames
+ *   fskrx [same options] -g gpus [-S streams] -o prefix < interleaved pcm
  *
  * Default: 48 kHz mono, N = hop = 1024, 2-FSK at 1500/3000 Hz, reads of 2880
  * frames (one 60 ms packet) each passed to demodulate(). -b reads all input
@@ -20,6 +21,15 @@
  * flushed at EOF. Statistics go to stderr.
  * Exit status: 0 ok, 2 usage, 3 demod_create failed (e.g. no gfx950 device:
  * there is no CPU fallback), 4 demodulation / framing error, 5 I/O error.
+ *
+ * Group mode (-g, configs[4] from the C host): S streams
+ * (-S, default the number of GPUs) demodulated over the first `gpus` GPUs of
+ * this process as one RCCL group (demod_group_create_local: the streams
+ * sharded over the GPUs, each GPU's symbols all-gathered over RCCL,
+ * demod_group_push). stdin carries the streams packet-interleaved: per
+ * round, one packet of -p frames of stream 0, then stream 1, ...; a short
+ * final round is dealt to the streams in order. Stream s's ToReceiver frames
+ * go to <prefix><s>.bin, byte-identical to fskrx run on that stream alone.
  *
  * Network mode (-l) takes the receiver's place on the
  * wire instead of stdin: it listens on TCP (58764 in the reference,
@@ -65,6 +75,7 @@ static int usage(void)
                     "< pcm > frames\n"
                     "       fskrx [options] -l tcp_port -r [-u udp_port] [-a addr] [-N name] [-1] "
                     "> frames\n"
+                    "       fskrx [options] -g gpus [-S streams] -o prefix < interleaved pcm\n"
                     "  -r: AudioData payloads are raw int16 PCM (this receiver does not decode "
                     "Opus; without -r audio is refused)\n");
     return 2;
@@ -78,6 +89,7 @@ struct sink {
     uint8_t *frame;
     size_t frame_cap;
     unsigned long long frames, bytes, symbols;
+    FILE *out; /* NULL: stdout */
 };
 
 /* Frame the first cnt buffered symbols, one payload (<= per symbols) per
@@ -92,7 +104,7 @@ static int sink_emit(struct sink *s, size_t cnt)
             fprintf(stderr, "fskrx: framing: %s\n", demod_strerror((int)w));
             return 4;
         }
-        if (fwrite(s->frame, 1, (size_t)w, stdout) != (size_t)w) return 5;
+        if (fwrite(s->frame, 1, (size_t)w, s->out ? s->out : stdout) != (size_t)w) return 5;
         s->frames += 1;
         s->bytes += (unsigned long long)w;
     }
@@ -338,6 +350,85 @@ static int serve(demod_t *st, const demod_cfg_t *cfg, struct sink *s, const stru
     return rc;
 }
 
+/* ---- group mode ---------------------------------------------------------- */
+
+static int run_group(const demod_cfg_t *cfg, int gpus, int n_streams, size_t per_read, const char *prefix)
+{
+    int devs[64];
+    for (int i = 0; i < gpus; ++i) devs[i] = i;
+    int err = 0;
+    demod_group_t *g = demod_group_create_local(cfg, (size_t)n_streams, gpus, devs, &err);
+    if (!g) {
+        fprintf(stderr, "fskrx: demod_group_create_local: %s\n", demod_strerror(err));
+        return 3;
+    }
+    const size_t S = (size_t)n_streams, ch = cfg->channels;
+    struct sink *sk = calloc(S, sizeof *sk);
+    int16_t *pcm = malloc(S * per_read * ch * sizeof(int16_t));
+    const int16_t **ptr = calloc(S, sizeof *ptr);
+    size_t *nf = calloc(S, sizeof *nf);
+    uint32_t *counts = calloc(S, sizeof *counts);
+    const size_t cap = S * ((per_read + cfg->n) / cfg->hop + 2);
+    uint8_t *sym = malloc(cap);
+    int rc = (sk && pcm && ptr && nf && counts && sym) ? 0 : 4;
+    for (size_t i = 0; !rc && i < S; ++i) {
+        char path[4096];
+        snprintf(path, sizeof path, "%s%zu.bin", prefix, i);
+        sk[i].bits = demod_bits_per_symbol(cfg->k);
+        sk[i].per = (size_t)DEMOD_MAX_FRAME_PAYLOAD * 8 / (size_t)sk[i].bits;
+        sk[i].frame_cap = demod_frame_size(DEMOD_MAX_FRAME_PAYLOAD);
+        sk[i].frame = malloc(sk[i].frame_cap);
+        sk[i].out = fopen(path, "wb");
+        if (!sk[i].frame || !sk[i].out) rc = 5;
+    }
+    unsigned long long frames_in = 0, syms = 0;
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    while (!rc) {
+        const size_t got = fread(pcm, sizeof(int16_t) * ch, S * per_read, stdin);
+        if (ferror(stdin)) { rc = 5; break; }
+        if (!got) break;
+        size_t left = got;
+        for (size_t i = 0; i < S; ++i) {   /* a short final round is dealt in stream order */
+            nf[i] = left < per_read ? left : per_read;
+            left -= nf[i];
+            ptr[i] = pcm + i * per_read * ch;
+        }
+        const int ns = demod_group_push(g, ptr, nf, sym, cap, counts);
+        if (ns < 0) {
+            fprintf(stderr, "fskrx: demod_group_push: %s\n", demod_strerror(ns));
+            rc = 4;
+            break;
+        }
+        frames_in += got;
+        syms += (unsigned long long)ns;
+        size_t off = 0;
+        for (size_t i = 0; i < S && !rc; ++i) {
+            rc = sink_push(&sk[i], sym + off, counts[i]);
+            off += counts[i];
+        }
+        if (got < S * per_read) break;
+    }
+    for (size_t i = 0; i < S && sk; ++i) {
+        if (!rc && sk[i].n) rc = sink_emit(&sk[i], sk[i].n);
+        if (sk[i].out && fclose(sk[i].out) != 0 && !rc) rc = 5;
+        free(sk[i].sym);
+        free(sk[i].frame);
+    }
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    const double el = (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+    fprintf(stderr, "fskrx: group of %d GPU(s), %d streams: %llu frames in, %llu symbols, %.3f s wall\n",
+            demod_group_world(g), n_streams, frames_in, syms, el);
+    free(sk);
+    free(pcm);
+    free(ptr);
+    free(nf);
+    free(counts);
+    free(sym);
+    demod_group_destroy(g);
+    return rc;
+}
+
 int main(int argc, char **argv)
 {
     demod_cfg_t cfg;
@@ -345,6 +436,8 @@ int main(int argc, char **argv)
     size_t per_read = 2880; /* one 60 ms packet at 48 kHz (playback.cpp:10) */
     int batch = 0;
     struct net nt = {"0.0.0.0", -1, -1, "", 0, 0};
+    int gpus = 0, n_streams = 0;
+    const char *prefix = NULL;
     for (int i = 1; i < argc; ++i) {
         const char *a = argv[i];
         const char *v = i + 1 < argc ? argv[i + 1] : NULL;
@@ -362,6 +455,9 @@ int main(int argc, char **argv)
         else if (!strcmp(a, "-H")) cfg.hop = (uint32_t)atoi(v);
         else if (!strcmp(a, "-p")) per_read = (size_t)strtoull(v, NULL, 10);
         else if (!strcmp(a, "-L")) cfg.lead_in = (uint32_t)strtoul(v, NULL, 10);
+        else if (!strcmp(a, "-g")) gpus = atoi(v);
+        else if (!strcmp(a, "-S")) n_streams = atoi(v);
+        else if (!strcmp(a, "-o")) prefix = v;
         else if (!strcmp(a, "-m")) {
             if (!strcmp(v, "left")) cfg.channel_mode = DEMOD_CH_LEFT;
             else if (!strcmp(v, "right")) cfg.channel_mode = DEMOD_CH_RIGHT;
@@ -392,6 +488,10 @@ int main(int argc, char **argv)
         strlen(nt.name) >= DEMOD_INFO_STRING_CAP)
         return usage();
 
+    if (gpus || n_streams || prefix) {
+        if (gpus < 1 || gpus > 64 || !prefix || n_streams < 0 || batch || nt.tcp_port >= 0) return usage();
+        return run_group(&cfg, gpus, n_streams ? n_streams : gpus, per_read, prefix);
+    }
     int err = 0;
     demod_t *st = demod_create(&cfg, &err);
     if (!st) {

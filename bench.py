@@ -385,6 +385,7 @@ def run_config(A, D, torch, dist, args, config, rank, world, local, use_dist, st
     ms_per_step_eager = None
     breakdown = None
     bucket = None
+    c_group = None
     ring_slots = 1
     graph_hook = bool(os.environ.get("BENCH_TEST_GRAPH_FAIL"))  # tests: the capture-failure path under gloo
     if use_dist and dev_framing and getattr(args, "graph", False) and (args.dist_backend == "nccl" or graph_hook):
@@ -561,6 +562,56 @@ def run_config(A, D, torch, dist, args, config, rank, world, local, use_dist, st
             ms_per_step = time_graphs(graphs, 1, n_rep)
             all_sym = graphs[(n_rep - 1) % 2][1]
             st["i"] = n_rep
+        if getattr(args, "c_group", False) and S > 1:
+            # the same bucket through the C ABI's RCCL group (demod_group_
+            # bucket_async: detector launches, device framing, ncclAllGather on
+            # its own communicator), captured and replayed the same way
+            # 
+            uid = None
+            if world > 1:
+                box = [A.group_unique_id() if rank == 0 else None]
+                dist.broadcast_object_list(box, src=0, group=group)
+                uid = box[0]
+            cg = A.Group(cfg, n_streams, rank=rank, world=world, uid=uid)
+            cblock = A.group_block_bytes(n_streams, world, S, wps, bits)
+            c_all = torch.zeros(cblock * world, dtype=torch.uint8, device=dev)
+            src = ring if ring is not None else d_pcm
+            Rc = R if ring is not None else 1
+
+            # one eager bucket first: it sizes the group's buffers (no
+            # allocation may happen under capture) and warms the communicator
+            cg.bucket_async([src], Rc, wps, S, [c_all], [torch.cuda.current_stream().cuda_stream])
+            torch.cuda.synchronize()
+
+            def build_c():
+                g_ = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g_):
+                    cg.bucket_async([src], Rc, wps, S, [c_all], [torch.cuda.current_stream().cuda_stream])
+                return [(g_, None)]
+            try:
+                c_ms = time_graphs(build_c(), S, -(-steps // S))
+                how = "hip graph"
+            except Exception as e:  # noqa: BLE001
+                c_ms = None
+                how = f"graph failed: {type(e).__name__}: {e}"[:200]
+            c_bad = None
+            if c_ms is not None:
+                all_true_c = D.gather_symbols(d_true, gunits, world, unit=gunit) if world > 1 else d_true
+                if rank == 0:
+                    blocks = c_all.view(world, cblock).cpu().numpy()
+                    tru = all_true_c.cpu().numpy().reshape(n_streams, wps)
+                    c_bad = 0
+                    for r_ in range(world):
+                        first, cnt = D.shard_range(n_streams, r_, world)
+                        for s_ in range(S):
+                            for j in range(cnt):
+                                off = (s_ * cnt + j) * fstride
+                                back = D.unframe_symbols(A, blocks[r_][off:off + fstride].tobytes(), wps, K)
+                                c_bad += int((back != tru[first + j]).sum())
+            cg.close()
+            c_group = {"ms_per_step": round(c_ms, 4) if c_ms is not None else None, "step": how,
+                       "symbol_errors": c_bad,
+                       "api": "demod_group_bucket_async (C ABI, its own RCCL communicator)"}
         if getattr(args, "breakdown", False):
             # where the step's time above the kernel goes
             def eager_det():
@@ -718,6 +769,10 @@ def run_config(A, D, torch, dist, args, config, rank, world, local, use_dist, st
                 r["overhead"]["graph_error"] = bucket.get("graph_error")
         if breakdown is not None:
             r["overhead"]["breakdown"] = breakdown
+        if c_group is not None:
+            if c_group["ms_per_step"]:
+                c_group["ratio_to_torch_path"] = round(c_group["ms_per_step"] / ms_per_step, 4)
+            r["overhead"]["c_group"] = c_group
     if config == "fft":
         # the FFT is reported against the VALU roof too.
         # Algorithmic flops per window: 2.5 N log2 N for the real N-point
@@ -953,6 +1008,8 @@ def streams_child(args, n_streams: int = 1024, breakdown: bool = False) -> dict:
            "--steps", str(max(args.steps, 256)), "--warmup", str(args.warmup), "--no-cpu-baseline"]
     if breakdown:
         cmd.append("--breakdown")
+    elif n_streams == 1024:
+        cmd.append("--c-group")   # the same bucket through the C ABI's RCCL group, beside it
     r = subprocess.run(cmd, capture_output=True, timeout=600, cwd=ROOT, env=env)
     lines = [ln for ln in r.stdout.decode().splitlines() if ln.startswith("{")]
     if r.returncode != 0 or not lines:
@@ -1272,6 +1329,9 @@ def main():
     ap.add_argument("--no-ring", dest="ring", action="store_false",
                     help="configs[4] graph bucket: S detector launches over one input buffer instead "
                          "of one launch over an S-slot input ring")
+    ap.add_argument("--c-group", action="store_true",
+                    help="streams config: also time the same bucket through the C ABI's RCCL group "
+                         "(demod_group_bucket_async) and report it beside the torch path")
     ap.add_argument("--breakdown", action="store_true",
                     help="streams config: also time the step's pieces (detector alone, graphs "
                          "without the gather / framing, 1 / S / 8 steps per graph)")

@@ -332,6 +332,74 @@ long long demod_streams_max_symbols(const demod_streams_t *ms, const size_t *n_f
 int demod_streams_push(demod_streams_t *ms, const int16_t *const *pcm, const size_t *n_frames,
                        uint8_t *symbols, float *mags, size_t cap, uint32_t *counts);
 
+/* ---- many streams over many GPUs (config 5), RCCL ---------------------- */
+/*
+ * A group of `world` ranks, one per GPU, demodulating n_streams streams of one
+ * configuration: rank r owns the contiguous stream shard
+ * demod_group_shard(n_streams, r, world) and demodulates it on its own device;
+ * RCCL (over xGMI) carries only the decoded result: an all-gather of every
+ * rank's symbols (push) or ToReceiver frames (bucket). SURVEY.md §7 step 5 /
+ * §8e: one process per GPU (demod_group_create: hipSetDevice to cfg->device +
+ * ncclCommInitRank with rank 0's demod_group_unique_id, shared out of band),
+ * or one process driving several GPUs (demod_group_create_local:
+ * ncclCommInitAll). The reference fans one stream out to N receivers
+ * (MulticastAudioOutput.kt:88-96); this gathers N GPUs' share of many streams.
+ * Every call that gathers is a collective: every rank makes it.
+ */
+#define DEMOD_GROUP_ID_BYTES 128   /* sizeof(ncclUniqueId) */
+typedef struct demod_group demod_group_t;
+
+/* A fresh group id (ncclGetUniqueId) into id[DEMOD_GROUP_ID_BYTES]. */
+int demod_group_unique_id(uint8_t *id);
+/* Rank `rank`'s contiguous, balanced stream shard (pure arithmetic). */
+int demod_group_shard(size_t n_streams, int rank, int world, size_t *first, size_t *count);
+/* Bytes per rank of a bucket's gathered frames: steps x ceil(n_streams /
+ * world) x demod_frame_symbols_size(symbols_per_stream, bits, 4096). */
+long long demod_group_block_bytes(size_t n_streams, int world, size_t steps,
+                                  size_t symbols_per_stream, int bits);
+/* One rank of a multi-process group (cfg->device is its GPU). NULL on
+ * failure, *error set. */
+demod_group_t *demod_group_create(const demod_cfg_t *cfg, size_t n_streams, int rank, int world,
+                                  const uint8_t *id, int *error);
+/* Every rank in this process, rank i on devices[i]. */
+demod_group_t *demod_group_create_local(const demod_cfg_t *cfg, size_t n_streams, int n_devices,
+                                        const int *devices, int *error);
+void demod_group_destroy(demod_group_t *g);
+int demod_group_world(const demod_group_t *g);
+int demod_group_local_ranks(const demod_group_t *g);   /* ranks this process drives */
+int demod_group_rank_shard(const demod_group_t *g, int local, int *rank, size_t *first,
+                           size_t *count);
+
+/*
+ * One packet per stream this process owns (a local group: all n_streams; one
+ * rank of a multi-process group: its shard, pcm[i] = stream first + i), each
+ * demodulated as demod_streams_push does (per-stream carry and lead-in).
+ * Every stream's count is gathered first, then every rank's symbols; on
+ * return, on every rank, symbols[] holds all n_streams streams' symbols
+ * (stream 0 first) and counts[0 .. n_streams-1] their counts. Returns the
+ * total; if cap is too small, every rank returns DEMOD_BUFFER_TOO_SMALL
+ * before anything is consumed.
+ */
+int demod_group_push(demod_group_t *g, const int16_t *const *pcm, const size_t *n_frames,
+                     uint8_t *symbols, size_t cap, uint32_t *counts);
+
+/*
+ * Config 5's step, device-resident, for each rank l this process drives
+ * (arrays indexed by l): d_pcm[l] holds `ring` steps' batches of the rank's
+ * streams, [ring][count][wps windows][n] (cfg.hop == n), the same batch in
+ * each slot or a fresh one. `steps` (a multiple of ring) steps run as
+ * steps / ring detector launches, ONE device framing launch over the steps'
+ * symbol rows (one ToReceiver run per stream per step) and ONE RCCL
+ * all-gather into d_all[l] ([world][block] bytes, rank q's block = its frames,
+ * [step][stream][stride]), all enqueued on streams[l] (hipStream_t; NULL
+ * array = default streams), so a caller may capture it in a HIP graph (make
+ * one call of the shape outside capture first: it sizes the rank's buffers).
+ * Returns block bytes (demod_group_block_bytes) or a negative code.
+ */
+long long demod_group_bucket_async(demod_group_t *g, const int16_t *const *d_pcm, size_t ring,
+                                   size_t wps, size_t steps, uint8_t *const *d_all,
+                                   void *const *streams);
+
 /* ---- ip.proto framing (ToReceiver{AudioData{bytes}}, delimited) ------- */
 
 /* Bytes demod_frame_encode needs for a payload of len bytes. */

@@ -237,3 +237,34 @@ def test_network_refuses_non_pcm_audio(A, fskrx, raw, payload):
     assert which == A.DEMOD_MSG_RECEIVER_ERROR and used == len(reply)
     assert fields == {"audio_underflow": False, "audio_decode_error": True}
     assert b"1 refused" in err and out == b""
+
+
+@pytest.mark.gpu
+def test_group_mode_matches_single_streams(fskrx, tmp_path, A, O):
+    """fskrx -g 1 -S 3: three packet-interleaved streams through a one-GPU
+    RCCL group (demod_group_create_local + demod_group_push); each stream's
+    frames are byte-identical to fskrx run on that stream alone, and decode
+    to the oracle's symbols."""
+    S, per = 3, 2880
+    streams = []
+    for s in range(S):
+        pcm, _ = O.synth_fsk(A.FSK2_FREQS, 1024, 40 + 7 * s, 77 + s)
+        streams.append(pcm.reshape(-1))
+    L = max(x.size for x in streams)
+    rounds = -(-L // per)
+    # whole rounds (zero-padded streams), so every stream sees the same packets
+    full = [np.concatenate([streams[s], np.zeros(rounds * per - streams[s].size, np.int16)])
+            for s in range(S)]
+    inter = np.concatenate([full[s][r * per:(r + 1) * per] for r in range(rounds) for s in range(S)])
+    prefix = str(tmp_path / "s")
+    r = _run(fskrx, inter, "-g", "1", "-S", str(S), "-o", prefix, "-p", str(per))
+    assert r.returncode == 0, r.stderr.decode()
+    for s in range(S):
+        alone = _run(fskrx, full[s], "-p", str(per))
+        assert alone.returncode == 0
+        got = open(f"{prefix}{s}.bin", "rb").read()
+        assert got == alone.stdout, s
+        n = full[s].size // 1024
+        sym = _symbols(A, got, n, 1)
+        ref, _ = O.goertzel(full[s][:n * 1024], A.FSK2_FREQS, 1024)
+        assert np.array_equal(sym, ref)

@@ -63,6 +63,30 @@ def test_config5_streams_rccl_gather_world1():
     assert ps["symbol_mismatches"] == 0 and ps["max_rel_mag_err"] <= 1e-5
 
 
+def test_config5_c_group_bucket_world1():
+    """bench.py --config streams --c-group: the configs[4] bucket through the
+    C ABI's RCCL group (demod_group_bucket_async, its own communicator),
+    captured in a HIP graph like the torch path's; every frame decodes to the
+    transmitted symbols and its step time is reported beside the torch
+    path's (within 2 % on the line; loosely here)."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU visible")
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    env.pop("MASTER_PORT", None)
+    r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--config", "streams",
+                        "--force-dist", "--c-group", "--steps", "64", "--warmup", "5",
+                        "--no-cpu-baseline"], capture_output=True, timeout=400, cwd=ROOT, env=env)
+    out = r.stdout.decode()
+    assert r.returncode == 0, (out[-2000:], r.stderr.decode()[-4000:])
+    line = json.loads([ln for ln in out.splitlines() if ln.startswith("{")][-1])
+    cg = line["overhead"]["c_group"]
+    print("\n" + json.dumps(cg))
+    assert cg["step"] == "hip graph" and cg["symbol_errors"] == 0
+    assert 0.8 <= cg["ratio_to_torch_path"] <= 1.25, cg
+
+
 def test_config5_rank_shard_world1():
     """One rank's shard of the 8-GPU configs[4] run (128 of the 1024 streams)
     through the same graph step at world size 1: the streams_shard entry and

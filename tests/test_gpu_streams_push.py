@@ -237,3 +237,60 @@ def test_mapped_staging_variant(A, O, torch, channels, hop, n_streams):
     results as per-stream handles, bit for bit."""
     streams_vs_single(A, O, n_streams, A.FSK2_FREQS, hop, channels=channels, rounds=6,
                       seed=91 + hop + channels, mapped=True)
+
+
+def test_group_push_and_bucket_world1(A):
+    """demod_group (the C ABI's RCCL group) at world 1 on
+    the box: pushes equal demod_streams_push symbol for symbol (stereo,
+    lead-in, ragged packets), both as one rank of a multi-process group and
+    as a one-device local group; the device bucket's gathered frames equal
+    demod_frame_streams_async of the same symbols byte for byte."""
+    import numpy as np
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU visible")
+    S = 7
+    cfg = A.make_cfg(channels=2, channel_mode=A.CH_DOWNMIX, lead_in=312)
+    rng = np.random.default_rng(5)
+    ms = A.Streams(S, cfg)
+    with A.Group(cfg, S) as g, A.Group(cfg, S, devices=[0]) as gl:
+        assert g.world == 1 and gl.world == 1 and g.shard(0) == (0, 0, S)
+        for rnd in range(5):
+            packets = [rng.integers(-20000, 20000, 2 * (2880 - 131 * s - 17 * rnd)).astype(np.int16)
+                       for s in range(S)]
+            per = ms.push(packets)
+            sa = np.concatenate(per)
+            ca = np.array([len(p) for p in per], np.uint32)
+            sb, cb = g.push(packets)
+            sc, cc = gl.push(packets)
+            assert np.array_equal(ca, cb) and np.array_equal(ca, cc)
+            assert np.array_equal(sa, sb) and np.array_equal(sa, sc)
+    ms.close()
+    # the bucket: 16 steps, ring 4, 3 streams x 64 windows, vs the torch path's framing
+    cfg1 = A.make_cfg()
+    S, wps, steps, ring = 3, 64, 16, 4
+    dev = torch.device("cuda", 0)
+    d_pcm = torch.empty((S * wps, 1024), dtype=torch.int16, device=dev)
+    tru = torch.empty(S * wps, dtype=torch.uint8, device=dev)
+    A.synth_fsk(cfg1, A.BENCH_SEED, S * wps, 8000, 400, d_pcm, tru)
+    ringbuf = torch.stack([d_pcm] * ring).contiguous()
+    bits = A.bits_per_symbol(2)
+    with A.Group(cfg1, S) as g:
+        block = A.group_block_bytes(S, 1, steps, wps, bits)
+        d_all = torch.zeros(block, dtype=torch.uint8, device=dev)
+        got = g.bucket_async([ringbuf], ring, wps, steps, [d_all],
+                             [torch.cuda.current_stream().cuda_stream])
+        torch.cuda.synchronize()
+        assert got == block
+    with A.Demodulator(cfg1) as d:
+        sym = torch.empty(S * wps, dtype=torch.uint8, device=dev)
+        d.batch_async(d_pcm, S * wps, sym, None)
+        stride = A.frame_symbols_size(wps, bits)
+        fr = torch.empty(S * stride, dtype=torch.uint8, device=dev)
+        A.frame_streams_async(sym, S, wps, bits, fr)
+        torch.cuda.synchronize()
+    one = fr.cpu().numpy()
+    allf = d_all.cpu().numpy()
+    for s in range(steps):
+        assert np.array_equal(allf[s * S * stride:(s + 1) * S * stride], one), s
+    assert (sym == tru).all()

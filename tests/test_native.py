@@ -51,3 +51,27 @@ def test_wire_codecs_under_sanitizers(seed):
                        capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "fuzz_wire OK" in r.stdout
+
+
+def test_group_shard_and_padding_arithmetic():
+    """The multi-GPU group's shard and padding arithmetic through the C ABI
+    (tests/native/group_arith.c): shards contiguous,
+    balanced and covering every stream once; a bucket's gathered block holds
+    every rank's frames; bad arguments refused. No device needed."""
+    _make("group_arith")
+    r = subprocess.run([os.path.join(NATIVE, "group_arith")], capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "group arithmetic OK" in r.stdout
+
+
+@pytest.mark.gpu
+def test_group_world1_push_equals_streams_push_native():
+    """The same C program on the GPU: a world-1 RCCL group's pushes equal
+    demod_streams_push byte for byte (stereo-free mono, lead-in, ragged
+    packets, a too-small buffer refused before anything is consumed)."""
+    _make("group_arith")
+    r = subprocess.run([os.path.join(NATIVE, "group_arith")], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "gpu demod_group_push: world 1 equals demod_streams_push" in r.stdout
