@@ -471,6 +471,10 @@ static int enqueue_rescue(demod_t *st, const int16_t *d_pcm, size_t n_windows, u
     r.sym_aligned4 = ((uintptr_t)d_sym & 3) == 0;
     r.mag = d_mag;
     for (uint32_t k = 0; k < st->cfg.k; ++k) r.coef[k] = st->rcoef[k];
+    // n = 1024: the segment-shared windows' rescue takes the first pass too
+    // (the in-kernel rescue's tables and threshold, error_model.cpp)
+    r.rot64 = st->d_rot64;
+    r.t2e64 = st->d_rot64 ? st->t2e64 : 0.0;
     HIP_TRY(launch_rescue(r, s));
     return DEMOD_OK;
 }

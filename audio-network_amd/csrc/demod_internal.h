@@ -216,6 +216,29 @@ __device__ __forceinline__ float row_sum16(float v)
     return v;
 }
 
+// The same tree in double (the rescue's pass 0): each stage's partner by DPP
+// (two 32-bit moves) instead of __shfl_xor's ds_bpermute round trips through
+// the LDS crossbar. Bit-identical to the xor butterfly: after each stage the
+// lanes of a group hold one value (a + b == b + a), so any lane of the
+// partner group is the partner.
+template <int C>
+__device__ __forceinline__ double dpp_d(double v)
+{
+    const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_mov_dpp((int)(unsigned)b, C, 0xF, 0xF, true);
+    const unsigned hi = (unsigned)__builtin_amdgcn_mov_dpp((int)(unsigned)(b >> 32), C, 0xF, 0xF, true);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+__device__ __forceinline__ double row_sum16d(double v)
+{
+    v += dpp_d<0xB1>(v);
+    v += dpp_d<0x4E>(v);
+    v += dpp_d<0x141>(v);
+    v += dpp_d<0x140>(v);
+    return v;
+}
+
 // Output store; NTS = non-temporal (streamed once, never re-read by the kernel).
 template <bool NTS, typename T>
 __device__ __forceinline__ void out_store(T *ptr, T v)
@@ -330,11 +353,8 @@ __device__ __forceinline__ void rescue_rows(const GoertzelParams &p, long long w
                 const double2 B = *reinterpret_cast<const double2 *>(p.rot64 + ro + 2);
                 re = re - B.x * s2;
                 im = im - B.y * s2;
-#pragma unroll
-                for (int m = 1; m < 16; m <<= 1) {
-                    re += __shfl_xor(re, m);
-                    im += __shfl_xor(im, m);
-                }
+                re = row_sum16d(re);
+                im = row_sum16d(im);
                 const double pk = re * re + im * im;
                 if (pk > best) {
                     second = best;
@@ -419,6 +439,10 @@ struct RescueParams {
     int sym_aligned4;        // sym is 4-byte aligned: dword scans
     float *mag;              // [n_windows][k] or nullptr
     double coef[kMaxTones];  // Goertzel: 2 cos(2 pi f_k / fs), the caller's tone order
+    // n = 1024 (round 5): the first pass by segments (rescue_rows pass 0's
+    // arithmetic and tables) before the exact chains; t2e64 = 0: exact only
+    const double *rot64;
+    double t2e64;
 };
 hipError_t launch_rescue(const RescueParams &p, hipStream_t s);
 

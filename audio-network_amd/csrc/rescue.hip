@@ -153,6 +153,304 @@ __global__ __launch_bounds__(64) void rescue_kernel(RescueParams p)
     }
 }
 
+// n = 1024 with the first pass (round 5): the rescue of
+// segment-shared windows (SLIDE, fold-slide), which every window of a stream
+// of near ties reaches. rescue_kernel stages each group of 64 / K windows in
+// 32 KiB of LDS for K lanes per window's exact chains: one wave per SIMD and
+// 1 024 dependent double steps per lane (6.1 ms for 4.19 M windows of two
+// equal tones at hop 256, 12x the detector). Here the flagged windows take
+// rescue_rows' pass 0 (demod_internal.h): every tone's double recurrence over
+// each of the window's 16 segments of 64 samples, rotated into the window's
+// phase (rot64), summed over the segments by xor butterfly in a 16-lane row;
+// where the top-2 margin clears t2e64 E P_max (the derived bound,
+// error_model.cpp) the window is decided (symbol, powers rounded to fp32).
+// A segment's recurrence starts from zero at the segment, so at hop = 64 H
+// (H < 16) the windows of a run share their segments' end states bit for bit:
+//  dense runs: R consecutive windows holding enough flagged ones run each of
+//    their (R - 1) H + 16 segments' chains once (lane per segment and tone
+//    pair, 128 contiguous bytes per lane), the end states and fp32 sums x^2
+//    go to LDS, and each flagged window's row rotates and sums its 16 (at
+//    hop 256: a quarter of the chains);
+//  sparse windows: the row runs its window's 16 segments itself;
+//  pass 1: the windows pass 0 leaves (exact ties) take the exact chain, lane
+//    f K + t on tone t of window f, its 1 024 samples read from L2 directly:
+//    every rounding step of oracle/fsk_oracle.c, bit-identical powers and
+//    symbol.
+constexpr int kSegStates = 512;  // LDS end states per dense run: segments x K
+
+// Tones c0, c1's recurrences over one segment's 64 samples (8 chunks of 8),
+// from zero: rescue_rows' pass-0 arithmetic, operation for operation.
+// v is made opaque first: the extractions are not shared with an earlier use
+// (seg_energy64's were kept live, 64 VGPRs, for these).
+__device__ __forceinline__ void seg_pair(u32x4q (&v)[8], double c0, double c1, double &a1,
+                                         double &a2, double &b1, double &b2)
+{
+#pragma clang fp contract(off)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) asm volatile("" : "+v"(v[q]));
+    a1 = a2 = b1 = b2 = 0.0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const unsigned d4[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const double x = (double)(short)((d4[i >> 1] >> (16 * (i & 1))) & 0xFFFFu);
+            double sa = x + c0 * a1;
+            sa = sa - a2;
+            a2 = a1;
+            a1 = sa;
+            double sb = x + c1 * b1;
+            sb = sb - b2;
+            b2 = b1;
+            b1 = sb;
+        }
+        // a chunk's conversions stay with its steps (scheduled early, the 64
+        // doubles took 128 VGPRs)
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+__device__ __forceinline__ float seg_energy64(const u32x4q (&v)[8])
+{
+    float e = 0.f;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const unsigned d4[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const float xf = (float)(short)((d4[i >> 1] >> (16 * (i & 1))) & 0xFFFFu);
+            e = __builtin_fmaf(xf, xf, e);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    return e;
+}
+
+__device__ __forceinline__ void wave_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Row (16 lanes) decision of window w from its lane's segment state per tone
+// (st(t) -> {s1, s2}) and the lane's fp32 sum x^2 e: rescue_rows' pass-0
+// rotation, butterfly, argmax and margin test. Returns "still ambiguous";
+// decided live rows write their symbol and powers.
+template <typename St>
+__device__ __forceinline__ bool seg_decide(const RescueParams &p, long long w, bool live, int seg,
+                                           float e, St st)
+{
+#pragma clang fp contract(off)
+    const int K = p.k;
+    double best = -1.0, second = -1.0, mine = 0.0;
+    int arg = 0;
+#pragma unroll 1
+    for (int t = 0; t < K; ++t) {
+        const double2 s = st(t);
+        const double *r = p.rot64 + 4 * (t * 16 + seg);
+        double re = r[0] * s.x, im = r[1] * s.x;
+        re = re - r[2] * s.y;
+        im = im - r[3] * s.y;
+        re = row_sum16d(re);
+        im = row_sum16d(im);
+        const double pk = re * re + im * im;
+        if (pk > best) {
+            second = best;
+            best = pk;
+            arg = t;
+        } else if (pk > second) {
+            second = pk;
+        }
+        if (t == seg) mine = pk;
+    }
+    const double cth = p.t2e64 * (double)row_sum16(e), dm = best - second;
+    const bool still = !(best > 0.0) || dm * dm < cth * best || 16.0 * best < cth;
+    if (live && !still) {
+        if (seg == 0) p.sym[w] = (uint8_t)arg;
+        if (p.mag && seg < K) p.mag[w * K + seg] = (float)mine;
+    }
+    return still;
+}
+
+__global__ __launch_bounds__(64) void rescue_seg_kernel(RescueParams p)
+{
+#pragma clang fp contract(off)
+    __shared__ unsigned short idx[kRescueChunk];   // flagged windows (chunk offsets), in order
+    __shared__ unsigned short left[kRescueChunk];  // pass 1's list
+    __shared__ double2 sst[kSegStates];            // dense run: [segment][tone] {s1, s2}
+    __shared__ float sen[kSegStates / 2];          // dense run: [segment] fp32 sum x^2
+    const int lane = threadIdx.x;
+    const long long base = tile_block(1) * kRescueChunk;
+    const int span = (int)min((long long)kRescueChunk, p.n_windows - base);
+    __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void *)(p.sym + base), (short)0, span, 0x00020000);
+    unsigned any = 0;
+    if (p.sym_aligned4) {
+#pragma unroll
+        for (int c = 0; c < kRescueChunk / 256; ++c)
+            any |= __builtin_amdgcn_raw_buffer_load_b32(rs, (64 * c + lane) * 4, 0, 0) & 0x80808080u;
+        if (lane < (span & 3)) any |= __builtin_amdgcn_raw_buffer_load_b8(rs, (span & ~3) + lane, 0, 0) & 0x80u;
+    } else {
+        for (int c = 0; c < kRescueChunk / 64; ++c)
+            any |= __builtin_amdgcn_raw_buffer_load_b8(rs, 64 * c + lane, 0, 0) & 0x80u;
+    }
+    if (__ballot(any != 0) == 0) return;
+    int T = 0;
+    for (int i = 0; i < kRescueChunk / 64; ++i) {
+        const int o = 64 * i + lane;
+        const bool f = o < span && (p.sym[base + o] & kSymAmbiguous);
+        const unsigned long long b = __ballot(f);
+        if (f) idx[T + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(b >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)b, 0u))] =
+            (unsigned short)o;
+        T += __popcll(b);
+    }
+    wave_sync();
+    const int K = p.k;
+    const int row = lane >> 4, seg = lane & 15;
+    int Tl = 0;  // left[0 .. Tl)
+
+    // dense runs (hop = 64 H, H < 16): runs of R windows, ((R - 1) H + 16) K
+    // end states in LDS
+    const int H = (p.hop % 64 == 0 && p.hop < 1024) ? (int)(p.hop / 64) : 0;
+    int Ts = T;  // windows for the per-window pass: idx[0 .. Ts)
+    if (H > 0) {
+        int R = 64;
+        while (R > 1 && ((R - 1) * H + 16) * K > kSegStates) R >>= 1;
+        const int pairs = (K + 1) >> 1;
+        Ts = 0;
+        int i = 0;
+#pragma unroll 1
+        while (i < T) {
+            const int rb = (idx[i] / R) * R;
+            const int my = i + lane < T ? (int)idx[i + lane] : kRescueChunk;
+            const int cnt = __popcll(__ballot(lane < R && my < rb + R));
+            const int nw = min(R, span - rb);
+            const int segs = (nw - 1) * H + 16;
+            if (cnt * 16 <= segs) {
+                // sparse: to the per-window pass (Ts <= i: the read is done
+                // before the write)
+                if (lane < cnt) idx[Ts + lane] = (unsigned short)my;
+                Ts += cnt;
+                i += cnt;
+                wave_sync();
+                continue;
+            }
+            const int16_t *s0 = p.pcm + (base + rb) * p.hop;
+#pragma unroll 1
+            for (int it = lane; it < segs * pairs; it += 64) {
+                const int pp = it / segs, s = it - pp * segs;
+                const u32x4q *src = reinterpret_cast<const u32x4q *>(s0 + 64 * s);
+                u32x4q v[8];
+#pragma unroll
+                for (int q = 0; q < 8; ++q) v[q] = src[q];
+                if (pp == 0) sen[s] = seg_energy64(v);
+                const int t0 = 2 * pp, t1 = t0 + 1 < K ? t0 + 1 : t0;
+                double a1, a2, b1, b2;
+                seg_pair(v, p.rot64[64 * K + t0], p.rot64[64 * K + t1], a1, a2, b1, b2);
+                // unconditional (t1 == t0: the same bits twice); under the
+                // condition the compiler ran b's chain after a's, the 64
+                // converted samples live in between
+                sst[s * K + t0] = make_double2(a1, a2);
+                sst[s * K + t1] = make_double2(b1, b2);
+            }
+            wave_sync();
+#pragma unroll 1
+            for (int j = 0; j < cnt; j += 4) {
+                const bool live = j + row < cnt;
+                const int o = idx[i + (live ? j + row : j)];
+                const int sb = (o - rb) * H + seg;
+                const bool still = seg_decide(p, base + o, live, seg, sen[sb],
+                                              [&](int t) { return sst[sb * K + t]; });
+                const unsigned long long lb = __ballot(live && still && seg == 0);
+                if (live && still && seg == 0) left[Tl + __popcll(lb & ((1ull << lane) - 1))] = (unsigned short)o;
+                Tl += __popcll(lb);
+            }
+            i += cnt;
+            wave_sync();
+        }
+    }
+
+    // per-window pass: rows of 16 lanes, one window each, its segments' chains
+    // run by the row
+#pragma unroll 1
+    for (int g0 = 0; g0 < Ts; g0 += 4) {
+        const bool live = g0 + row < Ts;
+        const int o = idx[live ? g0 + row : g0];
+        const long long w = base + o;
+        const u32x4q *src = reinterpret_cast<const u32x4q *>(p.pcm + w * p.hop + 64 * seg);
+        u32x4q v[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = src[q];
+        const float e = seg_energy64(v);
+        double2 sp[2];
+        bool still;
+        if (K <= 2) {
+            seg_pair(v, p.rot64[64 * K], p.rot64[64 * K + K - 1], sp[0].x, sp[0].y, sp[1].x, sp[1].y);
+            still = seg_decide(p, w, live, seg, e, [&](int t) { return t ? sp[1] : sp[0]; });
+        } else {
+            // K > 2: each tone's chain where seg_decide asks for it (one pass
+            // over the samples per tone; v opaque per pass so its conversions
+            // are not hoisted out of the tone loop as 64 doubles)
+            still = seg_decide(p, w, live, seg, e, [&](int t) {
+                const double c = p.rot64[64 * K + t];
+                double2 r, u;
+                seg_pair(v, c, c, r.x, r.y, u.x, u.y);
+                return r;
+            });
+        }
+        const unsigned long long lb = __ballot(live && still && seg == 0);
+        if (live && still && seg == 0) left[Tl + __popcll(lb & ((1ull << lane) - 1))] = (unsigned short)o;
+        Tl += __popcll(lb);
+    }
+    wave_sync();
+
+    // pass 1: the exact chains of what is left, straight from L2
+    const int wpw = 64 / K;
+    const int f = lane / K, t = lane - (lane / K) * K;
+#pragma unroll 1
+    for (int g0 = 0; g0 < Tl; g0 += wpw) {
+        const bool act = f < wpw && g0 + f < Tl;
+        const long long w = base + left[act ? g0 + f : g0];
+        double P = 0.0;
+        if (act) {
+            const double c = p.coef[t];
+            double s1 = 0.0, s2 = 0.0;
+            const u32x4q *xs = reinterpret_cast<const u32x4q *>(p.pcm + w * p.hop);
+            u32x4q nx = xs[0];
+#pragma unroll 1
+            for (int q = 0; q < 128; ++q) {
+                const u32x4q d = nx;
+                if (q + 1 < 128) nx = xs[q + 1];
+                const unsigned d4[4] = {d.x, d.y, d.z, d.w};
+#pragma unroll
+                for (int e2 = 0; e2 < 8; ++e2) {
+                    const double x = (double)(short)((d4[e2 >> 1] >> (16 * (e2 & 1))) & 0xFFFFu);
+                    double s = x + c * s1;
+                    s = s - s2;
+                    s2 = s1;
+                    s1 = s;
+                }
+            }
+            const double a = s1 * s1 + s2 * s2;
+            const double b = c * s1;
+            P = a - b * s2;
+            if (p.mag) p.mag[w * K + t] = (float)P;
+        }
+        // the window's argmax across its K lanes (ties to the lowest tone)
+        double bestx = -1.0;
+        int argx = 0;
+        for (int k = 0; k < K; ++k) {
+            const double pk = __shfl(P, (f * K + k) & 63);
+            if (pk > bestx) {
+                bestx = pk;
+                argx = k;
+            }
+        }
+        if (act && t == 0) p.sym[w] = (uint8_t)argx;
+    }
+}
+
 hipError_t launch_rescue(const RescueParams &p, hipStream_t s)
 {
     if (p.n_windows <= 0) return hipSuccess;
@@ -160,7 +458,10 @@ hipError_t launch_rescue(const RescueParams &p, hipStream_t s)
     if (p.n < 64 || (p.n % 8) || 2 * p.n + 16 > kRescueLdsBytes) return hipErrorInvalidValue;
     const long long blocks = (p.n_windows + kRescueChunk - 1) / kRescueChunk;
     if (blocks > 0x7FFFFFFFLL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(rescue_kernel, dim3((unsigned)blocks), dim3(64), 0, s, p);
+    if (p.n == 1024 && p.rot64 && p.t2e64 > 0.0)
+        hipLaunchKernelGGL(rescue_seg_kernel, dim3((unsigned)blocks), dim3(64), 0, s, p);
+    else
+        hipLaunchKernelGGL(rescue_kernel, dim3((unsigned)blocks), dim3(64), 0, s, p);
     return hipGetLastError();
 }
 

@@ -227,11 +227,8 @@ __device__ __forceinline__ bool rescue_fft_seg(const int16_t *__restrict__ x, co
         double re = r[0] * s1, im = r[1] * s1;
         re = re - r[2] * s2;
         im = im - r[3] * s2;
-#pragma unroll
-        for (int m = 1; m < 16; m <<= 1) {
-            re += __shfl_xor(re, m);
-            im += __shfl_xor(im, m);
-        }
+        re = row_sum16d(re);
+        im = row_sum16d(im);
         const double pk = re * re + im * im;
         if (pk > best) {
             second = best;
