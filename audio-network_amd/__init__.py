@@ -128,6 +128,7 @@ class DemodPlanInfo(ctypes.Structure):
         ("rcoef", ctypes.c_double * DEMOD_MAX_TONES),
         ("rot_len", ctypes.c_uint32),
         ("rot64_len", ctypes.c_uint32),
+        ("fold64", ctypes.c_int32),
     ]
 
 

@@ -62,6 +62,7 @@ struct demod {
     bool reinsch = false;       // plain detector: Reinsch-modified recurrence
     int dcls = 0;               // residue detector: compile-time class pattern (residue.hip DC), slots permuted
     bool f16 = false;           // fold detector: fold by 16, slots permuted (Z0 tones, Z8 tones)
+    bool fold64 = false;        // the rescue's pass 0 by the fold (plan.h)
     unsigned long long perm = 0;  // DCLS: nibble s = tone index of kernel slot s
     int zcls[kMaxTones] = {};   // residue detector: class each tone reads
     // staging for host-pointer calls
@@ -215,6 +216,7 @@ static int init_device_state(demod_t *st)
     // the tone plan's fp32 constants (error_model.cpp build_plan)
     st->reinsch = pl.reinsch;
     st->f16 = pl.f16;
+    st->fold64 = pl.fold64;
     st->dcls = pl.dcls;
     st->perm = pl.perm;
     for (uint32_t k = 0; k < c.k; ++k) {
@@ -475,6 +477,7 @@ static int enqueue_rescue(demod_t *st, const int16_t *d_pcm, size_t n_windows, u
     // (the in-kernel rescue's tables and threshold, error_model.cpp)
     r.rot64 = st->d_rot64;
     r.t2e64 = st->d_rot64 ? st->t2e64 : 0.0;
+    r.fold64 = st->fold64;
     HIP_TRY(launch_rescue(r, s));
     return DEMOD_OK;
 }
@@ -515,6 +518,7 @@ static int enqueue_fft(demod_t *st, const int16_t *d_pcm, size_t n_windows, uint
     // flagged window takes the double FFT, whose spectrum row is the oracle's)
     p.rot64 = st->d_rot64;
     p.t2e64 = st->t2e64;
+    p.fold64 = st->fold64 ? 1 : 0;
     HIP_TRY(launch_fft_quad(p, s));
     return (int)n_windows;
 }

@@ -18,7 +18,10 @@ constexpr int kLdsSegStride = 144;    // bytes: 128 B segment + 16 B pad (confli
 constexpr int kLdsWaveBytes = 64 * kLdsSegStride;
 constexpr int kMaxTones = 16;
 constexpr int kFoldSlideSegs = 80;    // fold.hip fold_slide_kernel: segments per tile (10 KiB)
-constexpr int kMaxDevices = 64;       // device ordinals the module tables cover
+constexpr int kMaxDevices = 64;
+// the rescue's pass 0 by the fold (plan.h fold64) for fold plans up to this K
+// (above, its code cost the fold kernels an occupancy step: K = 14, 4 -> 3)
+constexpr int kFold64MaxK = 12;       // device ordinals the module tables cover
 
 // Uniform per-launch parameters (kernarg -> SGPRs).
 struct GoertzelParams {
@@ -54,7 +57,9 @@ struct GoertzelParams {
     int rescue_inline;
     double rcoef[kMaxTones];
     // rescue_rows' tables: rot64 = [k][16][4] {Ar, Ai, Br, Bi} in double (the
-    // caller's tone order), then rcoef[k] again (read with a per-lane index);
+    // caller's tone order), pass 0's chain coefficients c[k] (= rcoef[k]
+    // except by the fold, plan.h fold64), then rcoef[k] again (the exact
+    // chains', read with a per-lane index);
     // pass 0 leaves a row to the exact chain when margin^2 < t2e64 E P_max;
     // t2e64 = 0: every flagged row takes the exact chain
     const double *rot64;
@@ -187,7 +192,26 @@ __device__ __forceinline__ float seg_energy(Chunk chunk)
     return (a.x + a.y) + (b.x + b.y);
 }
 
-// The same sum one chunk at a time (4 VGPRs of samples live instead of 32:
+// seg_energy's arithmetic, bit for bit, U chunks in flight at a time
+template <int U, typename Chunk>
+__device__ __forceinline__ float seg_energy_lowreg(Chunk chunk)
+{
+    f32x2e a = {0.f, 0.f}, b = {0.f, 0.f};
+#pragma unroll U
+    for (int i = 0; i < 8; ++i) {
+        const u32x4e d = chunk(i);
+        const unsigned d4[4] = {d.x, d.y, d.z, d.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const f32x2e x = {(float)(int)(short)(d4[q] & 0xFFFFu), (float)((int)d4[q] >> 16)};
+            if (q & 1) b = __builtin_elementwise_fma(x, x, b);
+            else a = __builtin_elementwise_fma(x, x, a);
+        }
+    }
+    return (a.x + a.y) + (b.x + b.y);
+}
+
+// A serial sum one chunk at a time (4 VGPRs of samples live instead of 32:
 // for rare paths inside kernels at their VGPR limit)
 template <typename Chunk>
 __device__ __forceinline__ float seg_energy_serial(Chunk chunk)
@@ -297,13 +321,95 @@ __device__ __forceinline__ long long tile_block(int swz)
 // Every lane of the wave calls it (the shuffles); rows with amb_row false
 // change nothing. The detector leaves the symbol and magnitudes of a flagged
 // row to this function (no second store).
+// Pass 0 by the fold (FOLD: fold detector plans, every tone on a multiple of
+// 8 bins; round 5): lane seg sums the window's samples
+// 128 m + 8 seg + i over m < 8 (exact integers: the folded samples 8 seg ..
+// 8 seg + 7 of the window folded to 128), then per tone an 8-step double
+// chain at the exact bin, the rotation (rot64: the fold tables, plan.h
+// fold64), the row sum and the power; the margin test as pass 0 above (t2e64
+// derived for this sequence, error_model.cpp first_pass_fold_rho). 8x fewer
+// double steps than 64 raw samples per lane per tone. Returns amb_row after
+// it (the rows left to the exact chains).
 template <int K, typename Chunk>
+__device__ __forceinline__ bool rescue_rows_fold0(const GoertzelParams &p, long long w, int seg,
+                                                  bool amb_row, Chunk chunk)
+{
+#pragma clang fp contract(off)
+    // opaque here: no address built from seg is hoisted into the detector's
+    // loop (where it would hold VGPRs across every tile)
+    asm volatile("" : "+v"(seg));
+    int xf[8];
+    float e = 0.f;  // the lane's 64 raw samples' sum x^2 (any partition of the window)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) xf[i] = 0;
+#pragma unroll 1
+    for (int m = 0; m < 8; ++m) {
+        const u32x4e d = chunk(16 * m + seg);
+        const unsigned d4[4] = {d.x, d.y, d.z, d.w};
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int v = (int)(short)((d4[i >> 1] >> (16 * (i & 1))) & 0xFFFFu);
+            xf[i] += v;
+            const float xv = (float)v;
+            e = __builtin_fmaf(xv, xv, e);
+        }
+    }
+    double best = -1.0, second = -1.0;
+    int arg = 0;
+#pragma unroll 1
+    for (int k = 0; k < K; ++k) {
+        int ci = 64 * K + k;
+        asm volatile("" : "+v"(ci));  // a vector load (as scalar, SGPR spills at large K)
+        const double c = p.rot64[ci];
+        double s1 = 0.0, s2 = 0.0;
+        // each sample converted at its step (scheduled together, the 8
+        // doubles raised the fold kernels' VGPR peak)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            double s = (double)xf[i] + c * s1;
+            s = s - s2;
+            s2 = s1;
+            s1 = s;
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        const double2 A = *reinterpret_cast<const double2 *>(p.rot64 + 4 * (k * 16 + seg));
+        const double2 B = *reinterpret_cast<const double2 *>(p.rot64 + 4 * (k * 16 + seg) + 2);
+        double re = A.x * s1, im = A.y * s1;
+        re = re - B.x * s2;
+        im = im - B.y * s2;
+        re = row_sum16d(re);
+        im = row_sum16d(im);
+        const double pk = re * re + im * im;
+        if (pk > best) {
+            second = best;
+            best = pk;
+            arg = k;
+        } else if (pk > second) {
+            second = pk;
+        }
+        if (k == seg && amb_row && p.mag) p.mag[w * K + seg] = (float)pk;
+    }
+    const double cth = p.t2e64 * (double)row_sum16(e), dm = best - second;
+    const bool still = !(best > 0.0) || dm * dm < cth * best || 16.0 * best < cth;
+    if (amb_row && !still && seg == 0) p.sym[w] = (uint8_t)arg;
+    return amb_row && still;
+}
+
+template <int K, bool FOLD = false, typename Chunk>
 __device__ __forceinline__ void rescue_rows(const GoertzelParams &p, long long w, int seg, int lane,
                                             bool amb_row, Chunk chunk)
 {
 #pragma clang fp contract(off)
+    int first = p.t2e64 > 0.0 ? 0 : 1;
+    if constexpr (FOLD) {
+        if (first == 0) {
+            amb_row = rescue_rows_fold0<K>(p, w, seg, amb_row, chunk);
+            if (__ballot(amb_row) == 0) return;
+            first = 1;
+        }
+    }
 #pragma unroll 1
-    for (int pass = p.t2e64 > 0.0 ? 0 : 1; pass < 2; ++pass) {
+    for (int pass = first; pass < 2; ++pass) {
         const bool exact = pass == 1;
         const bool run = exact ? amb_row && seg < K : true;  // lanes that run chains
         const int q0 = exact ? 0 : 8 * seg, q1 = exact ? 128 : 8 * seg + 8;
@@ -313,7 +419,8 @@ __device__ __forceinline__ void rescue_rows(const GoertzelParams &p, long long w
 #pragma unroll 1
         for (int t = 0; t < (exact ? 1 : K); ++t) {
             const int k = exact ? seg : t;
-            const double c = p.rot64[64 * K + (k < K ? k : 0)];  // rcoef[k], read per lane
+            // pass 0's coefficient, or the oracle's rcoef[k] (exact), per lane
+            const double c = p.rot64[(exact ? 65 : 64) * K + (k < K ? k : 0)];
             double s1 = 0.0, s2 = 0.0;
             if (run) {
 #pragma unroll 1
@@ -426,6 +533,7 @@ struct FftParams {
     // window takes the double FFT
     const double *rot64;
     double t2e64;
+    int fold64;              // rot64 by the fold (plan.h; every tone bin a multiple of 8)
 };
 
 // rescue.hip: re-decides every window whose symbol carries kSymAmbiguous.
@@ -440,9 +548,11 @@ struct RescueParams {
     float *mag;              // [n_windows][k] or nullptr
     double coef[kMaxTones];  // Goertzel: 2 cos(2 pi f_k / fs), the caller's tone order
     // n = 1024 (round 5): the first pass by segments (rescue_rows pass 0's
-    // arithmetic and tables) before the exact chains; t2e64 = 0: exact only
+    // arithmetic and tables) before the exact chains; t2e64 = 0: exact only;
+    // fold64: by the fold (rescue_rows_fold0's arithmetic, plan.h)
     const double *rot64;
     double t2e64;
+    int fold64;
 };
 hipError_t launch_rescue(const RescueParams &p, hipStream_t s);
 

@@ -259,15 +259,26 @@ void build_plan(const demod_cfg_t &c, Plan &pl)
     // double and in the caller's tone order, then the chains' coefficients
     // (the FFT detector: at its tone bins' frequencies b fs / n, with 2 cos
     // (2 pi b / n), for its own first pass, rescue_fft_seg)
+    // Fold detector plans (every tone on a multiple of 8 bins) run it by the
+    // fold (Plan::fold64): lane j over folded samples 8j .. 8j + 7 at the
+    // exact bin (8x fewer double steps than 64 raw samples per lane per tone).
     if (c.n == 1024 && c.k >= 2) {
         const bool fft = pl.detector == kDetFft;
-        pl.rot64.assign((size_t)c.k * 16 * 4 + c.k, 0.0);
+        pl.fold64 = c.k <= (uint32_t)kFold64MaxK && (pl.detector == kDetFolded || fft);
+        for (uint32_t k = 0; fft && k < c.k; ++k)
+            if (pl.fft_bins[k] % 8) pl.fold64 = false;
+        const double span = pl.fold64 ? 8.0 : 64.0;
+        // [k][16][4], pass 0's chain coefficients c[k], then the oracle's
+        // rcoef[k] (the exact chains' coefficients)
+        pl.rot64.assign((size_t)c.k * 16 * 4 + 2 * c.k, 0.0);
         for (uint32_t k = 0; k < c.k; ++k) {
-            pl.rot64[(size_t)c.k * 64 + k] =
-                fft ? 2.0 * std::cos(2.0 * M_PI * pl.fft_bins[k] / (double)c.n) : pl.rcoef[k];
-            const double w = fft ? 2.0 * M_PI * pl.fft_bins[k] / (double)c.n : 2.0 * M_PI * c.freqs[k] / c.fs;
+            const double w = fft          ? 2.0 * M_PI * pl.fft_bins[k] / (double)c.n
+                             : pl.fold64 ? 2.0 * M_PI * (double)integer_bin(c, k) / (double)c.n
+                                         : 2.0 * M_PI * c.freqs[k] / c.fs;
+            pl.rot64[(size_t)c.k * 64 + k] = (fft || pl.fold64) ? 2.0 * std::cos(w) : pl.rcoef[k];
+            pl.rot64[(size_t)c.k * 65 + k] = pl.rcoef[k];
             for (int j = 0; j < 16; ++j) {
-                const double a = -w * (64.0 * j + 63.0), b = -w * (64.0 * j + 64.0);
+                const double a = -w * (span * j + span - 1.0), b = -w * (span * j + span);
                 double *o = &pl.rot64[((size_t)k * 16 + j) * 4];
                 o[0] = std::cos(a);
                 o[1] = std::sin(a);
@@ -804,6 +815,30 @@ ld first_pass_rho(const Plan &pl, uint32_t K, uint32_t k, ld w_ref)
     return acc.finish(w_ref, 4, kU64);
 }
 
+// pass 0 by the fold (Plan::fold64) for tone k at its exact bin w_b, per
+// ||xf|| (xf the window folded to 128 samples, exact; ||xf|| <= sqrt 8 ||x||):
+// lane j's 8-step double chain over xf[8j .. 8j + 7], its rotation, the
+// 16-lane tree, the power
+ld first_pass_fold_rho(const Plan &pl, uint32_t K, uint32_t k, ld w_b)
+{
+    const double *r64 = pl.rot64.data();
+    const ld cc = r64[(size_t)K * 64 + k];
+    Lane L(8);
+    std::vector<int> x(8);
+    for (int i = 0; i < 8; ++i) x[i] = i;
+    int s1, s2;
+    chain_double(L, x, cc, s1, s2);
+    const Core core = analyze_core(L, {s1, s2});
+    WindowAcc acc(128);
+    std::vector<int> pos(8);
+    for (int j = 0; j < 16; ++j) {
+        const double *o = &r64[((size_t)k * 16 + j) * 4];
+        for (int i = 0; i < 8; ++i) pos[i] = 8 * j + i;
+        acc.add(rot_lane(core, o[0], o[1], o[2], o[3], kU64), pos);
+    }
+    return acc.finish(w_b, 4, kU64);
+}
+
 }  // namespace
 
 void error_model(const demod_cfg_t &c, const Plan &pl, bool first_pass, ErrModel &m)
@@ -872,9 +907,19 @@ void error_model(const demod_cfg_t &c, const Plan &pl, bool first_pass, ErrModel
     if (first_pass && n == 1024 && c.k >= 2 && !pl.rot64.empty()) {
         ld f = 0;
         for (uint32_t k = 0; k < c.k; ++k) {
-            const ld w = fft ? 2.0L * kPi * (ld)pl.fft_bins[k] / 1024.0L
-                             : std::acos((ld)pl.rcoef[k] / 2.0L);
-            const ld r = first_pass_rho(pl, c.k, k, w) + (fft ? fft_oracle_rho(n) : oracle_rho(pl.rcoef[k], n));
+            ld r;
+            if (pl.fold64) {
+                // pass 0 evaluates the exact bin; the Goertzel oracle its own
+                // frequency (the FFT oracle the bin)
+                const ld wb = 2.0L * kPi * (ld)(fft ? pl.fft_bins[k] : integer_bin(c, k)) / (ld)n;
+                r = std::sqrt(8.0L) * first_pass_fold_rho(pl, c.k, k, wb);
+                if (fft) r += fft_oracle_rho(n);
+                else r += freq_gap(std::acos((ld)pl.rcoef[k] / 2.0L), wb, n) + oracle_rho(pl.rcoef[k], n);
+            } else {
+                const ld w = fft ? 2.0L * kPi * (ld)pl.fft_bins[k] / 1024.0L
+                                 : std::acos((ld)pl.rcoef[k] / 2.0L);
+                r = first_pass_rho(pl, c.k, k, w) + (fft ? fft_oracle_rho(n) : oracle_rho(pl.rcoef[k], n));
+            }
             f = std::max(f, r);
         }
         m.rho_first = (double)f;
@@ -940,6 +985,7 @@ extern "C" int demod_plan_info(const demod_cfg_t *cfg, demod_plan_info_t *info, 
     }
     info->rot_len = (uint32_t)pl.rot.size();
     info->rot64_len = (uint32_t)pl.rot64.size();
+    info->fold64 = pl.fold64;
     if (rot && rot_cap >= 4 * pl.rot.size())
         std::memcpy(rot, pl.rot.data(), pl.rot.size() * sizeof(float4));
     if (rot64 && rot64_cap >= pl.rot64.size())

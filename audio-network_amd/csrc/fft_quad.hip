@@ -1245,7 +1245,7 @@ __device__ __attribute__((always_inline)) inline void fft1024_quad_body(const Ff
                         const long long ww = 4 * gs + row;
                         const bool amb = (fs >> row) & 1u;
                         (void)rescue_fft_seg(p.pcm + (amb ? ww : 0) * p.hop, p.rot64, p.t2e64, p.k, lane & 15,
-                                             amb, p.sym + ww, p.mag ? p.mag + ww * p.k : nullptr);
+                                             amb, p.sym + ww, p.mag ? p.mag + ww * p.k : nullptr, p.fold64 != 0);
                     }
                 }
                 __builtin_amdgcn_s_waitcnt(0);

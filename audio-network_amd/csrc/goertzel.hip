@@ -23,6 +23,10 @@
 // 64-sample chains keep the fp32 error <= ~3e-6 of max_k P (a single
 // 1024-sample chain reaches ~2e-5, over the 1e-5 bar).
 #include "demod_internal.h"
+
+#ifndef FSKD_SLIDE_EU
+#define FSKD_SLIDE_EU 4
+#endif
 #include "window_sum.h"
 
 namespace fskd {
@@ -97,6 +101,7 @@ __global__ __launch_bounds__(64 * WPB) void goertzel_tile_kernel(GoertzelParams 
 {
     static_assert(PF == 1 || PF == 2, "prefetch depth");
     static_assert(!SLIDE || (LOG2G == 4 && !DIRECT && PF == 1), "SLIDE: n = 1024");
+    static_assert(!SLIDE || K * 64 * 8 + 64 * 4 <= kLdsWaveBytes, "SLIDE: states + energies in the slice");
     __shared__ __attribute__((aligned(16))) unsigned char lds[DIRECT ? 16 : WPB * kLdsWaveBytes];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: tile bases stay in SGPRs (no waterfall loop per buffer load)
@@ -277,6 +282,13 @@ __global__ __launch_bounds__(64 * WPB) void goertzel_tile_kernel(GoertzelParams 
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             const int H = (int)(p.hop >> 6);
             const int wt = (int)wins_per_tile;
+            // stage 2's energies: the tile's segments' fp32 sums x^2, computed
+            // once per tile (lane = segment, re-read from L2) into LDS after
+            // the states, when a window of the tile first needs one (round 5:
+            // per window, 16 lanes re-read its 2 KiB, which at hop 256 with
+            // every window a candidate cost the detector 0.7 ms more)
+            float *le = reinterpret_cast<float *>(wl + K * 64 * sizeof(float2));
+            bool have_e = false;  // wave-uniform (efn runs on every lane)
             for (int u0 = 0; u0 < wt; u0 += 4) {
                 const int u = u0 + win_in_tile;                 // window of the tile
                 const int sg = (u < wt ? u * H : 0) + seg;      // its segment j = seg
@@ -302,11 +314,21 @@ __global__ __launch_bounds__(64 * WPB) void goertzel_tile_kernel(GoertzelParams 
                 }
                 // stage 2 of the ambiguity test: the window's energy from its
                 // segments, re-read from L2 (the samples in LDS are gone)
-                const int16_t *sp = p.pcm + tt * wins_per_tile * p.hop + 64 * sg;
                 auto efn = [&]() {
-                    return group_sum(seg_energy([&](int i) {
-                        return live ? global_chunk(sp, i) : u32x4{0u, 0u, 0u, 0u};
-                    }), 4);
+                    if (!have_e) {
+                        // the tile's segments of real windows: (nlive - 1) H + 16
+                        const long long nlive = min((long long)wt, p.n_windows - tt * wins_per_tile);
+                        const bool real = lane < (int)((nlive - 1) * H + 16);
+                        const int16_t *sp = p.pcm + tt * wins_per_tile * p.hop + 64 * lane;
+                        le[lane] = seg_energy_lowreg<FSKD_SLIDE_EU>([&](int i) {
+                            return real ? global_chunk(sp, i) : u32x4{0u, 0u, 0u, 0u};
+                        });
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                        __builtin_amdgcn_wave_barrier();
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                        have_e = true;
+                    }
+                    return group_sum(live ? le[sg] : 0.f, 4);
                 };
                 if constexpr (WS) {
                     window_sum_decide<K>(xr, xi, lane, w, live, p.sym, p.mag, 0,

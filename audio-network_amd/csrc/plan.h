@@ -30,6 +30,12 @@ struct Plan {
     int fft_bins[kMaxTones] = {};
     int fft_slot[kMaxTones] = {};
     std::vector<double> rot64;   // pass 0 tables (n = 1024, K >= 2): [k][16][4], then c[k]
+    // pass 0 by the fold (fold detector plans: every tone on a multiple of 8
+    // bins): lane j's chain runs over folded samples 8j .. 8j + 7 of the
+    // window folded to 128 (exact integer sums), rot64 = A = e^{-i w (8j + 7)},
+    // B = e^{-i w (8j + 8)} at the exact bin w = 2 pi b / n, c = 2 cos w;
+    // otherwise lane j's 64 raw samples (A = e^{-i w (64j + 63)}, ...)
+    bool fold64 = false;
 };
 
 // DEMOD_OK or the error code demod_create returns for it.

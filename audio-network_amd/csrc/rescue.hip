@@ -178,6 +178,22 @@ __global__ __launch_bounds__(64) void rescue_kernel(RescueParams p)
 //    symbol.
 constexpr int kSegStates = 512;  // LDS end states per dense run: segments x K
 
+#ifdef FSKD_BOUNDS_DEBUG
+// debug builds only (a bounds probe): report an out-of-range index and clamp it
+#define RS_CHECK(v, lim, tag)                                                                  \
+    do {                                                                                      \
+        if ((long long)(v) < 0 || (long long)(v) >= (long long)(lim)) {                       \
+            printf("RS_CHECK %s: %lld not in [0, %lld) block %d lane %d\n", tag, (long long)(v), \
+                   (long long)(lim), (int)blockIdx.x, (int)threadIdx.x);                      \
+            v = 0;                                                                            \
+        }                                                                                     \
+    } while (0)
+#else
+#define RS_CHECK(v, lim, tag) \
+    do {                      \
+    } while (0)
+#endif
+
 // Tones c0, c1's recurrences over one segment's 64 samples (8 chunks of 8),
 // from zero: rescue_rows' pass-0 arithmetic, operation for operation.
 // v is made opaque first: the extractions are not shared with an earlier use
@@ -312,21 +328,41 @@ __global__ __launch_bounds__(64) void rescue_seg_kernel(RescueParams p)
 
     // dense runs (hop = 64 H, H < 16): runs of R windows, ((R - 1) H + 16) K
     // end states in LDS
-    const int H = (p.hop % 64 == 0 && p.hop < 1024) ? (int)(p.hop / 64) : 0;
+    // (by the fold every window's pass 0 is 8 steps per lane and tone: no runs)
+    const int H = (!p.fold64 && p.hop % 64 == 0 && p.hop < 1024) ? (int)(p.hop / 64) : 0;
     int Ts = T;  // windows for the per-window pass: idx[0 .. Ts)
     if (H > 0) {
-        int R = 64;
-        while (R > 1 && ((R - 1) * H + 16) * K > kSegStates) R >>= 1;
+        // the run length with the most windows per lane pass of the segment
+        // loop (hop 256, K = 2: 61 windows, 256 segments = 4 full passes)
         const int pairs = (K + 1) >> 1;
+        int R = 1, Ri = 1;
+        for (int r = 1; r <= 64 && ((r - 1) * H + 16) * K <= kSegStates; ++r) {
+            const int it = (((r - 1) * H + 16) * pairs + 63) >> 6;
+            if (r * Ri > R * it) {
+                R = r;
+                Ri = it;
+            }
+        }
         Ts = 0;
         int i = 0;
 #pragma unroll 1
         while (i < T) {
             const int rb = (idx[i] / R) * R;
-            const int my = i + lane < T ? (int)idx[i + lane] : kRescueChunk;
+            // (past the list: a sentinel no run reaches; rb + R may pass the
+            // chunk's end when R does not divide it)
+            const int my = i + lane < T ? (int)idx[i + lane] : 0x7FFFFFFF;
             const int cnt = __popcll(__ballot(lane < R && my < rb + R));
             const int nw = min(R, span - rb);
             const int segs = (nw - 1) * H + 16;
+#ifdef FSKD_BOUNDS_DEBUG
+            {
+                int c2 = cnt, n2 = nw, t2 = T;
+                RS_CHECK(c2, 65, "cnt");
+                RS_CHECK(n2, 65, "nw");
+                RS_CHECK(t2, kRescueChunk + 1, "T");
+                if (cnt == 0) printf("RS cnt 0 at i %d T %d rb %d R %d\n", i, T, rb, R);
+            }
+#endif
             if (cnt * 16 <= segs) {
                 // sparse: to the per-window pass (Ts <= i: the read is done
                 // before the write)
@@ -339,7 +375,18 @@ __global__ __launch_bounds__(64) void rescue_seg_kernel(RescueParams p)
             const int16_t *s0 = p.pcm + (base + rb) * p.hop;
 #pragma unroll 1
             for (int it = lane; it < segs * pairs; it += 64) {
-                const int pp = it / segs, s = it - pp * segs;
+                const int pp = it / segs;
+                int s = it - pp * segs;
+#ifdef FSKD_BOUNDS_DEBUG
+                {
+                    long long smp = (base + rb) * p.hop + 64LL * s + 64;
+                    RS_CHECK(smp, (p.n_windows - 1) * p.hop + 1025, "dense samples");
+                    int ss = s;
+                    RS_CHECK(ss, kSegStates / 2, "sen");
+                    int si = s * K + 1;
+                    RS_CHECK(si, kSegStates, "sst");
+                }
+#endif
                 const u32x4q *src = reinterpret_cast<const u32x4q *>(s0 + 64 * s);
                 u32x4q v[8];
 #pragma unroll
@@ -358,8 +405,11 @@ __global__ __launch_bounds__(64) void rescue_seg_kernel(RescueParams p)
 #pragma unroll 1
             for (int j = 0; j < cnt; j += 4) {
                 const bool live = j + row < cnt;
-                const int o = idx[i + (live ? j + row : j)];
-                const int sb = (o - rb) * H + seg;
+                int ii = i + (live ? j + row : j);
+                RS_CHECK(ii, kRescueChunk, "idx combine");
+                const int o = idx[ii];
+                int sb = (o - rb) * H + seg;
+                RS_CHECK(sb, segs, "sb");
                 const bool still = seg_decide(p, base + o, live, seg, sen[sb],
                                               [&](int t) { return sst[sb * K + t]; });
                 const unsigned long long lb = __ballot(live && still && seg == 0);
@@ -377,14 +427,54 @@ __global__ __launch_bounds__(64) void rescue_seg_kernel(RescueParams p)
     for (int g0 = 0; g0 < Ts; g0 += 4) {
         const bool live = g0 + row < Ts;
         const int o = idx[live ? g0 + row : g0];
-        const long long w = base + o;
+        long long w = base + o;
+        RS_CHECK(w, p.n_windows, "per-window w");
+        bool still;
+        if (p.fold64) {
+            // rescue_rows_fold0's arithmetic: lane seg's folded samples
+            // 8 seg .. + 7 (samples 128 m + 8 seg + i, m < 8), 8-step chains
+            const int16_t *xs = p.pcm + w * p.hop + 8 * seg;
+            u32x4q v[8];
+#pragma unroll
+            for (int m = 0; m < 8; ++m) v[m] = *reinterpret_cast<const u32x4q *>(xs + 128 * m);
+            int xf[8];
+            float e = 0.f;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) xf[i] = 0;
+#pragma unroll
+            for (int m = 0; m < 8; ++m) {
+                const unsigned d4[4] = {v[m].x, v[m].y, v[m].z, v[m].w};
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    const int x = (int)(short)((d4[i >> 1] >> (16 * (i & 1))) & 0xFFFFu);
+                    xf[i] += x;
+                    const float xv = (float)x;
+                    e = __builtin_fmaf(xv, xv, e);
+                }
+            }
+            still = seg_decide(p, w, live, seg, e, [&](int t) {
+                const double c = p.rot64[64 * K + t];
+                double s1 = 0.0, s2 = 0.0;
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    double s = (double)xf[i] + c * s1;
+                    s = s - s2;
+                    s2 = s1;
+                    s1 = s;
+                }
+                return make_double2(s1, s2);
+            });
+            const unsigned long long lb = __ballot(live && still && seg == 0);
+            if (live && still && seg == 0) left[Tl + __popcll(lb & ((1ull << lane) - 1))] = (unsigned short)o;
+            Tl += __popcll(lb);
+            continue;
+        }
         const u32x4q *src = reinterpret_cast<const u32x4q *>(p.pcm + w * p.hop + 64 * seg);
         u32x4q v[8];
 #pragma unroll
         for (int q = 0; q < 8; ++q) v[q] = src[q];
         const float e = seg_energy64(v);
         double2 sp[2];
-        bool still;
         if (K <= 2) {
             seg_pair(v, p.rot64[64 * K], p.rot64[64 * K + K - 1], sp[0].x, sp[0].y, sp[1].x, sp[1].y);
             still = seg_decide(p, w, live, seg, e, [&](int t) { return t ? sp[1] : sp[0]; });
@@ -411,7 +501,8 @@ __global__ __launch_bounds__(64) void rescue_seg_kernel(RescueParams p)
 #pragma unroll 1
     for (int g0 = 0; g0 < Tl; g0 += wpw) {
         const bool act = f < wpw && g0 + f < Tl;
-        const long long w = base + left[act ? g0 + f : g0];
+        long long w = base + left[act ? g0 + f : g0];
+        RS_CHECK(w, p.n_windows, "pass1 w");
         double P = 0.0;
         if (act) {
             const double c = p.coef[t];

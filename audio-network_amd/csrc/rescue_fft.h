@@ -194,15 +194,29 @@ __device__ __attribute__((always_inline)) inline void rescue_fft_window(const in
 // here (symbol; tone powers rounded to fp32, within that bound of the oracle's).
 // Returns the lane's row verdict: still ambiguous (for rescue_fft_window).
 // x: the row's window (valid where amb_row); k tones at runtime.
+// fold (every tone bin a multiple of 8; round 5): the lane reads samples
+// 128 m + 8 seg .. + 7 (m < 8) instead and runs rescue_rows_fold0's 8-step
+// chains over their integer sums (the window folded to 128), rot64 then
+// holding the fold tables (plan.h fold64).
 __device__ __forceinline__ bool rescue_fft_seg(const int16_t *__restrict__ x, const double *__restrict__ rot64,
                                                double t2e64, int k, int seg, bool amb_row, uint8_t *sym,
-                                               float *mag)
+                                               float *mag, bool fold)
 {
 #pragma clang fp contract(off)
     unsigned v[32];
-    const unsigned *src = reinterpret_cast<const unsigned *>(x + 64 * seg);
+    const unsigned *src = reinterpret_cast<const unsigned *>(x + (fold ? 8 : 64) * seg);
 #pragma unroll
-    for (int i = 0; i < 32; ++i) v[i] = amb_row ? src[i] : 0u;
+    for (int i = 0; i < 32; ++i) v[i] = amb_row ? src[fold ? 64 * (i >> 2) + (i & 3) : i] : 0u;
+    int xf[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        int a = 0;
+        if (fold) {
+#pragma unroll
+            for (int m = 0; m < 8; ++m) a += (int)(short)((v[4 * m + (i >> 1)] >> (16 * (i & 1))) & 0xFFFFu);
+        }
+        xf[i] = a;
+    }
     float e = 0.f;
 #pragma unroll
     for (int i = 0; i < 64; ++i) {
@@ -215,13 +229,23 @@ __device__ __forceinline__ bool rescue_fft_seg(const int16_t *__restrict__ x, co
     for (int t = 0; t < k; ++t) {
         const double c = rot64[64 * k + t];
         double s1 = 0.0, s2 = 0.0;
+        if (fold) {
 #pragma unroll
-        for (int i = 0; i < 64; ++i) {
-            const double xd = (double)(short)((v[i >> 1] >> (16 * (i & 1))) & 0xFFFFu);
-            double s = xd + c * s1;
-            s = s - s2;
-            s2 = s1;
-            s1 = s;
+            for (int i = 0; i < 8; ++i) {
+                double s = (double)xf[i] + c * s1;
+                s = s - s2;
+                s2 = s1;
+                s1 = s;
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 64; ++i) {
+                const double xd = (double)(short)((v[i >> 1] >> (16 * (i & 1))) & 0xFFFFu);
+                double s = xd + c * s1;
+                s = s - s2;
+                s2 = s1;
+                s1 = s;
+            }
         }
         const double *r = rot64 + 4 * (t * 16 + seg);
         double re = r[0] * s1, im = r[1] * s1;

@@ -1097,8 +1097,9 @@ def rescue_worst(A, torch, steps, warm, W=1 << 20) -> dict:
     """Every window ambiguous: the rescue's cost bound per detector, 2^20
     windows of the two-tone worst case (two_tone_stream): 2-FSK (plain bank,
     rescue inside the kernel), 8-FSK (fold F16, inside the kernel), FFT hop
-    256 over the same 2^30-sample stream (inside the kernel), 2-FSK at hop
-    256 (segment-shared windows, SLIDE: the rescue launch). Per detector the
+    256 over the same 2^30-sample stream (inside the kernel), 2-FSK and 8-FSK
+    at hop 256 (segment-shared windows, SLIDE / fold-slide: the rescue
+    launch). Per detector the
     step with the rescue (shipped), without it (FSKD_NO_RESCUE=1), with its
     exact path only (FSKD_RESCUE_SEG=0: no first pass by segments), the
     flagged fraction (FSKD_NO_RESCUE=flags) and a parity sample of the first
@@ -1115,6 +1116,9 @@ def rescue_worst(A, torch, steps, warm, W=1 << 20) -> dict:
                                           ("fft_hop256", A.FSK8_FREQS, 2, 5, A.METHOD_FFT, 256),
                                           # segment-shared windows: the rescue launch
                                           ("fsk2_slide_hop256", A.FSK2_FREQS, 0, 1, A.METHOD_AUTO,
+                                           256),
+                                          # fold-slide: the rescue launch, pass 0 by the fold
+                                          ("fsk8_slide_hop256", A.FSK8_FREQS, 2, 5, A.METHOD_AUTO,
                                            256)):
         two_tone_stream(torch, d_pcm, freqs, a, b)
         n_eval = (W * n - n) // hop + 1

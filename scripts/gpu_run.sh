@@ -15,6 +15,8 @@
 #   sqw[:<ENV=V|-> <args>]  one SQ pass of its wait states (SQ_WAIT_ANY / _INST_ANY / _INST_LDS)
 #   testsall[:<args>] pytest -m gpu without -x (all failures in one call)
 #   testsk:<expr>    pytest -m gpu -k <expr> without -x
+#   ktr:<case>       rocprofv3 --kernel-trace --stats of scripts/rescue_probe.py <case>
+#   sqr:<case>       one SQ pass of scripts/rescue_probe.py <case> (rescue worst case)
 #   precision        scripts/precision_probe.py
 #   py:<script args> python3 <script args> (probes under scripts/)
 #   pyt:<secs>:<args> the same under a time limit of its own
@@ -77,6 +79,12 @@ for st in "$@"; do
     testsall)
       # the GPU suite without -x (every failure of a change set in one call)
       timeout -k 10 1100 python -u -m pytest -v --timeout 300 --timeout-method thread -m gpu tests $arg > "$log" 2>&1 || exit $? ;;
+    ktr)
+      # kernel trace of one rescue worst case (scripts/rescue_probe.py <case>)
+      (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/ktr_$i" -o run -- python3 "$R/scripts/rescue_probe.py" $arg) > "$log" 2>&1 || exit $? ;;
+    sqr)
+      # one SQ pass (issue / wait counts) of a rescue worst case
+      (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE --output-format csv -d "$O/sqr_$i" -o run -- python3 "$R/scripts/rescue_probe.py" $arg 3) > "$log" 2>&1 || exit $? ;;
     precision)
       timeout -k 10 600 python3 -u scripts/precision_probe.py $arg > "$log" 2>&1 || exit $? ;;
     py)

@@ -132,14 +132,82 @@ def test_fft_pass0_error_model(A, O, plan):
     double radix-2 FFT powers of those bins (oracle.fft_demod)."""
     bins = [round(f * N / FS) for f in PLANS[plan]]
     freqs = tuple(b * FS / N for b in bins)
-    m = A.error_model(A.make_cfg(freqs=PLANS[plan], method=A.METHOD_FFT))
+    cfg = A.make_cfg(freqs=PLANS[plan], method=A.METHOD_FFT)
+    m = A.error_model(cfg)
+    info = A.plan_info(cfg)
+    # every bin a multiple of 8: pass 0 by the fold (plan.h fold64)
+    assert info["fold64"] == int(all(b % 8 == 0 for b in bins))
     assert m["rho_first"] > 0
     worst = (0.0, None)
     for fi, fam in enumerate(EM.FAMILIES):
         W = 384
         x = EM.family(fam, freqs, N, W, seed=200 + fi).reshape(W, N)
         ref_sym, ref_P = O.fft_demod(x, PLANS[plan], N)
-        P = pass0_powers(x, freqs, coef=[2.0 * math.cos(2.0 * math.pi * b / N) for b in bins])
+        if info["fold64"]:
+            P = pass0_fold_powers(x, info, len(bins))
+        else:
+            P = pass0_powers(x, freqs, coef=[2.0 * math.cos(2.0 * math.pi * b / N) for b in bins])
         r = _check(P, ref_sym, ref_P, x, m)
         worst = max(worst, (r, fam))
     print(f"\nfft {plan}: rho_first {m['rho_first']:.3g}, worst error {worst[0]:.3g} of it ({worst[1]})")
+
+
+# fold detector plans (every tone on a multiple of 8 bins; plan.h fold64):
+# pass 0 by the fold (demod_internal.h rescue_rows_fold0, rescue.hip
+# rescue_seg_kernel), including the DC and Nyquist bins
+FOLD_PLANS = {
+    "fsk8": (tuple(1500.0 + 375.0 * i for i in range(8)), "AUTO"),
+    "fold3_edges": ((8 * BIN, 16 * BIN, 504 * BIN), "AUTO"),
+    "fold2_dc": ((0.0, 8 * BIN), "FOLDED"),
+    "fold2_nyq": ((504 * BIN, 512 * BIN), "FOLDED"),
+}
+
+
+def pass0_fold_powers(x, info, K):
+    """Pass 0 by the fold of W windows x[W][1024] (int16), operation for
+    operation with the plan's own tables (demod_plan_info rot64: [k][16][4],
+    then the chains' coefficients): lane j's folded samples xf[8j .. 8j+7]
+    (exact integer sums over the 8 blocks of 128), an 8-step double chain per
+    tone, the rotation, the 16-lane butterfly, the power."""
+    W = x.shape[0]
+    r = info["rot64"]
+    rot = r[:64 * K].reshape(K, 16, 4)
+    xf = x.astype(np.int64).reshape(W, 8, 128).sum(axis=1).reshape(W, 16, 8).astype(np.float64)
+    P = np.empty((W, K))
+    for k in range(K):
+        c = r[64 * K + k]
+        s1 = np.zeros((W, 16))
+        s2 = np.zeros((W, 16))
+        for i in range(8):
+            s = xf[:, :, i] + c * s1
+            s = s - s2
+            s2, s1 = s1, s
+        re = rot[k, :, 0] * s1
+        im = rot[k, :, 1] * s1
+        re = re - rot[k, :, 2] * s2
+        im = im - rot[k, :, 3] * s2
+        re = butterfly_sum16(re)
+        im = butterfly_sum16(im)
+        P[:, k] = re * re + im * im
+    return P
+
+
+@pytest.mark.parametrize("plan", sorted(FOLD_PLANS))
+def test_fold_pass0_error_model(A, O, plan):
+    freqs, meth = FOLD_PLANS[plan]
+    cfg = A.make_cfg(freqs=freqs, method=getattr(A, "METHOD_" + meth))
+    info = A.plan_info(cfg)
+    assert info["method"] == A.METHOD_FOLDED and info["fold64"] == 1
+    # the exact chains keep the oracle's coefficients after pass 0's
+    K = len(freqs)
+    assert np.array_equal(info["rot64"][65 * K:66 * K], info["rcoef"])
+    m = A.error_model(cfg)
+    assert m["rho_first"] > 0
+    worst = (0.0, None)
+    for fi, fam in enumerate(EM.FAMILIES):
+        W = 384
+        x = EM.family(fam, freqs, N, W, seed=300 + fi).reshape(W, N)
+        ref_sym, ref_P = O.goertzel(x, freqs, N, fs=FS, threads=4)
+        r = _check(pass0_fold_powers(x, info, K), ref_sym, ref_P, x, m)
+        worst = max(worst, (r, fam))
+    print(f"\nfold {plan}: rho_first {m['rho_first']:.3g}, worst error {worst[0]:.3g} of it ({worst[1]})")
