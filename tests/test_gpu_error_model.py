@@ -19,6 +19,7 @@ emulation bit for bit (test_kernels_equal_emulation), which ties the CPU
 check of the bounds (tests/test_error_bound.py) to the shipped code.
 """
 import json
+import math
 import os
 
 import pytest
@@ -83,6 +84,40 @@ def test_rescued_decisions_every_window(A, O, torch, case):
         assert not (sym & 0x80).any(), (name, fam)
         bad = np.flatnonzero(sym != rs[:W])
         assert bad.size == 0, (name, fam, bad[:8].tolist())
+
+
+@pytest.mark.parametrize("plan", ["fsk2", "fsk8"])
+@pytest.mark.parametrize("hop", [128, 256, 384])
+def test_rescue_launch_equals_in_kernel_rescue(A, O, torch, plan, hop):
+    """The rescue launch of segment-shared windows (rescue.hip
+    rescue_seg_kernel: pass 0 by shared segment states in dense runs, per
+    window otherwise, by the fold for fold plans; then the exact chain) runs
+    the in-kernel rescue's arithmetic (demod_internal.h rescue_rows), so on
+    two tones at equal power (every window flagged and rescued) every
+    segment-shared window that starts at a multiple of n carries the same
+    symbol and magnitude bits as the direct kernel's window at hop = n, with
+    pass 0 on both sides (round 5), and every symbol is the oracle's."""
+    import numpy as np
+    freqs = A.FSK2_FREQS if plan == "fsk2" else A.FSK8_FREQS
+    n, blocks = 1024, 96
+    x = EM.family("two_tone_equal", freqs, n, blocks, 11)
+    with A.Demodulator(A.make_cfg(n=n, hop=n, freqs=freqs)) as d:
+        sym_d, mag_d = d.batch(x, mags=True)
+    W = (x.size - n) // hop + 1
+    with A.Demodulator(A.make_cfg(n=n, hop=hop, freqs=freqs)) as d:
+        assert d.slide_windows > 0
+        sym_s, mag_s = d.batch(x, n_windows=W, mags=True)
+    rs, _ = O.goertzel(x, freqs, n, hop=hop, fs=EM.FS, threads=16)
+    assert not (sym_s & 0x80).any()
+    assert np.array_equal(sym_s, rs[:W])
+    # the segment-shared windows that start at a multiple of n
+    w = np.arange(0, W, n // math.gcd(n, hop))
+    dw = w * hop // n
+    keep = dw < sym_d.size
+    w, dw = w[keep], dw[keep]
+    assert w.size > 8
+    assert np.array_equal(sym_s[w], sym_d[dw])
+    assert np.array_equal(mag_s[w].view(np.uint32), mag_d[dw].view(np.uint32))
 
 
 # the direct kernels of each path (the segment-shared ones are bit-identical
