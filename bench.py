@@ -537,15 +537,21 @@ def run_config(A, D, torch, dist, args, config, rank, world, local, use_dist, st
             try:
                 graphs = build_bucket("full", S, use_ring=ring is not None)
                 note("captured")
-                ms_per_step = time_graphs(graphs, S, n_rep)
-                note(f"timed {ms_per_step:.4f} ms per step")
-                bucket = {"S": S, "gathered": graphs[0][1], "graph": True}
                 # the detector's share on the same basis: a graph of the
                 # bucket's detector launches alone (the full step minus it
                 # is the framing + gather cost; round 4 subtracted eager
-                # event times from graph replays, VERDICT r4 weak 3 iv)
-                det_graph_ms = time_graphs(build_bucket("det", S, use_ring=ring is not None), S, n_rep)
-                bucket["det_graph_ms"] = det_graph_ms
+                # event times from graph replays, VERDICT r4 weak 3 iv),
+                # timed interleaved with the full bucket (3 rounds each,
+                # medians: one pair of back-to-back timings read -0.1 us)
+                det_graphs = build_bucket("det", S, use_ring=ring is not None)
+                fulls, dets = [], []
+                for _ in range(3):
+                    fulls.append(time_graphs(graphs, S, n_rep))
+                    dets.append(time_graphs(det_graphs, S, n_rep))
+                ms_per_step = float(np.median(fulls))
+                note(f"timed {ms_per_step:.4f} ms per step")
+                bucket = {"S": S, "gathered": graphs[0][1], "graph": True}
+                bucket["det_graph_ms"] = float(np.median(dets))
             except Exception as e:  # noqa: BLE001 - the eager bucket is timed instead
                 err = f"{type(e).__name__}: {e}"[:300]
                 note(f"graph failed ({err}); timing the same bucket eagerly")
