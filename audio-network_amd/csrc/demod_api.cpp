@@ -440,7 +440,9 @@ double demod_rescue_tau(const demod_t *st)
 
 double demod_rescue_tau64(const demod_t *st)
 {
-    if (!st || !st->rescue || !(rescue_in_kernel(st) || st->detector == kDetFft)) return 0.0;
+    // every rescue at n = 1024 runs the first pass (round 5: the rescue launch
+    // of segment-shared windows too, rescue.hip rescue_seg_kernel)
+    if (!st || !st->rescue || !st->d_rot64) return 0.0;
     return st->tau64;
 }
 

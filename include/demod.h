@@ -176,14 +176,16 @@ int demod_batch_launches(const demod_t *st, size_t n_windows, int with_mags);
  * DESIGN.md §2a); no measured constant. For tests and diagnostics. */
 double demod_rescue_tau(const demod_t *st);
 
-/* The in-kernel rescue's first pass (n = 1024 Goertzel-family detectors, and
- * the FFT detector's TONES-ONLY batches at its tone bins; a spectrum batch's
- * flagged windows always take the double FFT): a flagged window's powers in
- * double by 64-sample segments decide it when their top-2 margin clears
- * tau64 sqrt(n sum x^2 P_max); windows inside that band take the exact double
- * chain (or double FFT). Returns tau64 = 4 rho_first / sqrt(n) (0: every
- * flagged window takes the exact path — rescue launches, FSKD_RESCUE_SEG=0).
- * For tests and diagnostics. */
+/* The rescue's first pass (n = 1024: the Goertzel-family detectors, in the
+ * kernel or, for segment-shared windows, in the rescue launch; and the FFT
+ * detector's TONES-ONLY batches at its tone bins; a spectrum batch's flagged
+ * windows always take the double FFT): a flagged window's powers in double by
+ * 64-sample segments (fold plans and FFT plans whose tone bins are multiples
+ * of 8: by the window folded to 128 samples) decide it when their top-2
+ * margin clears tau64 sqrt(n sum x^2 P_max); windows inside that band take the
+ * exact double chain (or double FFT). Returns tau64 = 4 rho_first / sqrt(n)
+ * (0: every flagged window takes the exact path — n != 1024,
+ * FSKD_RESCUE_SEG=0). For tests and diagnostics. */
 double demod_rescue_tau64(const demod_t *st);
 
 /* The error bounds behind the decision rescue, derived for a

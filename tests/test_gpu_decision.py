@@ -23,7 +23,7 @@ from decision import check_decisions
 
 pytestmark = pytest.mark.gpu
 
-GOERTZEL, FFT, FOLDED, RESIDUE = 1, 2, 3, 4
+AUTO, GOERTZEL, FFT, FOLDED, RESIDUE = 0, 1, 2, 3, 4
 FSK8_ODD = tuple(46.875 * (32 + 9 * i) for i in range(8))
 NONINT8 = tuple(1234.5 + 1111.1 * i for i in range(8))
 
@@ -195,7 +195,8 @@ def test_rescue_double_ties_take_the_exact_chain(A, O, torch, plan, method):
     (FSK8_ODD, RESIDUE, 1024, 1024, True),
     ((46.875 * 1, 46.875 * 2), GOERTZEL, 1024, 1024, True),      # bin 1
     ((46.875 * 0.3, 1500.0), GOERTZEL, 1024, 1024, True),        # below bin 1
-    ((1500.0, 3000.0), GOERTZEL, 1024, 256, False),              # SLIDE: rescue launch
+    ((1500.0, 3000.0), GOERTZEL, 1024, 256, True),               # SLIDE: the rescue launch's pass 0
+    (tuple(1500.0 + 375.0 * i for i in range(8)), AUTO, 1024, 256, True),  # fold-slide, by the fold
     ((1500.0, 3000.0), GOERTZEL, 4096, 4096, False),             # n != 1024
     ((1500.0, 3000.0), FFT, 1024, 1024, True),                   # FFT: at its bins
     ((1500.0, 3000.0), FFT, 1024, 256, True),
@@ -204,7 +205,7 @@ def test_rescue_double_ties_take_the_exact_chain(A, O, torch, plan, method):
 def test_rescue_tau64_is_the_stated_model(A, torch, freqs, method, n, hop, expect):
     """The handle's tau64 is the derived bound's (demod_error_model: 4
     rho_first / sqrt(n), rho_first checked by tests/test_rescue_model64.py),
-    and 0 where no first pass runs (the rescue launch, n != 1024)."""
+    and 0 where no first pass runs (n != 1024)."""
     cfg = A.make_cfg(n=n, hop=hop, freqs=freqs, method=method)
     with A.Demodulator(cfg) as d:
         t = d.rescue_tau64
