@@ -1,0 +1,85 @@
+"""The rescue launch of segment-shared windows (csrc/rescue.hip
+rescue_seg_kernel, round 5): flagged windows compacted per
+512-window chunk, then pass 0 by shared segment states over dense runs of R
+windows (R chosen per launch from H = hop / 64 and K, not necessarily a
+divisor of the chunk), pass 0 per window for sparse runs and for fold plans
+(by the fold), and the exact chain for what pass 0 leaves.
+
+The data here mixes runs of near-tie windows (two plan tones at equal power:
+every window flagged) with runs of clean FSK (nothing flagged), with random
+run lengths, so every chunk sees dense runs, sparse runs, runs cut by the
+chunk's end and partial last chunks; over every H from 1 to 15 and tone
+plans from K = 2 to 16 (plain SLIDE and fold-slide). Every symbol must be the
+oracle's (oracle/fsk_oracle.c through oracle.goertzel) and no flag bit may be
+left. A round-5 run length of 61 (hop 256, K = 2) once read past the list's
+end here (profiles/round5/r5n/bounds_probe_before_fix.log).
+"""
+import numpy as np
+import pytest
+
+import error_model as EM
+
+pytestmark = pytest.mark.gpu
+
+N = 1024
+K16 = tuple(46.875 * (20 + 7 * i) for i in range(16))
+FOLD3 = (8 * EM.BIN, 16 * EM.BIN, 504 * EM.BIN)
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch as t
+    if not t.cuda.is_available():
+        pytest.skip("no GPU visible")
+    return t
+
+
+def mixed_stream(freqs, blocks, seed):
+    """Runs of 1..40 n-sample blocks alternating between two tones at equal
+    power (near ties) and clean FSK at sigma 400."""
+    rng = np.random.default_rng(seed)
+    tie = EM.family("two_tone_equal", freqs, N, blocks, seed)
+    fsk = EM.family("fsk_s400", freqs, N, blocks, seed + 1)
+    out = np.empty(blocks * N, np.int16)
+    b, use_tie = 0, bool(rng.integers(0, 2))
+    while b < blocks:
+        r = int(rng.integers(1, 41))
+        e = min(blocks, b + r)
+        src = tie if use_tie else fsk
+        out[b * N:e * N] = src[b * N:e * N]
+        b, use_tie = e, not use_tie
+    return out
+
+
+def run(A, O, freqs, hop, W, seed, expect_slide=True):
+    blocks = -(-((W - 1) * hop + N) // N)
+    x = mixed_stream(freqs, blocks, seed)[:(W - 1) * hop + N]
+    with A.Demodulator(A.make_cfg(n=N, hop=hop, freqs=freqs)) as d:
+        if expect_slide:
+            assert d.slide_windows > 0
+        assert d.rescue_tau64 > 0
+        sym = d.batch(x, n_windows=W)
+    rs, _ = O.goertzel(x, freqs, N, hop=hop, fs=EM.FS, threads=16)
+    assert not (sym & 0x80).any()
+    bad = np.flatnonzero(sym != rs[:W])
+    assert bad.size == 0, bad[:8].tolist()
+
+
+@pytest.mark.parametrize("H", list(range(1, 16)))
+def test_every_hop_k2(A, O, torch, H):
+    """2-FSK at hop 64 H: every run length R the launch can pick for K = 2;
+    W leaves a partial last chunk."""
+    run(A, O, A.FSK2_FREQS, 64 * H, 3 * 512 + 77, seed=H)
+
+
+@pytest.mark.parametrize("plan", ["FSK8_FREQS", "K16", "FOLD3"])
+@pytest.mark.parametrize("H", [1, 3, 4, 7, 15])
+def test_plans(A, O, torch, plan, H):
+    """8-FSK (fold-slide: pass 0 by the fold, no runs), K = 16 on the plain
+    bank (few windows per run: ((R - 1) H + 16) K <= 512), K = 3 fold at the
+    band edges."""
+    freqs = getattr(A, plan) if hasattr(A, plan) else globals()[plan]
+    # (K = 16 on integer bins above hop 384: AUTO takes the residue detector,
+    # windows one by one, its rescue in the kernel)
+    run(A, O, freqs, 64 * H, 2 * 512 + 301, seed=100 + H,
+        expect_slide=not (plan == "K16" and 64 * H > 384))
