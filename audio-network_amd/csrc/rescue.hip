@@ -249,6 +249,47 @@ __device__ __forceinline__ void wave_sync()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// One tone of a row's pass-0 decision: rotation of the lane's segment state
+// (s1, s2) into the window's phase, the 16-lane sums, the power and the
+// running argmax (rescue_rows' pass 0, operation for operation).
+__device__ __forceinline__ void seg_tone_step(const RescueParams &p, int t, int seg, double s1,
+                                              double s2, double &best, double &second, double &mine,
+                                              int &arg)
+{
+#pragma clang fp contract(off)
+    const double *r = p.rot64 + 4 * (t * 16 + seg);
+    double re = r[0] * s1, im = r[1] * s1;
+    re = re - r[2] * s2;
+    im = im - r[3] * s2;
+    re = row_sum16d(re);
+    im = row_sum16d(im);
+    const double pk = re * re + im * im;
+    if (pk > best) {
+        second = best;
+        best = pk;
+        arg = t;
+    } else if (pk > second) {
+        second = pk;
+    }
+    if (t == seg) mine = pk;
+}
+
+// The row's margin test on its K powers (e: the lane's fp32 sum x^2); decided
+// live rows write their symbol and powers. Returns "still ambiguous".
+__device__ __forceinline__ bool seg_finish(const RescueParams &p, long long w, bool live, int seg,
+                                           float e, double best, double second, double mine, int arg)
+{
+#pragma clang fp contract(off)
+    const int K = p.k;
+    const double cth = p.t2e64 * (double)row_sum16(e), dm = best - second;
+    const bool still = !(best > 0.0) || dm * dm < cth * best || 16.0 * best < cth;
+    if (live && !still) {
+        if (seg == 0) p.sym[w] = (uint8_t)arg;
+        if (p.mag && seg < K) p.mag[w * K + seg] = (float)mine;
+    }
+    return still;
+}
+
 // Row (16 lanes) decision of window w from its lane's segment state per tone
 // (st(t) -> {s1, s2}) and the lane's fp32 sum x^2 e: rescue_rows' pass-0
 // rotation, butterfly, argmax and margin test. Returns "still ambiguous";
@@ -257,36 +298,14 @@ template <typename St>
 __device__ __forceinline__ bool seg_decide(const RescueParams &p, long long w, bool live, int seg,
                                            float e, St st)
 {
-#pragma clang fp contract(off)
-    const int K = p.k;
     double best = -1.0, second = -1.0, mine = 0.0;
     int arg = 0;
 #pragma unroll 1
-    for (int t = 0; t < K; ++t) {
+    for (int t = 0; t < p.k; ++t) {
         const double2 s = st(t);
-        const double *r = p.rot64 + 4 * (t * 16 + seg);
-        double re = r[0] * s.x, im = r[1] * s.x;
-        re = re - r[2] * s.y;
-        im = im - r[3] * s.y;
-        re = row_sum16d(re);
-        im = row_sum16d(im);
-        const double pk = re * re + im * im;
-        if (pk > best) {
-            second = best;
-            best = pk;
-            arg = t;
-        } else if (pk > second) {
-            second = pk;
-        }
-        if (t == seg) mine = pk;
+        seg_tone_step(p, t, seg, s.x, s.y, best, second, mine, arg);
     }
-    const double cth = p.t2e64 * (double)row_sum16(e), dm = best - second;
-    const bool still = !(best > 0.0) || dm * dm < cth * best || 16.0 * best < cth;
-    if (live && !still) {
-        if (seg == 0) p.sym[w] = (uint8_t)arg;
-        if (p.mag && seg < K) p.mag[w * K + seg] = (float)mine;
-    }
-    return still;
+    return seg_finish(p, w, live, seg, e, best, second, mine, arg);
 }
 
 __global__ __launch_bounds__(64) void rescue_seg_kernel(RescueParams p)
@@ -452,18 +471,39 @@ __global__ __launch_bounds__(64) void rescue_seg_kernel(RescueParams p)
                     e = __builtin_fmaf(xv, xv, e);
                 }
             }
-            still = seg_decide(p, w, live, seg, e, [&](int t) {
-                const double c = p.rot64[64 * K + t];
-                double s1 = 0.0, s2 = 0.0;
+            // the folded samples converted once (exact); the tones' chains two
+            // at a time (independent chains interleaved), then each tone's
+            // rotation, sums and argmax step exactly as seg_decide's
+            double xd[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) xd[i] = (double)xf[i];
+            double best = -1.0, second = -1.0, mine = 0.0;
+            int arg = 0;
+#pragma unroll 1
+            for (int t0 = 0; t0 < K; t0 += 2) {
+                const int t1 = t0 + 1 < K ? t0 + 1 : t0;
+                const double c0 = p.rot64[64 * K + t0], c1 = p.rot64[64 * K + t1];
+                double a1 = 0.0, a2 = 0.0, b1 = 0.0, b2 = 0.0;
 #pragma unroll
                 for (int i = 0; i < 8; ++i) {
-                    double s = (double)xf[i] + c * s1;
-                    s = s - s2;
-                    s2 = s1;
-                    s1 = s;
+                    double sa = xd[i] + c0 * a1;
+                    sa = sa - a2;
+                    a2 = a1;
+                    a1 = sa;
+                    double sb = xd[i] + c1 * b1;
+                    sb = sb - b2;
+                    b2 = b1;
+                    b1 = sb;
                 }
-                return make_double2(s1, s2);
-            });
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    if (h && t1 == t0) break;
+                    const int t = h ? t1 : t0;
+                    const double s1 = h ? b1 : a1, s2 = h ? b2 : a2;
+                    seg_tone_step(p, t, seg, s1, s2, best, second, mine, arg);
+                }
+            }
+            still = seg_finish(p, w, live, seg, e, best, second, mine, arg);
             const unsigned long long lb = __ballot(live && still && seg == 0);
             if (live && still && seg == 0) left[Tl + __popcll(lb & ((1ull << lane) - 1))] = (unsigned short)o;
             Tl += __popcll(lb);
