@@ -83,3 +83,40 @@ def test_plans(A, O, torch, plan, H):
     # windows one by one, its rescue in the kernel)
     run(A, O, freqs, 64 * H, 2 * 512 + 301, seed=100 + H,
         expect_slide=not (plan == "K16" and 64 * H > 384))
+
+
+FOLD16 = tuple(EM.BIN * 8 * (2 + i) for i in range(16))      # 16 tones on multiples of 8 bins
+FOLD13 = FOLD16[:13]
+FOLD12 = FOLD16[:12]
+FFT_ODD = tuple(EM.BIN * (33 + 7 * i) for i in range(4))      # FFT bins not multiples of 8
+
+
+@pytest.mark.parametrize("plan,method,fold64", [
+    ("FOLD12", 3, 1),    # fold kernel, pass 0 by the fold (K <= kFold64MaxK)
+    ("FOLD13", 3, 0),    # above it: the fold kernels' pass 0 by segments
+    ("FOLD16", 3, 0),
+    ("FOLD16", 2, 0),    # FFT, bins on multiples of 8 but K > 12: by segments
+    ("FOLD12", 2, 1),    # FFT by the fold
+    ("FFT_ODD", 2, 0),   # FFT, odd bins: by segments
+])
+@pytest.mark.parametrize("hop", [1024, 256])
+def test_pass0_forms(A, O, torch, plan, method, fold64, hop):
+    """Each form of the first pass the plan selects (plan.h fold64: by the
+    fold at K <= 12 on multiples of 8 bins, else by 64-sample segments; in the
+    detector kernel at hop = n, in the rescue launch of segment-shared windows
+    at hop 256, in the FFT kernel) on runs of near ties: every symbol the
+    oracle's, no flag left."""
+    freqs = globals()[plan]
+    cfg = A.make_cfg(n=N, hop=hop, freqs=freqs, method=method)
+    assert A.plan_info(cfg)["fold64"] == fold64
+    W = 1536 + 77
+    blocks = -(-((W - 1) * hop + N) // N)
+    x = mixed_stream(freqs, blocks, seed=7 + len(freqs) + hop)[:(W - 1) * hop + N]
+    with A.Demodulator(cfg) as d:
+        assert d.rescue_tau64 > 0
+        sym = d.batch(x, n_windows=W)
+    rs, _ = (O.fft_demod(x, freqs, N, hop=hop, fs=EM.FS, threads=16) if method == 2 else
+             O.goertzel(x, freqs, N, hop=hop, fs=EM.FS, threads=16))
+    assert not (sym & 0x80).any()
+    bad = np.flatnonzero(sym != rs[:W])
+    assert bad.size == 0, bad[:8].tolist()
