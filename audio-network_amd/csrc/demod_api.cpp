@@ -571,6 +571,7 @@ static int enqueue_batch(demod_t *st, const int16_t *d_pcm, size_t n_windows, ui
     // covers its rounding), 0: the exact chain only
     p.rot64 = st->d_rot64;
     p.t2e64 = st->t2e64;
+    p.fold64 = st->fold64 ? 1 : 0;
     p.amb_d = st->amb_d;
     for (size_t w0 = 0; w0 < n_windows; w0 += per) {
         const size_t cnt = std::min(per, n_windows - w0);

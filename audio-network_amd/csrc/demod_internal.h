@@ -56,6 +56,9 @@ struct GoertzelParams {
     // order
     int rescue_inline;
     double rcoef[kMaxTones];
+    // rescue_rows' pass 0 by the fold (plan.h fold64; plain-bank plans on
+    // multiples of 8 bins read it at run time)
+    int fold64;
     // rescue_rows' tables: rot64 = [k][16][4] {Ar, Ai, Br, Bi} in double (the
     // caller's tone order), pass 0's chain coefficients c[k] (= rcoef[k]
     // except by the fold, plan.h fold64), then rcoef[k] again (the exact
@@ -395,14 +398,16 @@ __device__ __forceinline__ bool rescue_rows_fold0(const GoertzelParams &p, long 
     return amb_row && still;
 }
 
-template <int K, bool FOLD = false, typename Chunk>
+// FOLD: 0 = pass 0 by segments, 1 = by the fold (fold kernels), 2 = as the
+// plan says at run time (p.fold64: plain-bank plans on multiples of 8 bins)
+template <int K, int FOLD = 0, typename Chunk>
 __device__ __forceinline__ void rescue_rows(const GoertzelParams &p, long long w, int seg, int lane,
                                             bool amb_row, Chunk chunk)
 {
 #pragma clang fp contract(off)
     int first = p.t2e64 > 0.0 ? 0 : 1;
-    if constexpr (FOLD) {
-        if (first == 0) {
+    if constexpr (FOLD != 0) {
+        if (first == 0 && (FOLD == 1 || p.fold64)) {
             amb_row = rescue_rows_fold0<K>(p, w, seg, amb_row, chunk);
             if (__ballot(amb_row) == 0) return;
             first = 1;

@@ -264,7 +264,14 @@ void build_plan(const demod_cfg_t &c, Plan &pl)
     // exact bin (8x fewer double steps than 64 raw samples per lane per tone).
     if (c.n == 1024 && c.k >= 2) {
         const bool fft = pl.detector == kDetFft;
-        pl.fold64 = c.k <= (uint32_t)kFold64MaxK && (pl.detector == kDetFolded || fft);
+        // plain-bank plans at K <= 2 on multiples of 8 bins too (the survey's
+        // 2-FSK), where the windows are evaluated one by one (SLIDE's rescue
+        // launch shares segment states instead, cheaper at hop < n);
+        // FSKD_PASS0_FOLD=0 (a test / measurement switch) keeps segments
+        const char *pf_env = std::getenv("FSKD_PASS0_FOLD");
+        const bool plain_fold = pl.detector == kDetGoertzel && c.k <= 2 && !pl.slide && fold_eligible(c);
+        pl.fold64 = c.k <= (uint32_t)kFold64MaxK && (pl.detector == kDetFolded || fft || plain_fold) &&
+                    !(pf_env && pf_env[0] == '0');
         for (uint32_t k = 0; fft && k < c.k; ++k)
             if (pl.fft_bins[k] % 8) pl.fold64 = false;
         const double span = pl.fold64 ? 8.0 : 64.0;

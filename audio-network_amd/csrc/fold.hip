@@ -290,7 +290,7 @@ __global__ __launch_bounds__(64 * WPB) void fold_tile_kernel(GoertzelParams p)
             const bool amb = fold_decide<K, F16, MST>(acc, r, c16, lane, w, live, p, defer, rawfn);
             if constexpr (kInline) {
                 if (defer && __ballot(amb && live) != 0)
-                    rescue_rows<K, (K <= kFold64MaxK)>(p, w, j, lane, amb && live, [&](int q) { return wl[128 * win_in_tile + q]; });
+                    rescue_rows<K, (K <= kFold64MaxK) ? 1 : 0>(p, w, j, lane, amb && live, [&](int q) { return wl[128 * win_in_tile + q]; });
             }
             continue;
         }

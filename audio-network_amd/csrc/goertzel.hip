@@ -397,7 +397,7 @@ __global__ __launch_bounds__(64 * WPB) void goertzel_tile_kernel(GoertzelParams 
             const bool amb = window_sum_decide<K>(xr, xi, lane, w, live, p.sym, p.mag, 0,
                                                   AmbTest{p.amb_tq, p.amb_floor, p.amb_t2e, defer}, efn);
             if constexpr (kInline) {
-                if (defer && __ballot(amb && live) != 0) rescue_rows<K>(p, w, seg, lane, amb && live, chunk);
+                if (defer && __ballot(amb && live) != 0) rescue_rows<K, (K <= 2 ? 2 : 0)>(p, w, seg, lane, amb && live, chunk);
             }
             return;
         }
@@ -424,7 +424,7 @@ __global__ __launch_bounds__(64 * WPB) void goertzel_tile_kernel(GoertzelParams 
         if constexpr (kInline) {
             // decision rescue in the kernel (demod_internal.h rescue_rows); every
             // lane of a row holds the same all-reduced powers, so the same verdict
-            if (defer && __ballot(amb && live) != 0) rescue_rows<K>(p, w, seg, lane, amb && live, chunk);
+            if (defer && __ballot(amb && live) != 0) rescue_rows<K, (K <= 2 ? 2 : 0)>(p, w, seg, lane, amb && live, chunk);
         }
     };
 

@@ -2,7 +2,9 @@
 """The rescue worst case of one detector alone (for rocprofv3 PMC passes and
 kernel traces): bench.rescue_worst's two-tone stream, every window flagged.
     python3 scripts/rescue_probe.py fsk2_slide_hop256 [steps]
-Cases: fsk2, fsk8, fft_hop256, fsk2_slide_hop256, fsk8_slide_hop256. Prints
+Cases: fsk2, fsk8, fft_hop256, fsk2_slide_hop256, fsk8_slide_hop256, fsk8odd
+(residue detector). FSKD_NO_RESCUE=1 in the environment: the step without
+the rescue (for the slowdown). Prints
 the step time (HIP events over the timed steps) and the flagged fraction."""
 import os
 import sys
@@ -21,7 +23,9 @@ def main():
              "fsk8": (A.FSK8_FREQS, 2, 5, A.METHOD_AUTO, 1024),
              "fft_hop256": (A.FSK8_FREQS, 2, 5, A.METHOD_FFT, 256),
              "fsk2_slide_hop256": (A.FSK2_FREQS, 0, 1, A.METHOD_AUTO, 256),
-             "fsk8_slide_hop256": (A.FSK8_FREQS, 2, 5, A.METHOD_AUTO, 256)}
+             "fsk8_slide_hop256": (A.FSK8_FREQS, 2, 5, A.METHOD_AUTO, 256),
+             # 8 tones on integer bins 32 + 9 i (not multiples of 8): the residue detector
+             "fsk8odd": (tuple(46.875 * (32 + 9 * i) for i in range(8)), 2, 5, A.METHOD_AUTO, 1024)}
     freqs, a, b, method, hop = cases[case]
     W, n = 1 << 20, 1024
     dev = torch.device("cuda", 0)

@@ -88,7 +88,7 @@ def test_rescued_decisions_every_window(A, O, torch, case):
 
 @pytest.mark.parametrize("plan", ["fsk2", "fsk8"])
 @pytest.mark.parametrize("hop", [128, 256, 384])
-def test_rescue_launch_equals_in_kernel_rescue(A, O, torch, plan, hop):
+def test_rescue_launch_equals_in_kernel_rescue(A, O, torch, monkeypatch, plan, hop):
     """The rescue launch of segment-shared windows (rescue.hip
     rescue_seg_kernel: pass 0 by shared segment states in dense runs, per
     window otherwise, by the fold for fold plans; then the exact chain) runs
@@ -96,11 +96,15 @@ def test_rescue_launch_equals_in_kernel_rescue(A, O, torch, plan, hop):
     two tones at equal power (every window flagged and rescued) every
     segment-shared window that starts at a multiple of n carries the same
     symbol and magnitude bits as the direct kernel's window at hop = n, with
-    pass 0 on both sides (round 5), and every symbol is the oracle's."""
+    pass 0 on both sides (round 5), and every symbol is the oracle's. (The
+    2-FSK plain bank takes pass 0 by the fold at hop = n and by shared
+    segments at hop < n: FSKD_PASS0_FOLD=0 puts both on segments here.)"""
     import numpy as np
     freqs = A.FSK2_FREQS if plan == "fsk2" else A.FSK8_FREQS
     n, blocks = 1024, 96
     x = EM.family("two_tone_equal", freqs, n, blocks, 11)
+    if plan == "fsk2":
+        monkeypatch.setenv("FSKD_PASS0_FOLD", "0")
     with A.Demodulator(A.make_cfg(n=n, hop=n, freqs=freqs)) as d:
         sym_d, mag_d = d.batch(x, mags=True)
     W = (x.size - n) // hop + 1

@@ -120,3 +120,24 @@ def test_pass0_forms(A, O, torch, plan, method, fold64, hop):
     assert not (sym & 0x80).any()
     bad = np.flatnonzero(sym != rs[:W])
     assert bad.size == 0, bad[:8].tolist()
+
+
+@pytest.mark.parametrize("hop", [1024, 512, 256])
+def test_plain_fsk2_pass0_forms(A, O, torch, hop):
+    """The survey's 2-FSK on the plain bank: pass 0 by the fold where its
+    windows are evaluated one by one (hop = n and hop 512 ... any hop without
+    segment sharing is direct), by shared segment states in the rescue launch
+    at hop 256 (SLIDE)."""
+    freqs = A.FSK2_FREQS
+    cfg = A.make_cfg(n=N, hop=hop, freqs=freqs)
+    slide = hop < N and hop % 64 == 0
+    assert A.plan_info(cfg)["fold64"] == int(not slide)
+    W = 1536 + 77
+    blocks = -(-((W - 1) * hop + N) // N)
+    x = mixed_stream(freqs, blocks, seed=3 + hop)[:(W - 1) * hop + N]
+    with A.Demodulator(cfg) as d:
+        assert (d.slide_windows > 0) == slide
+        sym = d.batch(x, n_windows=W)
+    rs, _ = O.goertzel(x, freqs, N, hop=hop, fs=EM.FS, threads=16)
+    assert not (sym & 0x80).any()
+    assert np.array_equal(sym, rs[:W])

@@ -113,14 +113,19 @@ def _check(P, ref_sym, ref_P, x, m):
 @pytest.mark.parametrize("plan", sorted(PLANS))
 def test_pass0_error_model(A, O, plan):
     freqs = PLANS[plan]
-    m = A.error_model(A.make_cfg(freqs=freqs, method=A.METHOD_GOERTZEL))
+    cfg = A.make_cfg(freqs=freqs, method=A.METHOD_GOERTZEL)
+    m = A.error_model(cfg)
+    info = A.plan_info(cfg)
+    # K <= 2 on multiples of 8 bins (fsk2): the plain bank's pass 0 by the fold
+    assert info["fold64"] == int(plan == "fsk2")
     assert m["rho_first"] > 0
     worst = (0.0, None)
     for fi, fam in enumerate(EM.FAMILIES):
         W = 384
         x = EM.family(fam, freqs, N, W, seed=100 + fi).reshape(W, N)
         ref_sym, ref_P = O.goertzel(x, freqs, N, fs=FS, threads=4)
-        r = _check(pass0_powers(x, freqs), ref_sym, ref_P, x, m)
+        P = pass0_fold_powers(x, info, len(freqs)) if info["fold64"] else pass0_powers(x, freqs)
+        r = _check(P, ref_sym, ref_P, x, m)
         worst = max(worst, (r, fam))
     print(f"\n{plan}: rho_first {m['rho_first']:.3g}, worst error {worst[0]:.3g} of it ({worst[1]})")
 
