@@ -1105,7 +1105,7 @@ def rescue_worst(A, torch, steps, warm, W=1 << 20) -> dict:
     rescue inside the kernel), 8-FSK (fold F16, inside the kernel), FFT hop
     256 over the same 2^30-sample stream (inside the kernel), 2-FSK and 8-FSK
     at hop 256 (segment-shared windows, SLIDE / fold-slide: the rescue
-    launch). Per detector the
+    launch), 8-FSK on bins 32 + 9 i (the residue detector). Per detector the
     step with the rescue (shipped), without it (FSKD_NO_RESCUE=1), with its
     exact path only (FSKD_RESCUE_SEG=0: no first pass by segments), the
     flagged fraction (FSKD_NO_RESCUE=flags) and a parity sample of the first
@@ -1125,7 +1125,11 @@ def rescue_worst(A, torch, steps, warm, W=1 << 20) -> dict:
                                            256),
                                           # fold-slide: the rescue launch, pass 0 by the fold
                                           ("fsk8_slide_hop256", A.FSK8_FREQS, 2, 5, A.METHOD_AUTO,
-                                           256)):
+                                           256),
+                                          # 8 tones on bins 32 + 9 i: the residue detector,
+                                          # pass 0 by segments
+                                          ("fsk8odd", tuple(46.875 * (32 + 9 * i) for i in range(8)),
+                                           2, 5, A.METHOD_AUTO, n)):
         two_tone_stream(torch, d_pcm, freqs, a, b)
         n_eval = (W * n - n) // hop + 1
         K = len(freqs)
