@@ -28,9 +28,11 @@
  * error bound (derived from the kernel's operation sequence and constants,
  * demod_error_model) is flagged, and the decision rescue
  * decides it again in double and rewrites its symbol and powers: first by
- * 64-sample segments (n = 1024; its own derived bound against the
- * definition's, so the rewritten powers are within that bound of the
- * definition's, not its bits), and where that pass cannot decide, with the
+ * 64-sample segments, or by the window folded to 128 samples where every
+ * tone sits on a multiple of 8 bins (n = 1024; its own derived bound against
+ * the definition's, so the rewritten powers are within that bound of the
+ * definition's, not its bits; FSKD_PASS0_FOLD=0 keeps segments), and where
+ * that pass cannot decide, with the
  * definition's own arithmetic (powers bit-identical to it; every rescued
  * window with FSKD_RESCUE_SEG=0). The flag test runs in two stages: the int16 worst-case
  * energy first (no per-sample work), then, only for windows that test
