@@ -15,6 +15,11 @@
 // fp32) over the window's magnitudes. (The FFT detector rescues its windows
 // inside its own kernel: rescue_fft.h.)
 //
+// Two kernels share the scan and compaction below: rescue_kernel (n != 1024,
+// or the first pass switched off: the exact chains only) and
+// rescue_seg_kernel (n = 1024, round 5: the first pass, then the exact
+// chains of what it leaves).
+//
 // Layout: one wave per 512 consecutive windows (round 3: 4096; with every
 // window of a chunk flagged a wave served them one group after another, so
 // eight times more waves bound the worst case eight times lower). It first reads
@@ -161,7 +166,8 @@ __global__ __launch_bounds__(64) void rescue_kernel(RescueParams p)
 // equal tones at hop 256, 12x the detector). Here the flagged windows take
 // rescue_rows' pass 0 (demod_internal.h): every tone's double recurrence over
 // each of the window's 16 segments of 64 samples, rotated into the window's
-// phase (rot64), summed over the segments by xor butterfly in a 16-lane row;
+// phase (rot64), summed over the segments in a 16-lane row (DPP, the xor
+// butterfly's tree);
 // where the top-2 margin clears t2e64 E P_max (the derived bound,
 // error_model.cpp) the window is decided (symbol, powers rounded to fp32).
 // A segment's recurrence starts from zero at the segment, so at hop = 64 H
@@ -172,6 +178,9 @@ __global__ __launch_bounds__(64) void rescue_kernel(RescueParams p)
 //    go to LDS, and each flagged window's row rotates and sums its 16 (at
 //    hop 256: a quarter of the chains);
 //  sparse windows: the row runs its window's 16 segments itself;
+//  fold plans (plan.h fold64; p.fold64): every window's pass 0 by the fold
+//    (rescue_rows_fold0's arithmetic: lane j's folded samples 8j .. 8j + 7,
+//    8-step chains), no runs;
 //  pass 1: the windows pass 0 leaves (exact ties) take the exact chain, lane
 //    f K + t on tone t of window f, its 1 024 samples read from L2 directly:
 //    every rounding step of oracle/fsk_oracle.c, bit-identical powers and
