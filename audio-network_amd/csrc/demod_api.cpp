@@ -62,7 +62,7 @@ struct demod {
     bool reinsch = false;       // plain detector: Reinsch-modified recurrence
     int dcls = 0;               // residue detector: compile-time class pattern (residue.hip DC), slots permuted
     bool f16 = false;           // fold detector: fold by 16, slots permuted (Z0 tones, Z8 tones)
-    bool fold64 = false;        // the rescue's pass 0 by the fold (plan.h)
+    int fold64 = 0;             // the rescue's pass 0 by the fold / residue fold (plan.h)
     unsigned long long perm = 0;  // DCLS: nibble s = tone index of kernel slot s
     int zcls[kMaxTones] = {};   // residue detector: class each tone reads
     // staging for host-pointer calls
@@ -429,6 +429,13 @@ static int burst_count(const demod_t *st, size_t n_windows, bool mags)
 // always rescues in its own kernel (rescue_fft.h).
 static bool rescue_in_kernel(const demod_t *st)
 {
+    // the residue detector's plans take the rescue launch (round 5): its first
+    // pass by the residue fold lives there (its per-lane class data would not
+    // fit the residue kernels' registers). Worst case (every window a near
+    // tie) 2.09 -> 1.59 ms per 2^20 8-FSK windows on bins 32 + 9i; the extra
+    // launch costs the clean step 0.4-0.75 % (0.3446 vs 0.3420 ms,
+    // profiles/round5/r5zg/, r5zh/)
+    if (st->detector == kDetResidue && st->fold64 == 2) return false;
     return st->detector != kDetFft && st->log2g == 4 && st->slide_wt == 0 && !st->rescue_kernel_forced;
 }
 
@@ -520,7 +527,7 @@ static int enqueue_fft(demod_t *st, const int16_t *d_pcm, size_t n_windows, uint
     // flagged window takes the double FFT, whose spectrum row is the oracle's)
     p.rot64 = st->d_rot64;
     p.t2e64 = st->t2e64;
-    p.fold64 = st->fold64 ? 1 : 0;
+    p.fold64 = st->fold64 == 1 ? 1 : 0;
     HIP_TRY(launch_fft_quad(p, s));
     return (int)n_windows;
 }
@@ -571,7 +578,7 @@ static int enqueue_batch(demod_t *st, const int16_t *d_pcm, size_t n_windows, ui
     // covers its rounding), 0: the exact chain only
     p.rot64 = st->d_rot64;
     p.t2e64 = st->t2e64;
-    p.fold64 = st->fold64 ? 1 : 0;
+    p.fold64 = st->fold64 == 1 ? 1 : 0;  // rescue_rows: by the fold (the residue fold: the launch)
     p.amb_d = st->amb_d;
     for (size_t w0 = 0; w0 < n_windows; w0 += per) {
         const size_t cnt = std::min(per, n_windows - w0);

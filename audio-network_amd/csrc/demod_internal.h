@@ -554,7 +554,8 @@ struct RescueParams {
     double coef[kMaxTones];  // Goertzel: 2 cos(2 pi f_k / fs), the caller's tone order
     // n = 1024 (round 5): the first pass by segments (rescue_rows pass 0's
     // arithmetic and tables) before the exact chains; t2e64 = 0: exact only;
-    // fold64: by the fold (rescue_rows_fold0's arithmetic, plan.h)
+    // fold64: 1 = by the fold (rescue_rows_fold0's arithmetic), 2 = by the
+    // residue fold (rescue.hip seg_residue_window; plan.h)
     const double *rot64;
     double t2e64;
     int fold64;

@@ -270,20 +270,26 @@ void build_plan(const demod_cfg_t &c, Plan &pl)
         // FSKD_PASS0_FOLD=0 (a test / measurement switch) keeps segments
         const char *pf_env = std::getenv("FSKD_PASS0_FOLD");
         const bool plain_fold = pl.detector == kDetGoertzel && c.k <= 2 && !pl.slide && fold_eligible(c);
-        pl.fold64 = c.k <= (uint32_t)kFold64MaxK && (pl.detector == kDetFolded || fft || plain_fold) &&
-                    !(pf_env && pf_env[0] == '0');
+        const bool off = pf_env && pf_env[0] == '0';
+        pl.fold64 = (c.k <= (uint32_t)kFold64MaxK && (pl.detector == kDetFolded || fft || plain_fold) &&
+                     !off) ? 1 : 0;
         for (uint32_t k = 0; fft && k < c.k; ++k)
-            if (pl.fft_bins[k] % 8) pl.fold64 = false;
+            if (pl.fft_bins[k] % 8) pl.fold64 = 0;
+        // the residue detector's plans (round 5): by the residue fold, in the
+        // rescue launch (demod_api.cpp rescue_in_kernel)
+        if (pl.detector == kDetResidue && !off) pl.fold64 = 2;
         const double span = pl.fold64 ? 8.0 : 64.0;
-        // [k][16][4], pass 0's chain coefficients c[k], then the oracle's
-        // rcoef[k] (the exact chains' coefficients)
-        pl.rot64.assign((size_t)c.k * 16 * 4 + 2 * c.k, 0.0);
+        // [k][16][4], pass 0's chain coefficients c[k], the oracle's rcoef[k]
+        // (the exact chains' coefficients), then each tone's residue rho
+        // (fold64 = 2)
+        pl.rot64.assign((size_t)c.k * 16 * 4 + 3 * c.k, 0.0);
         for (uint32_t k = 0; k < c.k; ++k) {
             const double w = fft          ? 2.0 * M_PI * pl.fft_bins[k] / (double)c.n
                              : pl.fold64 ? 2.0 * M_PI * (double)integer_bin(c, k) / (double)c.n
                                          : 2.0 * M_PI * c.freqs[k] / c.fs;
             pl.rot64[(size_t)c.k * 64 + k] = (fft || pl.fold64) ? 2.0 * std::cos(w) : pl.rcoef[k];
             pl.rot64[(size_t)c.k * 65 + k] = pl.rcoef[k];
+            if (pl.fold64 == 2) pl.rot64[(size_t)c.k * 66 + k] = (double)(integer_bin(c, k) % 8);
             for (int j = 0; j < 16; ++j) {
                 const double a = -w * (span * j + span - 1.0), b = -w * (span * j + span);
                 double *o = &pl.rot64[((size_t)k * 16 + j) * 4];
@@ -846,6 +852,81 @@ ld first_pass_fold_rho(const Plan &pl, uint32_t K, uint32_t k, ld w_b)
     return acc.finish(w_b, 4, kU64);
 }
 
+// pass 0 by the residue fold (Plan::fold64 = 2) for tone k (bin b, residue
+// rho = b mod 8) at w_b, per ||x||: lane j's 64 raw samples x[128 m + 8 j + i]
+// (input 8 m + i), per position i the exact integer butterflies a_m = x_m +
+// x_{m+4}, d_m = x_m - x_{m+4} (m < 4) and Y_rho = sum_m x_m e^{-2 pi i rho m
+// / 8}: rho 0 / 4 real (a0 + a2 +- (a1 + a3)), rho 2 / 6 complex integers
+// (a0 - a2, -+(a1 - a3)), odd rho d0 +- c u, -+d2 -+ c v with u = d1 - d3, v =
+// d1 + d3, c = sqrt(2) / 2 in double (the products and sums rounded); two
+// 8-step double chains (real and imaginary part; one for a real Y), the
+// complex rotation X = A S1 - B S2 (every product and sum rounded), the
+// 16-lane tree, the power (rescue.hip rescue_seg_kernel, op for op)
+ld first_pass_residue_rho(const Plan &pl, uint32_t K, uint32_t k, ld w_b, int rho)
+{
+    const double *r64 = pl.rot64.data();
+    const ld cc = r64[(size_t)K * 64 + k];
+    const ld cq = (ld)0.70710678118654752440;  // (double) sqrt(2) / 2, as the kernel's constant
+    Lane L(64);
+    std::vector<int> yr(8), yi(8);
+    const bool cplx = !(rho == 0 || rho == 4);
+    for (int i = 0; i < 8; ++i) {
+        int x[8];
+        for (int m = 0; m < 8; ++m) x[m] = 8 * m + i;
+        int a[4], d[4];
+        for (int m = 0; m < 4; ++m) {
+            a[m] = L.op({{x[m], 1}, {x[m + 4], 1}}, false);
+            d[m] = L.op({{x[m], 1}, {x[m + 4], -1}}, false);
+        }
+        if (rho == 0 || rho == 4) {
+            const ld sg = rho == 0 ? 1.0L : -1.0L;
+            yr[i] = L.op({{a[0], 1}, {a[2], 1}, {a[1], sg}, {a[3], sg}}, false);
+        } else if (rho == 2 || rho == 6) {
+            yr[i] = L.op({{a[0], 1}, {a[2], -1}}, false);
+            const ld sg = rho == 2 ? -1.0L : 1.0L;
+            yi[i] = L.op({{a[1], sg}, {a[3], -sg}}, false);
+        } else {
+            const int u = L.op({{d[1], 1}, {d[3], -1}}, false), v = L.op({{d[1], 1}, {d[3], 1}}, false);
+            const int cu = L.op({{u, cq}}, true), cv = L.op({{v, cq}}, true);
+            const ld su = (rho == 1 || rho == 7) ? 1.0L : -1.0L;       // re = d0 +- c u
+            const ld sd = (rho == 1 || rho == 5) ? -1.0L : 1.0L;       // im = +-d2 +- c v
+            const ld sv = (rho == 1 || rho == 3) ? -1.0L : 1.0L;
+            yr[i] = L.op({{d[0], 1}, {cu, su}}, true);
+            yi[i] = L.op({{d[2], sd}, {cv, sv}}, true);
+        }
+    }
+    int s1r, s2r, s1i = -1, s2i = -1;
+    chain_double(L, yr, cc, s1r, s2r);
+    if (cplx) chain_double(L, yi, cc, s1i, s2i);
+    const Core core = cplx ? analyze_core(L, {s1r, s2r, s1i, s2i}) : analyze_core(L, {s1r, s2r});
+    WindowAcc acc(1024);
+    std::vector<int> pos(64);
+    for (int j = 0; j < 16; ++j) {
+        const double *o = &r64[((size_t)k * 16 + j) * 4];
+        for (int m = 0; m < 8; ++m)
+            for (int i = 0; i < 8; ++i) pos[8 * m + i] = 128 * m + 8 * j + i;
+        if (!cplx) {
+            acc.add(rot_lane(core, o[0], o[1], o[2], o[3], kU64), pos);
+            continue;
+        }
+        // head over (S1r, S2r, S1i, S2i) = inputs 0 .. 3:
+        // re = (Ar S1r - Ai S1i) - (Br S2r - Bi S2i), im = (Ar S1i + Ai S1r) - (Br S2i + Bi S2r)
+        Lane H(4);
+        const int p1 = H.op({{0, o[0]}}, true), p2 = H.op({{2, o[1]}}, true);
+        const int t1 = H.op({{p1, 1}, {p2, -1}}, true);
+        const int q1 = H.op({{1, o[2]}}, true), q2 = H.op({{3, o[3]}}, true);
+        const int t2 = H.op({{q1, 1}, {q2, -1}}, true);
+        const int re = H.op({{t1, 1}, {t2, -1}}, true);
+        const int p3 = H.op({{2, o[0]}}, true), p4 = H.op({{0, o[1]}}, true);
+        const int t3 = H.op({{p3, 1}, {p4, 1}}, true);
+        const int q3 = H.op({{3, o[2]}}, true), q4 = H.op({{1, o[3]}}, true);
+        const int t4 = H.op({{q3, 1}, {q4, 1}}, true);
+        const int im = H.op({{t3, 1}, {t4, -1}}, true);
+        acc.add(analyze_lane(core, H, re, im, kU64), pos);
+    }
+    return acc.finish(w_b, 4, kU64);
+}
+
 }  // namespace
 
 void error_model(const demod_cfg_t &c, const Plan &pl, bool first_pass, ErrModel &m)
@@ -918,8 +999,10 @@ void error_model(const demod_cfg_t &c, const Plan &pl, bool first_pass, ErrModel
             if (pl.fold64) {
                 // pass 0 evaluates the exact bin; the Goertzel oracle its own
                 // frequency (the FFT oracle the bin)
-                const ld wb = 2.0L * kPi * (ld)(fft ? pl.fft_bins[k] : integer_bin(c, k)) / (ld)n;
-                r = std::sqrt(8.0L) * first_pass_fold_rho(pl, c.k, k, wb);
+                const long long b = fft ? pl.fft_bins[k] : integer_bin(c, k);
+                const ld wb = 2.0L * kPi * (ld)b / (ld)n;
+                r = pl.fold64 == 2 ? first_pass_residue_rho(pl, c.k, k, wb, (int)(b % 8))
+                                   : std::sqrt(8.0L) * first_pass_fold_rho(pl, c.k, k, wb);
                 if (fft) r += fft_oracle_rho(n);
                 else r += freq_gap(std::acos((ld)pl.rcoef[k] / 2.0L), wb, n) + oracle_rho(pl.rcoef[k], n);
             } else {

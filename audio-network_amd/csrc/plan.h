@@ -30,12 +30,16 @@ struct Plan {
     int fft_bins[kMaxTones] = {};
     int fft_slot[kMaxTones] = {};
     std::vector<double> rot64;   // pass 0 tables (n = 1024, K >= 2): [k][16][4], then c[k]
-    // pass 0 by the fold (fold detector plans: every tone on a multiple of 8
-    // bins): lane j's chain runs over folded samples 8j .. 8j + 7 of the
-    // window folded to 128 (exact integer sums), rot64 = A = e^{-i w (8j + 7)},
-    // B = e^{-i w (8j + 8)} at the exact bin w = 2 pi b / n, c = 2 cos w;
-    // otherwise lane j's 64 raw samples (A = e^{-i w (64j + 63)}, ...)
-    bool fold64 = false;
+    // pass 0 by the fold (1: every tone on a multiple of 8 bins): lane j's
+    // chain runs over folded samples 8j .. 8j + 7 of the window folded to 128
+    // (exact integer sums), rot64 = A = e^{-i w (8j + 7)}, B = e^{-i w (8j +
+    // 8)} at the exact bin w = 2 pi b / n, c = 2 cos w; by the residue fold
+    // (2: the residue detector's plans, every tone on an integer bin b): the
+    // same positions of Y_rho = sum_m x[p + 128 m] e^{-2 pi i rho m / 8},
+    // rho = b mod 8 (complex for odd / 2, 6 residues), its two real chains
+    // and a complex rotation, rho after the coefficients in rot64; 0: lane
+    // j's 64 raw samples (A = e^{-i w (64j + 63)}, ...)
+    int fold64 = 0;
 };
 
 // DEMOD_OK or the error code demod_create returns for it.

@@ -36,6 +36,11 @@ namespace fskd {
 
 // windows whose symbols one wave scans
 constexpr int kRescueChunk = 512;
+// rescue_seg_kernel: waves per chunk's block. A chunk of 512 near ties is ~2 ms
+// of one wave's work; 2048 chunks per 2^20 windows at one wave each are 2
+// waves per SIMD, too few to hide the double chains' latency (and 4 x the
+// blocks of one wave each cost ~2.5 us of dispatch per launch)
+constexpr int kRescueSplit = 4;
 constexpr int kRescueLdsBytes = 32768;    // Goertzel: staged samples per group
 
 typedef unsigned int u32x4q __attribute__((ext_vector_type(4)));
@@ -317,31 +322,217 @@ __device__ __forceinline__ bool seg_decide(const RescueParams &p, long long w, b
     return seg_finish(p, w, live, seg, e, best, second, mine, arg);
 }
 
-__global__ __launch_bounds__(64) void rescue_seg_kernel(RescueParams p)
+// Pass 0 of window w by the residue fold (plan.h fold64 = 2; the residue
+// detector's plans, every tone on an integer bin b, residue rho = b mod 8):
+// lane seg reads the window's samples 128 m + 8 seg + i (m, i < 8), forms per
+// position i, once per window, the exact butterflies a_m = x_m + x_{m+4},
+// d_m = x_m - x_{m+4} and the class values every residue needs (six exact
+// integers and c u, c v in double, c = sqrt(2) / 2); per tone Y_rho = sum_m
+// x_m e^{-2 pi i rho m / 8} (rho 0 / 4 real, 2 / 6 complex integers, odd rho
+// d0 +- c u, +-d2 +- c v), its real and imaginary 8-step chains at the exact
+// bin, the complex rotation into the window's phase and the row sums. Every
+// operation as error_model.cpp first_pass_residue_rho analyses it
+// (contraction off; tests/test_rescue_model64.py pass0_residue_powers
+// restates it). Returns "still ambiguous"; decided live rows write their
+// symbol and powers. 128 VGPRs (occupancy 4) with the class data as integers
+// converted per use; as doubles (16 fewer converts per odd tone) 192.
+__device__ __forceinline__ bool seg_residue_window(const RescueParams &p, long long w, bool live,
+                                                   int seg)
 {
 #pragma clang fp contract(off)
-    __shared__ unsigned short idx[kRescueChunk];   // flagged windows (chunk offsets), in order
-    __shared__ unsigned short left[kRescueChunk];  // pass 1's list
-    __shared__ double2 sst[kSegStates];            // dense run: [segment][tone] {s1, s2}
-    __shared__ float sen[kSegStates / 2];          // dense run: [segment] fp32 sum x^2
-    const int lane = threadIdx.x;
-    const long long base = tile_block(1) * kRescueChunk;
-    const int span = (int)min((long long)kRescueChunk, p.n_windows - base);
+    const int K = p.k;
+    const int16_t *xs = p.pcm + w * p.hop + 8 * seg;
+    u32x4q v[8];
+#pragma unroll
+    for (int m = 0; m < 8; ++m) v[m] = *reinterpret_cast<const u32x4q *>(xs + 128 * m);
+    auto smp = [&](int m, int i) {
+        const unsigned d4[4] = {v[m].x, v[m].y, v[m].z, v[m].w};
+        return (int)(short)((d4[i >> 1] >> (16 * (i & 1))) & 0xFFFFu);
+    };
+    // per position: its 8 samples, the lane's sum x^2 (any order: E only
+    // scales the threshold, within error_model's safety factor), the exact
+    // butterflies and the class values every residue's Y is formed from, in
+    // double once per window (shared by the tones): Y_0 = (a0 + a2) + (a1 +
+    // a3), Y_4 = (a0 + a2) - (a1 + a3), P = a0 - a2, Q = a1 - a3 (Y_2 = P -
+    // i Q, Y_6 = P + i Q), d0, d2, c u, c v (u = d1 - d3, v = d1 + d3)
+    const double kC = 0.70710678118654752440;
+    // class values as exact integers, pair (m, m + 4) by pair (the pair's
+    // samples die with it), then converted position by position
+    float e = 0.f;
+    int q[8][8];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int xl = smp(m, i), xh = smp(m + 4, i);
+            const float fl = (float)xl, fh = (float)xh;
+            e = __builtin_fmaf(fl, fl, e);
+            e = __builtin_fmaf(fh, fh, e);
+            const int am = xl + xh, dm = xl - xh;
+            int *c = q[i];
+            if (m == 0) {
+                c[0] = am; c[1] = am; c[2] = am; c[4] = dm;
+            } else if (m == 1) {
+                c[0] += am; c[1] -= am; c[3] = am; c[6] = dm; c[7] = dm;
+            } else if (m == 2) {
+                c[0] += am; c[1] += am; c[2] -= am; c[5] = dm;
+            } else {
+                c[0] += am; c[1] -= am; c[3] -= am; c[6] -= dm; c[7] += dm;
+            }
+        }
+    }
+    // (e is done here: not sunk past the tone loop with the samples held)
+    asm volatile("" : "+v"(e));
+    // c u, c v in double (rounded once, shared by the odd residues); the
+    // exact integer classes converted where a tone uses them
+    double cw[8][2];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        cw[i][0] = kC * (double)q[i][6];
+        cw[i][1] = kC * (double)q[i][7];
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    double best = -1.0, second = -1.0, mine = 0.0;
+    int arg = 0;
+#pragma unroll 1
+    for (int t = 0; t < K; ++t) {
+        // wave-uniform (an SGPR): the residue's branches below are uniform
+        const int rho = __builtin_amdgcn_readfirstlane((int)p.rot64[66 * K + t]);
+        const double c0 = p.rot64[64 * K + t];
+        const bool cplx = (rho & 3) != 0;
+        // opaque per tone: the odd residues' sums (d0 +- c u ...) are formed
+        // per tone, not hoisted out of the tone loop (64 more VGPRs)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+#pragma unroll
+            for (int c = 0; c < 6; ++c) asm volatile("" : "+v"(q[i][c]));
+            asm volatile("" : "+v"(cw[i][0]), "+v"(cw[i][1]));
+        }
+        auto yv = [&](int i, int c) { return c < 6 ? (double)q[i][c] : cw[i][c - 6]; };
+        double a1 = 0.0, a2 = 0.0, b1 = 0.0, b2 = 0.0;
+        auto step = [&](double yr, double yi) {
+            double sa = yr + c0 * a1;
+            sa = sa - a2;
+            a2 = a1;
+            a1 = sa;
+            double sb = yi + c0 * b1;
+            sb = sb - b2;
+            b2 = b1;
+            b1 = sb;
+        };
+        // (negations are exact and rounding is sign-symmetric: -(D2 + CV) is
+        // the bits of (-d2) - c v)
+        auto real = [&](int qc) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                double sa = yv(i, qc) + c0 * a1;
+                sa = sa - a2;
+                a2 = a1;
+                a1 = sa;
+            }
+        };
+        if (rho == 0) {
+            real(0);
+        } else if (rho == 4) {
+            real(1);
+        } else if (rho == 2) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) step(yv(i, 2), -yv(i, 3));
+        } else if (rho == 6) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) step(yv(i, 2), yv(i, 3));
+        } else if (rho == 1) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) step(yv(i, 4) + yv(i, 6), -(yv(i, 5) + yv(i, 7)));
+        } else if (rho == 3) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) step(yv(i, 4) - yv(i, 6), yv(i, 5) - yv(i, 7));
+        } else if (rho == 5) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) step(yv(i, 4) - yv(i, 6), -(yv(i, 5) - yv(i, 7)));
+        } else {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) step(yv(i, 4) + yv(i, 6), yv(i, 5) + yv(i, 7));
+        }
+        const double *r = p.rot64 + 4 * (t * 16 + seg);
+        double re, im;
+        if (cplx) {
+            const double t1 = r[0] * a1 - r[1] * b1, t2 = r[2] * a2 - r[3] * b2;
+            re = t1 - t2;
+            const double t3 = r[0] * b1 + r[1] * a1, t4 = r[2] * b2 + r[3] * a2;
+            im = t3 - t4;
+        } else {
+            re = r[0] * a1;
+            im = r[1] * a1;
+            re = re - r[2] * a2;
+            im = im - r[3] * a2;
+        }
+        re = row_sum16d(re);
+        im = row_sum16d(im);
+        const double pk = re * re + im * im;
+        if (pk > best) {
+            second = best;
+            best = pk;
+            arg = t;
+        } else if (pk > second) {
+            second = pk;
+        }
+        if (t == seg) mine = pk;
+    }
+    return seg_finish(p, w, live, seg, e, best, second, mine, arg);
+}
+
+// MODE = p.fold64 (0: by segments, dense runs at hop 64 H; 1: by the fold;
+// 2: by the residue fold), a template argument so that each form's registers
+// stay in its own kernel (by segments 109 VGPRs, by the fold 85, by the
+// residue fold 128)
+template <int MODE>
+__global__ __launch_bounds__(64 * kRescueSplit) __attribute__((amdgpu_waves_per_eu(4)))
+void rescue_seg_kernel(RescueParams p)
+{
+#pragma clang fp contract(off)
+    // per wave: its flagged windows (offsets from base), in order, and pass
+    // 1's list; dense runs (MODE 0): [segment][tone] {s1, s2} and [segment]
+    // fp32 sum x^2
+    constexpr int kL = MODE == 0 ? kRescueChunk : kRescueChunk / kRescueSplit;
+    constexpr int kD = MODE == 0 ? kSegStates : 1;
+    __shared__ unsigned short idx_w[kRescueSplit][kL];
+    __shared__ unsigned short left_w[kRescueSplit][kL];
+    __shared__ double2 sst_w[kRescueSplit][kD];
+    __shared__ float sen_w[kRescueSplit][(kD + 1) / 2];
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    unsigned short *idx = idx_w[wv], *left = left_w[wv];
+    double2 *sst = sst_w[wv];
+    float *sen = sen_w[wv];
+    // a block per 512-window chunk, kRescueSplit waves. With dense runs (hop =
+    // 64 H, H < 16) every wave scans the whole chunk (512 symbol bytes from
+    // L2) and takes every S-th run; otherwise each scans and works on its own
+    // 512 / S windows of it
+    constexpr int S = kRescueSplit;
+    const int sub = wv;
+    const int H = (MODE == 0 && p.hop % 64 == 0 && p.hop < 1024) ? (int)(p.hop / 64) : 0;
+    const int len = H > 0 ? kRescueChunk : kRescueChunk / S;
+    const long long base = tile_block(1) * kRescueChunk + (H > 0 ? 0 : sub * len);
+    if (base >= p.n_windows) return;
+    const int span = (int)min((long long)len, p.n_windows - base);
+    // (buffer loads bounded by span: nothing past the last window is read,
+    // a last dword cut by the bound reads as 0, its bytes one by one)
     __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc((void *)(p.sym + base), (short)0, span, 0x00020000);
     unsigned any = 0;
     if (p.sym_aligned4) {
-#pragma unroll
-        for (int c = 0; c < kRescueChunk / 256; ++c)
+#pragma unroll 1
+        for (int c = 0; 256 * c < len; ++c)
             any |= __builtin_amdgcn_raw_buffer_load_b32(rs, (64 * c + lane) * 4, 0, 0) & 0x80808080u;
         if (lane < (span & 3)) any |= __builtin_amdgcn_raw_buffer_load_b8(rs, (span & ~3) + lane, 0, 0) & 0x80u;
     } else {
-        for (int c = 0; c < kRescueChunk / 64; ++c)
+#pragma unroll 1
+        for (int c = 0; 64 * c < len; ++c)
             any |= __builtin_amdgcn_raw_buffer_load_b8(rs, 64 * c + lane, 0, 0) & 0x80u;
     }
     if (__ballot(any != 0) == 0) return;
     int T = 0;
-    for (int i = 0; i < kRescueChunk / 64; ++i) {
+    for (int i = 0; 64 * i < len; ++i) {
         const int o = 64 * i + lane;
         const bool f = o < span && (p.sym[base + o] & kSymAmbiguous);
         const unsigned long long b = __ballot(f);
@@ -357,7 +548,6 @@ __global__ __launch_bounds__(64) void rescue_seg_kernel(RescueParams p)
     // dense runs (hop = 64 H, H < 16): runs of R windows, ((R - 1) H + 16) K
     // end states in LDS
     // (by the fold every window's pass 0 is 8 steps per lane and tone: no runs)
-    const int H = (!p.fold64 && p.hop % 64 == 0 && p.hop < 1024) ? (int)(p.hop / 64) : 0;
     int Ts = T;  // windows for the per-window pass: idx[0 .. Ts)
     if (H > 0) {
         // the run length with the most windows per lane pass of the segment
@@ -372,7 +562,7 @@ __global__ __launch_bounds__(64) void rescue_seg_kernel(RescueParams p)
             }
         }
         Ts = 0;
-        int i = 0;
+        int i = 0, run = 0;
 #pragma unroll 1
         while (i < T) {
             const int rb = (idx[i] / R) * R;
@@ -391,6 +581,11 @@ __global__ __launch_bounds__(64) void rescue_seg_kernel(RescueParams p)
                 if (cnt == 0) printf("RS cnt 0 at i %d T %d rb %d R %d\n", i, T, rb, R);
             }
 #endif
+            // run run % S is this sub-block's (the others skip it)
+            if (run++ % S != sub) {
+                i += cnt;
+                continue;
+            }
             if (cnt * 16 <= segs) {
                 // sparse: to the per-window pass (Ts <= i: the read is done
                 // before the write)
@@ -458,7 +653,14 @@ __global__ __launch_bounds__(64) void rescue_seg_kernel(RescueParams p)
         long long w = base + o;
         RS_CHECK(w, p.n_windows, "per-window w");
         bool still;
-        if (p.fold64) {
+        if constexpr (MODE == 2) {
+            still = seg_residue_window(p, w, live, seg);
+            const unsigned long long lb = __ballot(live && still && seg == 0);
+            if (live && still && seg == 0) left[Tl + __popcll(lb & ((1ull << lane) - 1))] = (unsigned short)o;
+            Tl += __popcll(lb);
+            continue;
+        }
+        if constexpr (MODE == 1) {
             // rescue_rows_fold0's arithmetic: lane seg's folded samples
             // 8 seg .. + 7 (samples 128 m + 8 seg + i, m < 8), 8-step chains
             const int16_t *xs = p.pcm + w * p.hop + 8 * seg;
@@ -483,6 +685,7 @@ __global__ __launch_bounds__(64) void rescue_seg_kernel(RescueParams p)
             // the folded samples converted once (exact); the tones' chains two
             // at a time (independent chains interleaved), then each tone's
             // rotation, sums and argmax step exactly as seg_decide's
+            asm volatile("" : "+v"(e));  // done here, not sunk past the tone loop
             double xd[8];
 #pragma unroll
             for (int i = 0; i < 8; ++i) xd[i] = (double)xf[i];
@@ -599,7 +802,15 @@ hipError_t launch_rescue(const RescueParams &p, hipStream_t s)
     const long long blocks = (p.n_windows + kRescueChunk - 1) / kRescueChunk;
     if (blocks > 0x7FFFFFFFLL) return hipErrorInvalidValue;
     if (p.n == 1024 && p.rot64 && p.t2e64 > 0.0)
-        hipLaunchKernelGGL(rescue_seg_kernel, dim3((unsigned)blocks), dim3(64), 0, s, p);
+    {
+        const dim3 grid((unsigned)blocks), block(64 * kRescueSplit);
+        if (p.fold64 == 2)
+            hipLaunchKernelGGL(rescue_seg_kernel<2>, grid, block, 0, s, p);
+        else if (p.fold64 == 1)
+            hipLaunchKernelGGL(rescue_seg_kernel<1>, grid, block, 0, s, p);
+        else
+            hipLaunchKernelGGL(rescue_seg_kernel<0>, grid, block, 0, s, p);
+    }
     else
         hipLaunchKernelGGL(rescue_kernel, dim3((unsigned)blocks), dim3(64), 0, s, p);
     return hipGetLastError();

@@ -80,7 +80,7 @@ def test_plans(A, O, torch, plan, H):
     band edges."""
     freqs = getattr(A, plan) if hasattr(A, plan) else globals()[plan]
     # (K = 16 on integer bins above hop 384: AUTO takes the residue detector,
-    # windows one by one, its rescue in the kernel)
+    # windows one by one, pass 0 by the residue fold in this launch)
     run(A, O, freqs, 64 * H, 2 * 512 + 301, seed=100 + H,
         expect_slide=not (plan == "K16" and 64 * H > 384))
 
@@ -89,6 +89,8 @@ FOLD16 = tuple(EM.BIN * 8 * (2 + i) for i in range(16))      # 16 tones on multi
 FOLD13 = FOLD16[:13]
 FOLD12 = FOLD16[:12]
 FFT_ODD = tuple(EM.BIN * (33 + 7 * i) for i in range(4))      # FFT bins not multiples of 8
+ODD8 = tuple(EM.BIN * (32 + 9 * i) for i in range(8))         # residues 0 .. 7
+EDGES4 = (1 * EM.BIN, 2 * EM.BIN, 511 * EM.BIN, 510 * EM.BIN)  # residues 1, 2, 7, 6
 
 
 @pytest.mark.parametrize("plan,method,fold64", [
@@ -98,11 +100,15 @@ FFT_ODD = tuple(EM.BIN * (33 + 7 * i) for i in range(4))      # FFT bins not mul
     ("FOLD16", 2, 0),    # FFT, bins on multiples of 8 but K > 12: by segments
     ("FOLD12", 2, 1),    # FFT by the fold
     ("FFT_ODD", 2, 0),   # FFT, odd bins: by segments
+    ("ODD8", 4, 2),      # residue detector: by the residue fold, every residue class
+    ("EDGES4", 4, 2),    # the band edges, complex classes only
+    ("FOLD16", 4, 2),    # K = 16, residue 0 only (real chains)
 ])
 @pytest.mark.parametrize("hop", [1024, 256])
 def test_pass0_forms(A, O, torch, plan, method, fold64, hop):
     """Each form of the first pass the plan selects (plan.h fold64: by the
-    fold at K <= 12 on multiples of 8 bins, else by 64-sample segments; in the
+    fold at K <= 12 on multiples of 8 bins, by the residue fold on the residue
+    detector, else by 64-sample segments; in the
     detector kernel at hop = n, in the rescue launch of segment-shared windows
     at hop 256, in the FFT kernel) on runs of near ties: every symbol the
     oracle's, no flag left."""

@@ -216,3 +216,94 @@ def test_fold_pass0_error_model(A, O, plan):
         r = _check(pass0_fold_powers(x, info, K), ref_sym, ref_P, x, m)
         worst = max(worst, (r, fam))
     print(f"\nfold {plan}: rho_first {m['rho_first']:.3g}, worst error {worst[0]:.3g} of it ({worst[1]})")
+
+
+# residue detector plans (integer bins, not all multiples of 8; plan.h fold64
+# = 2): pass 0 by the residue fold (rescue.hip seg_residue_window), every
+# residue class 0 .. 7 and the band edges
+RESIDUE_PLANS = {
+    "odd8": tuple((32 + 9 * i) * BIN for i in range(8)),        # residues 0, 1, ..., 7
+    "edges4": (1 * BIN, 2 * BIN, 511 * BIN, 510 * BIN),         # residues 1, 2, 7, 6
+    "k16": tuple((20 + 7 * i) * BIN for i in range(16)),
+    "nyq_dc": (0.0, 4 * BIN, 508 * BIN, 512 * BIN),             # residues 0, 4, 4, 0 (real Y)
+}
+KC = 0.70710678118654752440
+
+
+def pass0_residue_powers(x, info, K):
+    """Pass 0 by the residue fold of W windows x[W][1024] (int16), operation
+    for operation: lane j's samples x[128 m + 8 j + i], the exact integer
+    butterflies a_m = x_m + x_{m+4}, d_m = x_m - x_{m+4}, Y_rho (odd rho: d0
+    +- c u, +-d2 +- c v, each product and sum rounded once), the real and
+    imaginary 8-step chains at the exact bin, the complex rotation, the
+    16-lane butterfly, the power."""
+    W = x.shape[0]
+    r = info["rot64"]
+    rot = r[:64 * K].reshape(K, 16, 4)
+    xs = x.astype(np.int64).reshape(W, 8, 16, 8)               # [w][m][j][i]
+    a = [xs[:, m] + xs[:, m + 4] for m in range(4)]            # [w][j][i], exact
+    d = [xs[:, m] - xs[:, m + 4] for m in range(4)]
+    P = np.empty((W, K))
+    for k in range(K):
+        c = r[64 * K + k]
+        rho = int(r[66 * K + k])
+        if rho in (0, 4):
+            sg = 1 if rho == 0 else -1
+            yr, yi = ((a[0] + a[2]) + sg * (a[1] + a[3])).astype(np.float64), None
+        elif rho in (2, 6):
+            sg = -1 if rho == 2 else 1
+            yr = (a[0] - a[2]).astype(np.float64)
+            yi = (sg * (a[1] - a[3])).astype(np.float64)
+        else:
+            cu = KC * (d[1] - d[3]).astype(np.float64)
+            cv = KC * (d[1] + d[3]).astype(np.float64)
+            d0 = d[0].astype(np.float64)
+            d2 = ((-1 if rho in (1, 5) else 1) * d[2]).astype(np.float64)
+            yr = d0 + cu if rho in (1, 7) else d0 - cu
+            yi = d2 - cv if rho in (1, 3) else d2 + cv
+
+        def chain(y):
+            s1 = np.zeros((W, 16))
+            s2 = np.zeros((W, 16))
+            for i in range(8):
+                s = y[:, :, i] + c * s1
+                s = s - s2
+                s2, s1 = s1, s
+            return s1, s2
+        a1, a2 = chain(yr)
+        R = rot[k]
+        if yi is None:
+            re = R[:, 0] * a1
+            im = R[:, 1] * a1
+            re = re - R[:, 2] * a2
+            im = im - R[:, 3] * a2
+        else:
+            b1, b2 = chain(yi)
+            re = (R[:, 0] * a1 - R[:, 1] * b1) - (R[:, 2] * a2 - R[:, 3] * b2)
+            im = (R[:, 0] * b1 + R[:, 1] * a1) - (R[:, 2] * b2 + R[:, 3] * a2)
+        re = butterfly_sum16(re)
+        im = butterfly_sum16(im)
+        P[:, k] = re * re + im * im
+    return P
+
+
+@pytest.mark.parametrize("plan", sorted(RESIDUE_PLANS))
+def test_residue_pass0_error_model(A, O, plan):
+    freqs = RESIDUE_PLANS[plan]
+    cfg = A.make_cfg(freqs=freqs, method=A.METHOD_RESIDUE)
+    info = A.plan_info(cfg)
+    assert info["method"] == A.METHOD_RESIDUE and info["fold64"] == 2
+    K = len(freqs)
+    bins = [round(f / BIN) for f in freqs]
+    assert np.array_equal(info["rot64"][66 * K:67 * K], [b % 8 for b in bins])
+    assert np.array_equal(info["rot64"][65 * K:66 * K], info["rcoef"])
+    m = A.error_model(cfg)
+    assert m["rho_first"] > 0
+    worst = (0.0, None)
+    for fi, fam in enumerate(EM.FAMILIES):
+        W = 384
+        x = EM.family(fam, freqs, N, W, seed=400 + fi).reshape(W, N)
+        ref_sym, ref_P = O.goertzel(x, freqs, N, fs=FS, threads=4)
+        r = _check(pass0_residue_powers(x, info, K), ref_sym, ref_P, x, m)
+        worst = max(worst, (r, fam))
+    print(f"\nresidue {plan}: rho_first {m['rho_first']:.3g}, worst error {worst[0]:.3g} of it ({worst[1]})")
