@@ -129,6 +129,7 @@ class DemodPlanInfo(ctypes.Structure):
         ("rot_len", ctypes.c_uint32),
         ("rot64_len", ctypes.c_uint32),
         ("fold64", ctypes.c_int32),
+        ("fft_pmask", ctypes.c_uint32),
     ]
 
 

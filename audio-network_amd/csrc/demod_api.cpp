@@ -39,6 +39,7 @@ struct demod {
     int *d_bins = nullptr;
     int fft_bins[kMaxTones] = {};  // FFT detector: tone bins round(f n / fs)
     int fft_slot[kMaxTones] = {};  // FFT detector: where each tone bin's power sits (fft_quad_slot)
+    unsigned fft_pmask = 0xFFu;    // tones only: the post-pass pair blocks holding a tone (fft_quad_pmask)
     // decision rescue (rescue.hip)
     bool rescue = false;        // K >= 2 and not switched off (FSKD_NO_RESCUE=1)
     bool rescue_launch = true;  // FSKD_NO_RESCUE=flags: flag only, no rescue launch (diagnostics)
@@ -190,6 +191,9 @@ static int init_device_state(demod_t *st)
             st->fft_bins[k] = pl.fft_bins[k];
             st->fft_slot[k] = pl.fft_slot[k];
         }
+        // FSKD_FFT_PMASK=0 (measurement): the full post-pass on tones-only batches
+        const char *pm_env = std::getenv("FSKD_FFT_PMASK");
+        st->fft_pmask = pm_env && std::strcmp(pm_env, "0") == 0 ? 0xFFu : fft_quad_pmask(bins.data(), (int)c.k);
         // the rescue's radix-2 twiddles: stage len (2 .. n), j < len / 2 at
         // len / 2 - 1 + j, each the (cos, sin) of (-2 pi / len) j exactly as
         // the double FFT of the definition evaluates it (one libm sincos of
@@ -513,6 +517,7 @@ static int enqueue_fft(demod_t *st, const int16_t *d_pcm, size_t n_windows, uint
     p.tw1024 = st->d_tw1024;
     p.bins = st->d_bins;
     for (uint32_t k = 0; k < st->cfg.k; ++k) p.slot[k] = st->fft_slot[k];
+    p.pmask = st->fft_pmask;
     p.sym = d_sym;
     p.mag = d_mag;
     p.spec = d_spec;

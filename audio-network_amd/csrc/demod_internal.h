@@ -524,6 +524,12 @@ struct FftParams {
     const float *tw1024;     // [512][2]  e^{-2 pi i k / 1024}
     const int *bins;         // [k] tone bins round(f n / fs), device
     int slot[kMaxTones];     // fft_quad_slot(bin) of each tone (quad2 register pick)
+    // tones only: bit jb set = the post-pass pair block jb (pairs 2 jb and
+    // 2 jb + 1 of every lane) holds some tone bin; 0xFF: every block (the
+    // full post-pass, stage 2's energy by Parseval of the bin powers), else
+    // only those blocks (PICK 2) and stage 2's energy n sum x^2 from the
+    // samples (fft_quad_pmask; FSKD_FFT_PMASK=0: every block, measurement)
+    unsigned pmask;
     uint8_t *sym;
     float *mag;              // [n_windows][k] or nullptr
     float *spec;             // [n_windows][513] or nullptr
@@ -590,6 +596,7 @@ hipError_t synth_prepare();  // upload the sine table to the current device (onc
 hipError_t launch_synth(const SynthParams &p, hipStream_t s);
 hipError_t launch_read_ceiling(const int16_t *p, long long n_bytes, hipStream_t s);
 hipError_t launch_fft_quad(const FftParams &p, hipStream_t s);  // 16 lanes / window (fft_quad.hip)
+unsigned fft_quad_pmask(const int *bins, int k);  // FftParams::pmask of a tone plan
 int fft_quad_slot(int bin);  // where fft_quad keeps |X[bin]|^2: 2 (16 j + t) + half, or 512 / 513 (bins 0 / 512)
 // ip.proto framing of [n_streams][n] symbols, one frame run per stream (frame_gpu.hip)
 long long frame_streams_size(long long n, int bits, long long max_payload, unsigned *per,

@@ -968,7 +968,10 @@ void error_model(const demod_cfg_t &c, const Plan &pl, bool first_pass, ErrModel
     if (fft) {
         // E = Parseval's 2 sum_{b<=512} P_b >= n sum x^2 (1 - 2e-4): the fp32
         // powers' norm-wise error is below rho_det sqrt(513) ||x|| against
-        // ||X|| >= sqrt(n / 2) ||x||
+        // ||X|| >= sqrt(n / 2) ||x||. (Tones-only batches whose tone bins
+        // leave post-pass pair blocks unused skip those blocks and form E =
+        // n sum x^2 from the samples instead: fft_quad.hip PICK 2, a 64-term
+        // sum per lane and the 16-lane tree, within the 100 u above.)
         const ld rho = det + ref;
         t2e = 16.0L * rho * rho / (ld)n * safe / (1.0L - 2e-4L);
         emax = (ld)n * xmax2;
@@ -1076,6 +1079,7 @@ extern "C" int demod_plan_info(const demod_cfg_t *cfg, demod_plan_info_t *info, 
     info->rot_len = (uint32_t)pl.rot.size();
     info->rot64_len = (uint32_t)pl.rot64.size();
     info->fold64 = pl.fold64;
+    info->fft_pmask = pl.detector == fskd::kDetFft ? fskd::fft_quad_pmask(pl.fft_bins, (int)cfg->k) : 0u;
     if (rot && rot_cap >= 4 * pl.rot.size())
         std::memcpy(rot, pl.rot.data(), pl.rot.size() * sizeof(float4));
     if (rot64 && rot64_cap >= pl.rot64.size())

@@ -985,6 +985,13 @@ __device__ __attribute__((always_inline)) inline void fft1024_quad_body(const Ff
         f32x32 pv;
         static_for<0, 8>([&](auto jc) {
             constexpr int j0 = 2 * decltype(jc)::value, j1 = j0 + 1;
+            f2 pw0, pw1;  // (|X[kP]|^2, |X[512-kP]|^2)
+            // PICK 2: only the pair blocks holding a tone bin (p.pmask,
+            // wave-uniform: a scalar branch per block; the skipped blocks'
+            // powers are undefined and never read, and only their values,
+            // not the power tuple, merge at the branch)
+            const bool need = SPEC || PICK != 2 || ((p.pmask >> decltype(jc)::value) & 1u);
+            if (need) {
             f2 P0 = b[j0], Q0 = b[16 + 15 - j0];
             f2 P1 = b[j1], Q1 = b[16 + 15 - j1];
             // lane 0 (columns 0 and 16): pairs j < 8 are column 16's
@@ -998,7 +1005,6 @@ __device__ __attribute__((always_inline)) inline void fft1024_quad_body(const Ff
                 Q0 = sel_l0(b[16 - j0], Q0);
                 Q1 = sel_l0(b[16 - j1], Q1);
             }
-            f2 pw0, pw1;  // (|X[kP]|^2, |X[512-kP]|^2)
             f2 w0, w1;
             if constexpr (RD >= 2) {
                 const f4 x = *reinterpret_cast<const f4 *>(&tw3[tw3_at(j0, t)]);
@@ -1030,6 +1036,7 @@ __device__ __attribute__((always_inline)) inline void fft1024_quad_body(const Ff
                 const f2 re0 = pp_re_h(S0, T0), re1 = pp_re_h(S1, T1);
                 const f2 im0 = pp_im_h(S0, T0), im1 = pp_im_h(S1, T1);
                 pwr2(pw0, re0, im0, pw1, re1, im1);
+            }
             }
             if constexpr (SPEC && SPL) {
                 const int a = j0 < 8 ? spl_a_lo : spl_a_hi, m = j0 < 8 ? spl_m_lo : spl_m_hi;
@@ -1072,7 +1079,7 @@ __device__ __attribute__((always_inline)) inline void fft1024_quad_body(const Ff
             // SPL: the fenced lane id again, so the store address is formed
             // here rather than held across the loop
             if (live && t < p.k && p.mag) p.mag[w * p.k + (SPL ? tt : t)] = pk;
-        } else if constexpr (PICK == 1) {
+        } else if constexpr (PICK == 1 || PICK == 2) {
             // 5. tone pick, gathered: tone i's power (register slot and lane
             //    from its uniform slot, as below) is read across the row with
             //    one ds_bpermute into lane t = i, so lanes t < K end holding
@@ -1134,6 +1141,21 @@ __device__ __attribute__((always_inline)) inline void fft1024_quad_body(const Ff
                 for (int i = tl2 & 15; i < 513; i += 16) e += row[i];
             } else if constexpr (SPEC) {
                 for (int i = t; i < 513; i += 16) e += pq[quad_slot(i)];
+            } else if constexpr (PICK == 2) {
+                // not every bin's power exists here: n sum x^2 from the
+                // window's samples, read again (L2; only waves stage 1
+                // flagged), lane t's 64 (dwords t + 16 n1)
+                if (live) {
+                    const uint32_t *src = reinterpret_cast<const uint32_t *>(p.pcm + w * p.hop) + t;
+#pragma unroll
+                    for (int n1 = 0; n1 < 32; ++n1) {
+                        const uint32_t d = src[16 * n1];
+                        const float lo = (float)(int16_t)(d & 0xFFFFu), hi = (float)(int16_t)(d >> 16);
+                        e = __builtin_fmaf(lo, lo, e);
+                        e = __builtin_fmaf(hi, hi, e);
+                    }
+                }
+                return 1024.f * row_sum16(e);
             } else {
                 f2 a = {0.f, 0.f};
 #pragma unroll
@@ -1372,15 +1394,30 @@ hipError_t launch_fft_quad_t(const FftParams &p, hipStream_t s)
 hipError_t launch_fft_quad(const FftParams &p, hipStream_t s)
 {
     const bool lin = p.spec && ((uintptr_t)p.spec & 15) == 0;
-    if (p.hop < 1024)
-        return lin ? launch_fft_quad_t<4, 4, 0, true, false, 0, 4, 0, 2>(p, s)
-             : p.spec ? launch_fft_quad_t<4, 4, 0, true, false, 0, 4>(p, s)
-                      : launch_fft_quad_t<4, 4, 0, false, false, 0, 4, 0, 0, 0, 0, 1, 1>(p, s);
-    return lin ? launch_fft_quad_t<4, 4, 0, true, false, 2, 4, 0, 2>(p, s)
-         : p.spec ? launch_fft_quad_t<4, 4, 0, true, false, 2, 4>(p, s)
-                  : launch_fft_quad_t<4, 4, 0, false, false, 2, 4, 0, 0, 0, 0, 1, 1>(p, s);
+    if (p.hop < 1024) {
+        if (lin) return launch_fft_quad_t<4, 4, 0, true, false, 0, 4, 0, 2>(p, s);
+        if (p.spec) return launch_fft_quad_t<4, 4, 0, true, false, 0, 4>(p, s);
+        return p.pmask == 0xFFu ? launch_fft_quad_t<4, 4, 0, false, false, 0, 4, 0, 0, 0, 0, 1, 1>(p, s)
+                                : launch_fft_quad_t<4, 4, 0, false, false, 0, 4, 0, 0, 0, 0, 1, 2>(p, s);
+    }
+    if (lin) return launch_fft_quad_t<4, 4, 0, true, false, 2, 4, 0, 2>(p, s);
+    if (p.spec) return launch_fft_quad_t<4, 4, 0, true, false, 2, 4>(p, s);
+    return p.pmask == 0xFFu ? launch_fft_quad_t<4, 4, 0, false, false, 2, 4, 0, 0, 0, 0, 1, 1>(p, s)
+                            : launch_fft_quad_t<4, 4, 0, false, false, 2, 4, 0, 0, 0, 0, 1, 2>(p, s);
 }
 
 int fft_quad_slot(int bin) { return quad_slot(bin); }
+
+// The post-pass pair blocks (pairs 2 jb, 2 jb + 1) the tone bins sit in
+// (quad_slot: pair j = slot >> 5; bins 0 and 512 come from Z[0] on the side)
+unsigned fft_quad_pmask(const int *bins, int k)
+{
+    unsigned m = 0;
+    for (int i = 0; i < k; ++i) {
+        const int f = quad_slot(bins[i]);
+        if (f < 512) m |= 1u << ((f >> 5) >> 1);
+    }
+    return m;
+}
 
 }  // namespace fskd

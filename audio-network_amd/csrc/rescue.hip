@@ -487,7 +487,7 @@ __device__ __forceinline__ bool seg_residue_window(const RescueParams &p, long l
 // stay in its own kernel (by segments 109 VGPRs, by the fold 85, by the
 // residue fold 128)
 template <int MODE>
-__global__ __launch_bounds__(64 * kRescueSplit) __attribute__((amdgpu_waves_per_eu(4)))
+__global__ __launch_bounds__(64 * kRescueSplit) __attribute__((amdgpu_waves_per_eu(MODE == 0 ? 3 : 4)))
 void rescue_seg_kernel(RescueParams p)
 {
 #pragma clang fp contract(off)

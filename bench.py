@@ -782,8 +782,18 @@ def run_config(A, D, torch, dist, args, config, rank, world, local, use_dist, st
     if config == "fft":
         # the FFT is reported against the VALU roof too.
         # Algorithmic flops per window: 2.5 N log2 N for the real N-point
-        # FFT + 3 per |X[b]|^2 over the N/2+1 bins.
-        fpw = 2.5 * n * 10 + 3 * (n // 2 + 1)
+        # FFT + 3 per |X[b]|^2 over the N/2+1 bins. Tones only, the kernel
+        # runs the real split's post-pass only in the pair blocks holding a
+        # tone bin (plan fft_pmask, m of 8 blocks: 64 m bins): then the
+        # 512-point complex FFT's 5 (N/2) log2 (N/2) plus m/8 of the post-pass
+        # (2.5 N log2 N - 5 (N/2) log2 (N/2) = 2560) and 3 per bin evaluated.
+        pm = (A.plan_info(cfg)["fft_pmask"]
+              if d_spec is None and os.environ.get("FSKD_FFT_PMASK") != "0" else 0xFF)
+        m_blk = bin(pm & 0xFF).count("1")
+        if m_blk == 8:
+            fpw = 2.5 * n * 10 + 3 * (n // 2 + 1)
+        else:
+            fpw = 5 * (n // 2) * 9 + (2.5 * n * 10 - 5 * (n // 2) * 9 + 3 * (n // 2)) * m_blk / 8
         tf = fpw * n_eval / (kernel_ms / 1e3) / 1e12
         tf50 = fpw * n_eval / (kernel_p50 / 1e3) / 1e12
         r["roofline_valu"] = {"bound": "valu", "achieved": round(tf, 2),
@@ -791,7 +801,8 @@ def run_config(A, D, torch, dist, args, config, rank, world, local, use_dist, st
                               "frac": round(tf / VALU_PEAK_TFLOPS, 4),
                               "achieved_p50": round(tf50, 2),
                               "frac_p50": round(tf50 / VALU_PEAK_TFLOPS, 4),
-                              "flop_per_window": fpw}
+                              "flop_per_window": fpw,
+                              "post_pass_blocks": m_blk}
     if sustain_s > 0 and not use_dist:
         # the same step back to back for sustain_s seconds (synchronised every
         # 256 steps): the steady rate over seconds rather than milliseconds,

@@ -242,9 +242,15 @@ typedef struct demod_plan_info {
     double   rcoef[DEMOD_MAX_TONES];
     uint32_t rot_len;       /* float4 entries of rot */
     uint32_t rot64_len;     /* doubles of rot64 */
-    int32_t  fold64;        /* pass 0 by the fold: rot64 rows are lane j's folded
-                             * positions 8j .. 8j + 7 at the exact bins (fold
-                             * detector plans), else lane j's raw samples 64j .. */
+    int32_t  fold64;        /* pass 0's form: 1 = by the fold (rot64 rows are lane
+                             * j's folded positions 8j .. 8j + 7 at the exact
+                             * bins; fold detector plans), 2 = by the residue
+                             * fold (residue detector plans, in the rescue
+                             * launch), 0 = lane j's raw samples 64j .. */
+    uint32_t fft_pmask;     /* FFT detector, tones only: bit jb = the real-split
+                             * post-pass pair block jb (pairs 2jb, 2jb + 1 of
+                             * every lane) holds a tone bin; only those blocks
+                             * run (0xFF: all, the full spectrum's post-pass) */
 } demod_plan_info_t;
 int demod_plan_info(const demod_cfg_t *cfg, demod_plan_info_t *info, float *rot, size_t rot_cap,
                     double *rot64, size_t rot64_cap);
