@@ -694,11 +694,13 @@ def test_batch_launch_slices(A, O, torch, monkeypatch, mode, plan):
     sym = torch.empty(W, dtype=torch.uint8, device="cuda")
     mag = torch.empty((W, 8), dtype=torch.float32, device="cuda")
     with A.Demodulator(cfg) as d:
-        # detector launches only: fold and residue re-decide their flagged
-        # windows inside the detector at n = 1024 (round 4)
-        assert d.batch_launches(W, mags=True) == (4 if mode == "slices" else 1)
-        assert d.batch_launches(W, mags=False) == 1
-        assert d.batch_launches(1 << 18, mags=True) == 1
+        # detector launches, + the rescue launch for the residue detector's
+        # plans (round 5: pass 0 by the residue fold lives there); the fold
+        # detector re-decides its flagged windows inside its own kernel
+        r = 1 if plan == "odd" else 0
+        assert d.batch_launches(W, mags=True) == (4 if mode == "slices" else 1) + r
+        assert d.batch_launches(W, mags=False) == 1 + r
+        assert d.batch_launches(1 << 18, mags=True) == 1 + r
         d.batch_device(d_pcm, W, sym, mag)
         ref_sym = torch.empty_like(sym)
         ref_mag = torch.empty_like(mag)
