@@ -989,7 +989,10 @@ __device__ __attribute__((always_inline)) inline void fft1024_quad_body(const Ff
             // PICK 2: only the pair blocks holding a tone bin (p.pmask,
             // wave-uniform: a scalar branch per block; the skipped blocks'
             // powers are undefined and never read, and only their values,
-            // not the power tuple, merge at the branch)
+            // not the power tuple, merge at the branch). The empty asm
+            // defines them without an instruction (left undefined, the
+            // compiler zeroed them: 4 v_mov per block, executed or not)
+            if constexpr (!SPEC && PICK == 2) asm volatile("" : "=v"(pw0), "=v"(pw1));
             const bool need = SPEC || PICK != 2 || ((p.pmask >> decltype(jc)::value) & 1u);
             if (need) {
             f2 P0 = b[j0], Q0 = b[16 + 15 - j0];
