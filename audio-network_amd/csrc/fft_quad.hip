@@ -1393,7 +1393,11 @@ hipError_t launch_fft_quad_t(const FftParams &p, hipStream_t s)
 // profiles/round2/spec_lin/).
 // Tones only: the gathered tone pick (PICK 1), -1.8 % at hop 256 and -1.7 %
 // at hop 1024 against the per-lane register pick, identical outputs
-// (profiles/round3/r3s/).
+// (profiles/round3/r3s/); round 5: only the post-pass blocks holding a tone
+// bin (PICK 2, -13 %), with round 1 of the transpose overlapping column 0's
+// DFT-16 (OVL: within +-0.5 % on the full post-pass, -2.7 % once the VALU
+// stream had shrunk; the twiddles from registers, TW3R, another -1 % but
+// other bits than the table's, not taken; profiles/round5/r5zp/).
 hipError_t launch_fft_quad(const FftParams &p, hipStream_t s)
 {
     const bool lin = p.spec && ((uintptr_t)p.spec & 15) == 0;
@@ -1401,12 +1405,12 @@ hipError_t launch_fft_quad(const FftParams &p, hipStream_t s)
         if (lin) return launch_fft_quad_t<4, 4, 0, true, false, 0, 4, 0, 2>(p, s);
         if (p.spec) return launch_fft_quad_t<4, 4, 0, true, false, 0, 4>(p, s);
         return p.pmask == 0xFFu ? launch_fft_quad_t<4, 4, 0, false, false, 0, 4, 0, 0, 0, 0, 1, 1>(p, s)
-                                : launch_fft_quad_t<4, 4, 0, false, false, 0, 4, 0, 0, 0, 0, 1, 2>(p, s);
+                                : launch_fft_quad_t<4, 4, 0, false, false, 0, 4, 0, 0, 1, 0, 1, 2>(p, s);
     }
     if (lin) return launch_fft_quad_t<4, 4, 0, true, false, 2, 4, 0, 2>(p, s);
     if (p.spec) return launch_fft_quad_t<4, 4, 0, true, false, 2, 4>(p, s);
     return p.pmask == 0xFFu ? launch_fft_quad_t<4, 4, 0, false, false, 2, 4, 0, 0, 0, 0, 1, 1>(p, s)
-                            : launch_fft_quad_t<4, 4, 0, false, false, 2, 4, 0, 0, 0, 0, 1, 2>(p, s);
+                            : launch_fft_quad_t<4, 4, 0, false, false, 2, 4, 0, 0, 1, 0, 1, 2>(p, s);
 }
 
 int fft_quad_slot(int bin) { return quad_slot(bin); }
