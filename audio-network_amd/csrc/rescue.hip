@@ -240,6 +240,12 @@ __device__ __forceinline__ void seg_pair(u32x4q (&v)[8], double c0, double c1, d
     }
 }
 
+// A lane's sum x^2 over its 64 samples (8 x 16 bytes): per dword the exact
+// x_lo^2 + x_hi^2 by one v_dot2_i32_i16 (clamped: only (-32768, -32768)
+// reaches 2^31, read as 2^31 - 1), converted and summed in fp32 — 3
+// instructions per 2 samples instead of 4, relative error < 36 u for the 32
+// non-negative terms (error_model.cpp's E allows 100 u)
+typedef short rs_short2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ float seg_energy64(const u32x4q (&v)[8])
 {
     float e = 0.f;
@@ -247,11 +253,10 @@ __device__ __forceinline__ float seg_energy64(const u32x4q (&v)[8])
     for (int q = 0; q < 8; ++q) {
         const unsigned d4[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const float xf = (float)(short)((d4[i >> 1] >> (16 * (i & 1))) & 0xFFFFu);
-            e = __builtin_fmaf(xf, xf, e);
+        for (int c = 0; c < 4; ++c) {
+            const rs_short2 s = __builtin_bit_cast(rs_short2, d4[c]);
+            e += (float)__builtin_amdgcn_sdot2(s, s, 0, true);
         }
-        __builtin_amdgcn_sched_barrier(0);
     }
     return e;
 }
@@ -358,16 +363,13 @@ __device__ __forceinline__ bool seg_residue_window(const RescueParams &p, long l
     const double kC = 0.70710678118654752440;
     // class values as exact integers, pair (m, m + 4) by pair (the pair's
     // samples die with it), then converted position by position
-    float e = 0.f;
+    float e = seg_energy64(v);
     int q[8][8];
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             const int xl = smp(m, i), xh = smp(m + 4, i);
-            const float fl = (float)xl, fh = (float)xh;
-            e = __builtin_fmaf(fl, fl, e);
-            e = __builtin_fmaf(fh, fh, e);
             const int am = xl + xh, dm = xl - xh;
             int *c = q[i];
             if (m == 0) {
@@ -668,19 +670,14 @@ void rescue_seg_kernel(RescueParams p)
 #pragma unroll
             for (int m = 0; m < 8; ++m) v[m] = *reinterpret_cast<const u32x4q *>(xs + 128 * m);
             int xf[8];
-            float e = 0.f;
+            float e = seg_energy64(v);
 #pragma unroll
             for (int i = 0; i < 8; ++i) xf[i] = 0;
 #pragma unroll
             for (int m = 0; m < 8; ++m) {
                 const unsigned d4[4] = {v[m].x, v[m].y, v[m].z, v[m].w};
 #pragma unroll
-                for (int i = 0; i < 8; ++i) {
-                    const int x = (int)(short)((d4[i >> 1] >> (16 * (i & 1))) & 0xFFFFu);
-                    xf[i] += x;
-                    const float xv = (float)x;
-                    e = __builtin_fmaf(xv, xv, e);
-                }
+                for (int i = 0; i < 8; ++i) xf[i] += (int)(short)((d4[i >> 1] >> (16 * (i & 1))) & 0xFFFFu);
             }
             // the folded samples converted once (exact); the tones' chains two
             // at a time (independent chains interleaved), then each tone's
