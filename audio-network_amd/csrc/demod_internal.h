@@ -333,6 +333,22 @@ __device__ __forceinline__ long long tile_block(int swz)
 // derived for this sequence, error_model.cpp first_pass_fold_rho). 8x fewer
 // double steps than 64 raw samples per lane per tone. Returns amb_row after
 // it (the rows left to the exact chains).
+// x_lo^2 + x_hi^2 of 4 dwords (8 int16 samples): exact per dword by
+// v_dot2_i32_i16 (clamped, only (-32768, -32768) saturates, to 2^31 - 1),
+// converted and summed in fp32 (pass 0's energy: error_model.cpp allows E
+// 100 u, this is < 36 u over a lane's 64 samples)
+typedef short i16x2_dot __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float dot_energy4(const unsigned (&d4)[4])
+{
+    float e = 0.f;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const i16x2_dot s = __builtin_bit_cast(i16x2_dot, d4[c]);
+        e += (float)__builtin_amdgcn_sdot2(s, s, 0, true);
+    }
+    return e;
+}
+
 template <int K, typename Chunk>
 __device__ __forceinline__ bool rescue_rows_fold0(const GoertzelParams &p, long long w, int seg,
                                                   bool amb_row, Chunk chunk)
@@ -350,12 +366,8 @@ __device__ __forceinline__ bool rescue_rows_fold0(const GoertzelParams &p, long 
         const u32x4e d = chunk(16 * m + seg);
         const unsigned d4[4] = {d.x, d.y, d.z, d.w};
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const int v = (int)(short)((d4[i >> 1] >> (16 * (i & 1))) & 0xFFFFu);
-            xf[i] += v;
-            const float xv = (float)v;
-            e = __builtin_fmaf(xv, xv, e);
-        }
+        for (int i = 0; i < 8; ++i) xf[i] += (int)(short)((d4[i >> 1] >> (16 * (i & 1))) & 0xFFFFu);
+        e += dot_energy4(d4);
     }
     double best = -1.0, second = -1.0;
     int arg = 0;
@@ -432,13 +444,7 @@ __device__ __forceinline__ void rescue_rows(const GoertzelParams &p, long long w
                 for (int q = q0; q < q1; ++q) {
                     const u32x4e d = chunk(q);
                     const unsigned d4[4] = {d.x, d.y, d.z, d.w};
-                    if (!exact && t == 0) {
-#pragma unroll
-                        for (int i = 0; i < 8; ++i) {
-                            const float xf = (float)(short)((d4[i >> 1] >> (16 * (i & 1))) & 0xFFFFu);
-                            e = __builtin_fmaf(xf, xf, e);
-                        }
-                    }
+                    if (!exact && t == 0) e += dot_energy4(d4);
 #pragma unroll
                     for (int i = 0; i < 8; ++i) {
                         const double x = (double)(short)((d4[i >> 1] >> (16 * (i & 1))) & 0xFFFFu);
