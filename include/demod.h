@@ -29,18 +29,22 @@
  * demod_error_model) is flagged, and the decision rescue
  * decides it again in double and rewrites its symbol and powers: first by
  * 64-sample segments, or by the window folded to 128 samples where every
- * tone sits on a multiple of 8 bins (n = 1024; its own derived bound against
- * the definition's, so the rewritten powers are within that bound of the
- * definition's, not its bits; FSKD_PASS0_FOLD=0 keeps segments), and where
+ * tone sits on a multiple of 8 bins, or by the residue fold (per tone the
+ * 8-point DFT of the N/8-spaced samples at its residue b mod 8) for the
+ * residue detector's integer-bin plans (n = 1024; each form with its own
+ * derived bound against the definition's, so the rewritten powers are within
+ * that bound of the definition's, not its bits; FSKD_PASS0_FOLD=0 keeps
+ * segments), and where
  * that pass cannot decide, with the
  * definition's own arithmetic (powers bit-identical to it; every rescued
  * window with FSKD_RESCUE_SEG=0). The flag test runs in two stages: the int16 worst-case
  * energy first (no per-sample work), then, only for windows that test
  * flags, the window's own energy, so quiet input is not flagged wholesale.
  * The rescue runs inside the detector's own launch for every detector at
- * n = 1024 whose windows are evaluated one by one (plain bank, fold, residue
- * and FFT); segment-shared windows (hop = 64 H < n, demod_slide_windows() > 0)
- * and other window lengths take a second launch on the same stream
+ * n = 1024 whose windows are evaluated one by one (plain bank, fold and FFT);
+ * segment-shared windows (hop = 64 H < n, demod_slide_windows() > 0), the
+ * residue detector's plans (their first pass lives there) and other window
+ * lengths take a second launch on the same stream
  * (demod_batch_launches counts it). A batch is complete when its stream has
  * passed its launches; there is no state shared between batches, so batches
  * of one handle may run on different streams.
@@ -157,8 +161,8 @@ int demod_max_symbols(const demod_t *st, size_t n_frames);
 /* Kernel launches one device-pointer demod_batch / demod_batch_async of
  * n_windows makes (with_mags: magnitudes requested): the detector's, plus one
  * for the decision rescue where it is not inside the detector (K >= 2 on
- * segment-shared windows or n != 1024; every other detector, the FFT
- * included, rescues inside its own launch). A Goertzel-family batch is one
+ * segment-shared windows, residue plans or n != 1024; every other detector,
+ * the FFT included, rescues inside its own launch). A Goertzel-family batch is one
  * detector launch; from 4 MiB of symbol + magnitude output it writes each
  * XCD's L2 back in a few bursts inside that launch instead of interleaving the
  * write-back with the input stream. With the environment
