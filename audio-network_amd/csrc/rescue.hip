@@ -190,7 +190,10 @@ __global__ __launch_bounds__(64) void rescue_kernel(RescueParams p)
 //    f K + t on tone t of window f, its 1 024 samples read from L2 directly:
 //    every rounding step of oracle/fsk_oracle.c, bit-identical powers and
 //    symbol.
-constexpr int kSegStates = 512;  // LDS end states per dense run: segments x K
+// LDS end states per dense run: segments x K (256: 4 waves per SIMD with the
+// 4-wave chunk blocks; 512 held them at 3 by LDS and measured 2 % slower on
+// the 2-FSK hop-256 worst case, profiles/round5/r5zx/)
+constexpr int kSegStates = 256;
 
 #ifdef FSKD_BOUNDS_DEBUG
 // debug builds only (a bounds probe): report an out-of-range index and clamp it
@@ -489,7 +492,7 @@ __device__ __forceinline__ bool seg_residue_window(const RescueParams &p, long l
 // stay in its own kernel (by segments 109 VGPRs, by the fold 85, by the
 // residue fold 128)
 template <int MODE>
-__global__ __launch_bounds__(64 * kRescueSplit) __attribute__((amdgpu_waves_per_eu(MODE == 0 ? 3 : 4)))
+__global__ __launch_bounds__(64 * kRescueSplit) __attribute__((amdgpu_waves_per_eu(4)))
 void rescue_seg_kernel(RescueParams p)
 {
 #pragma clang fp contract(off)
