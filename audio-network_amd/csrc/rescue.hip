@@ -556,7 +556,7 @@ void rescue_seg_kernel(RescueParams p)
     int Ts = T;  // windows for the per-window pass: idx[0 .. Ts)
     if (H > 0) {
         // the run length with the most windows per lane pass of the segment
-        // loop (hop 256, K = 2: 61 windows, 256 segments = 4 full passes)
+        // loop (hop 256, K = 2: 29 windows, 128 segments = 2 full passes)
         const int pairs = (K + 1) >> 1;
         int R = 1, Ri = 1;
         for (int r = 1; r <= 64 && ((r - 1) * H + 16) * K <= kSegStates; ++r) {
