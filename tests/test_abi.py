@@ -127,3 +127,29 @@ def test_batch_launches_matches_the_split_rule(A):
     and rejects a NULL handle."""
     lib = A.load_library()
     assert lib.demod_batch_launches(None, 10, 1) == A.DEMOD_BAD_ARG
+
+
+def test_plan_info_fft_pmask_and_pass0_forms(A):
+    """demod_plan_info without a device: the FFT's tones-only post-pass blocks
+    (fft_pmask, against the kernel's bin layout restated in
+    tests/test_gpu_fft_pmask.py) and the rescue first pass's form (fold64: 1
+    the fold, 2 the residue fold, 0 segments)."""
+    import numpy as np
+    from test_gpu_fft_pmask import pmask
+    rng = np.random.default_rng(5)
+    for _ in range(40):
+        k = int(rng.integers(2, 17))
+        bins = sorted(int(b) for b in rng.choice(np.arange(1, 512), size=k, replace=False))
+        if min(np.diff(bins)) < 2:
+            continue
+        cfg = A.make_cfg(freqs=tuple(46.875 * b for b in bins), method=A.METHOD_FFT)
+        assert A.plan_info(cfg)["fft_pmask"] == pmask(bins)
+    bin_ = 46.875
+    cases = [((1500.0, 3000.0), A.METHOD_AUTO, 1),                              # plain K = 2, fold form
+             (tuple(1500.0 + 375.0 * i for i in range(8)), A.METHOD_AUTO, 1),   # fold detector
+             (tuple(bin_ * (32 + 9 * i) for i in range(8)), A.METHOD_AUTO, 2),  # residue detector
+             (tuple(1234.5 + 1111.1 * i for i in range(8)), A.METHOD_GOERTZEL, 0)]
+    for freqs, method, form in cases:
+        info = A.plan_info(A.make_cfg(freqs=freqs, method=method))
+        assert info["fold64"] == form, (freqs, info["method"], info["fold64"])
+        assert info["fft_pmask"] == 0
