@@ -20,9 +20,10 @@
 // rescue_seg_kernel (n = 1024, round 5: the first pass, then the exact
 // chains of what it leaves).
 //
-// Layout: one wave per 512 consecutive windows (round 3: 4096; with every
-// window of a chunk flagged a wave served them one group after another, so
-// eight times more waves bound the worst case eight times lower). It first reads
+// Layout (rescue_kernel): one wave per 512 consecutive windows (round 3:
+// 4096; with every window of a chunk flagged a wave served them one group
+// after another, so eight times more waves bound the worst case eight times
+// lower; rescue_seg_kernel runs 4 waves per chunk, below). It first reads
 // their symbol bytes (dword loads, all in flight at once) and exits if none is
 // flagged — the common case: one short pass over 1 byte per window. Otherwise
 // it compacts the flagged windows, in order, into an LDS list. Goertzel:
