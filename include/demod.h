@@ -98,7 +98,12 @@ extern "C" {
                                     shared by the windows that contain them, same
                                     results as evaluating each window alone) */
 #define DEMOD_METHOD_FFT       2 /* full-spectrum n-point real FFT (n = 1024), argmax
-                                    over the tone bins round(f*n/fs) */
+                                    over the tone bins round(f*n/fs); tones-only
+                                    batches run the real split's post-pass only in
+                                    the pair blocks holding a tone bin (same tone
+                                    powers; demod_plan_info_t.fft_pmask;
+                                    FSKD_FFT_PMASK=0 at demod_create: every block,
+                                    a measurement switch) */
 #define DEMOD_METHOD_FOLDED    3 /* Goertzel over the window folded to n/8 samples:
                                     exact when every tone is on a multiple of 8
                                     bins (f*n/fs integer, divisible by 8); at
@@ -205,7 +210,8 @@ double demod_rescue_tau64(const demod_t *st);
  * E_det = sum x^2 of the window (plain bank, residue, FFT) or sum xf^2 of the
  * window folded to n/8 samples (energy = DEMOD_ENERGY_FOLDED). The kernels
  * flag a window when (P_1 - P_2)^2 < t2e E_eff P_1 (E_eff: the kernel's energy
- * E, Parseval's 2 sum_b P_b for the FFT, (sqrt E + amb_d)^2 for the fold
+ * E, Parseval's 2 sum_b P_b for the FFT (n sum x^2 from the samples on
+ * tones-only batches that skip post-pass blocks), (sqrt E + amb_d)^2 for the fold
  * detector), which leaves unflagged only windows whose sqrt-power margin
  * exceeds twice the two bounds: their symbol is the oracle's. */
 #define DEMOD_ENERGY_RAW      0
