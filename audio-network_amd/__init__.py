@@ -236,6 +236,9 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "demod_group_local_ranks": (ctypes.c_int, [_P]),
         "demod_group_rank_shard": (ctypes.c_int, [_P, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
                                                   ctypes.POINTER(_SZ), ctypes.POINTER(_SZ)]),
+        "demod_group_rank_device": (ctypes.c_int, [_P, ctypes.c_int]),
+        "demod_group_status": (ctypes.c_int, [_P]),
+        "demod_group_wait": (ctypes.c_int, [_P, _P]),
         "demod_group_push": (ctypes.c_int, [_P, _P, _P, _P, _SZ, _P]),
         "demod_group_bucket_async": (ctypes.c_longlong, [_P, _P, _SZ, _SZ, _SZ, _P, _P]),
         "demod_strerror": (ctypes.c_char_p, [ctypes.c_int]),
@@ -911,6 +914,26 @@ class Group:
         if rc != DEMOD_OK:
             raise DemodError(rc, "demod_group_rank_shard")
         return r.value, f.value, c.value
+
+    def device(self, local: int = 0) -> int:
+        """demod_group_rank_device: the GPU of the local-th rank this process drives."""
+        rc = self._lib.demod_group_rank_device(self._h, local)
+        if rc < 0:
+            raise DemodError(rc, "demod_group_rank_device")
+        return rc
+
+    def status(self) -> int:
+        """demod_group_status: DEMOD_OK while alive, else the code that killed it."""
+        return self._lib.demod_group_status(self._h)
+
+    def wait(self, streams: Optional[Sequence[int]] = None) -> None:
+        """demod_group_wait: wait for the last bucket on `streams`; raises the
+        lowest failing rank's code (the same on every rank)."""
+        n = self.local_ranks
+        ps = (ctypes.c_void_p * n)(*(streams or [0] * n))
+        rc = self._lib.demod_group_wait(self._h, ps if streams else None)
+        if rc != DEMOD_OK:
+            raise DemodError(rc, "demod_group_wait")
 
     def push(self, packets: Sequence[np.ndarray], cap: Optional[int] = None):
         """One packet per stream this process owns -> (symbols of every stream,

@@ -1097,18 +1097,31 @@ static size_t streams_windows(const demod_streams_t *ms, size_t s, size_t n_fram
 
 }  // extern "C"
 
-// The symbols each stream emits on a push of these packet sizes (exactly what
-// demod_streams_push will write to counts; demod_group.cpp gathers them
-// before the push). Returns the total.
-long long fskd::streams_counts(const demod_streams_t *ms, const size_t *n_frames, uint32_t *counts)
+// Every refusal demod_streams_push makes from its arguments and the handle's
+// state, before anything is consumed (all but the caller's cap and symbols
+// buffer), and the symbols each stream will emit (exactly what the push
+// writes to counts; nullable). demod_group.cpp runs it on every rank before
+// the first collective, so a refusal is agreed on rather than met mid-protocol.
+// Returns the total, or the push's negative code.
+long long fskd::streams_check(const demod_streams_t *ms, const int16_t *const *pcm, const size_t *n_frames,
+                              uint32_t *counts)
 {
-    if (!ms || !n_frames || !counts) return DEMOD_BAD_ARG;
-    long long w = 0;
-    for (size_t s = 0; s < ms->carry.size(); ++s) {
-        counts[s] = (uint32_t)streams_windows(ms, s, n_frames[s]);
-        w += counts[s];
+    if (!ms || !n_frames) return DEMOD_BAD_ARG;
+    const size_t S = ms->carry.size(), n = ms->cfg.n, hop = ms->cfg.hop;
+    size_t W = 0, Wb = 0;
+    for (size_t s = 0; s < S; ++s) {
+        if (n_frames[s] && (!pcm || !pcm[s])) return DEMOD_BAD_ARG;
+        if (n_frames[s] > ((size_t)1 << 40)) return DEMOD_BAD_ARG;
+        const size_t w = streams_windows(ms, s, n_frames[s]);
+        if (counts) counts[s] = (uint32_t)w;
+        W += w;
+        if (w) Wb += ((w - 1) * hop + n + hop - 1) / hop;  // ceil(L_s / hop): the batch slots
     }
-    return w;
+    if (W > 0x7FFFFFFF || W * n > ((size_t)1 << 40)) return DEMOD_BAD_ARG;
+    // the batch also counts the straddling windows that are computed and
+    // dropped, up to ~W n / hop: it must still fit an int count
+    if (Wb > 0x7FFFFFFF || Wb * hop > ((size_t)1 << 40)) return DEMOD_BAD_ARG;
+    return (long long)W;
 }
 
 int fskd::streams_device(const demod_streams_t *ms) { return ms ? ms->st->device : -1; }
@@ -1129,17 +1142,10 @@ int demod_streams_push(demod_streams_t *ms, const int16_t *const *pcm, const siz
     if (!ms || !n_frames || !counts) return DEMOD_BAD_ARG;
     const demod_cfg_t &c = ms->cfg;
     const size_t S = ms->carry.size(), n = c.n, hop = c.hop;
-    if (!pcm)
-        for (size_t s = 0; s < S; ++s)
-            if (n_frames[s]) return DEMOD_BAD_ARG;
-    size_t W = 0;
-    for (size_t s = 0; s < S; ++s) {
-        if (n_frames[s] && !pcm[s]) return DEMOD_BAD_ARG;
-        if (n_frames[s] > ((size_t)1 << 40)) return DEMOD_BAD_ARG;
-        W += streams_windows(ms, s, n_frames[s]);
-    }
+    const long long Wc = fskd::streams_check(ms, pcm, n_frames, nullptr);
+    if (Wc < 0) return (int)Wc;
+    const size_t W = (size_t)Wc;
     if (W > cap) return DEMOD_BUFFER_TOO_SMALL;
-    if (W > 0x7FFFFFFF || W * n > ((size_t)1 << 40)) return DEMOD_BAD_ARG;
     if (W && !symbols) return DEMOD_BAD_ARG;
     demod_t *st = ms->st;
     DeviceGuard guard(st->device);
@@ -1173,9 +1179,7 @@ int demod_streams_push(demod_streams_t *ms, const int16_t *const *pcm, const siz
             ms->first[s] = Wb;
             if (w) Wb += ((w - 1) * hop + n + hop - 1) / hop;  // ceil(L_s / hop)
         }
-        // Wb also counts the straddling windows that are computed and
-        // dropped, up to ~W n / hop: the batch must still fit an int count
-        if (Wb > 0x7FFFFFFF || Wb * hop > ((size_t)1 << 40)) return DEMOD_BAD_ARG;
+        // (Wb, with the straddling windows, was bounded by streams_check)
         const size_t samples = (Wb - 1) * hop + n;  // the last run ends exactly here or earlier
         int rc = ms->mapped ? ensure_mapped(ms, Wb * hop + n, Wb)
                             : ensure_host(st, std::max(Wb * hop + n, kSmallHostSamples),

@@ -75,9 +75,11 @@ struct ErrModel {
 // runs pass 0 (n = 1024, K >= 2, not switched off).
 void error_model(const demod_cfg_t &c, const Plan &pl, bool first_pass, ErrModel &m);
 
-// demod_api.cpp helpers for demod_group.cpp: the per-stream symbol counts a
-// push of these packet sizes emits (its total), and a streams handle's device
-long long streams_counts(const demod_streams_t *ms, const size_t *n_frames, uint32_t *counts);
+// demod_api.cpp helpers for demod_group.cpp: every argument refusal of
+// demod_streams_push (its code) or the per-stream symbol counts the push
+// emits (nullable counts; returns their total), and a streams handle's device
+long long streams_check(const demod_streams_t *ms, const int16_t *const *pcm, const size_t *n_frames,
+                        uint32_t *counts);
 int streams_device(const demod_streams_t *ms);
 
 }  // namespace fskd

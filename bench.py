@@ -234,6 +234,159 @@ def free_port() -> int:
     return p
 
 
+def hip_runtime():
+    """The process's HIP runtime (torch's libamdhip64.so.7, which
+    libfskdemod.so binds too: one runtime per process)."""
+    import ctypes
+    h = ctypes.CDLL("libamdhip64.so.7")
+    for f in ("hipGetLastError", "hipMalloc", "hipFree", "hipStreamIsCapturing", "hipStreamEndCapture",
+              "hipGraphDestroy"):
+        getattr(h, f).restype = ctypes.c_int
+    return h
+
+
+def capture_fail_hook():
+    """tests (BENCH_TEST_GRAPH_FAIL): a failure INSIDE a capture, as the
+    8-GPU node could meet one (profiles/round5/r5f_group_tests.log:77-86): a
+    hipMalloc while the stream captures (refused; it may invalidate the
+    capture and leaves a sticky error), then the exception it raises."""
+    import ctypes
+    hip = hip_runtime()
+    p = ctypes.c_void_p()
+    rc = hip.hipMalloc(ctypes.byref(p), 1 << 20)
+    raise RuntimeError("graph capture refused (BENCH_TEST_GRAPH_FAIL test hook: hipMalloc under "
+                       f"capture returned {rc})")
+
+
+def recover_after_capture(torch, ctx, dev):
+    """After an exception inside `with ctx` (a torch.cuda.graph): end the
+    capture if it is still open or was invalidated (torch's __exit__ skips
+    restoring the stream when capture_end raises), make the default stream
+    current again and clear the runtime's sticky error, so the eager fallback
+    starts from a clean state."""
+    import ctypes
+    hip = hip_runtime()
+    cs = getattr(ctx, "capture_stream", None)
+    if cs is not None:
+        st = ctypes.c_int(0)
+        if hip.hipStreamIsCapturing(ctypes.c_void_p(cs.cuda_stream), ctypes.byref(st)) == 0 and st.value:
+            gr = ctypes.c_void_p()
+            hip.hipStreamEndCapture(ctypes.c_void_p(cs.cuda_stream), ctypes.byref(gr))
+            if gr.value:
+                hip.hipGraphDestroy(gr)
+    torch.cuda.set_stream(torch.cuda.default_stream(dev))
+    hip.hipGetLastError()
+    try:
+        torch.cuda.synchronize()
+    except Exception:  # noqa: BLE001 - an error left by the failed capture
+        hip.hipGetLastError()
+        torch.cuda.synchronize()
+
+
+def capture(torch, dev, fn, hook=False):
+    """A HIP graph of fn() (returns (graph, fn's result)); on any failure
+    inside the capture the state is recovered (recover_after_capture) before
+    the exception propagates."""
+    g = torch.cuda.CUDAGraph()
+    ctx = torch.cuda.graph(g)
+    try:
+        with ctx:
+            out = fn()
+            if hook:
+                capture_fail_hook()
+    except Exception:
+        recover_after_capture(torch, ctx, dev)
+        raise
+    return g, out
+
+
+def c_group_bucket(A, D, torch, dist, cfg, n_streams, rank, world, group, dev, wps, bits, fstride, K,
+                   src, Rc, S, steps, warm, d_true, gunits, gunit, time_reps) -> dict:
+    """configs[4]'s bucket through demod_group_* (one communicator per rank:
+    demod_group_create with rank 0's demod_group_unique_id), timed as a HIP
+    graph (eager bucket if the capture fails), every rank's frames decoded
+    against the transmitted symbols, the ranks' status agreed through
+    demod_group_wait. A group that cannot be created on some rank (RCCL
+    refuses two ranks on one GPU) is a labelled error on every rank."""
+    api = "demod_group_bucket_async (C ABI, its own RCCL communicator)"
+    cg, err = None, None
+    try:
+        uid = None
+        if world > 1:
+            box = [A.group_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(box, src=0, group=group)
+            uid = box[0]
+        cg = A.Group(cfg, n_streams, rank=rank, world=world, uid=uid)
+    except Exception as e:  # noqa: BLE001 - reported in the line
+        err = f"{type(e).__name__}: {e}"[:300]
+    if world > 1:
+        # creation is agreed: one rank's failure is every rank's
+        oks = [None] * world
+        dist.all_gather_object(oks, err, group=group)
+        errs = [e for e in oks if e]
+        if errs and err is None:
+            err = "a peer rank: " + errs[0]
+    if err is not None:
+        if cg is not None:
+            cg.close()
+        return {"error": f"demod_group_create: {err}", "api": api}
+    hook = bool(os.environ.get("BENCH_TEST_GRAPH_FAIL"))
+    try:
+        cblock = A.group_block_bytes(n_streams, world, S, wps, bits)
+        c_all = torch.zeros(cblock * world, dtype=torch.uint8, device=dev)
+
+        def bucket():
+            cg.bucket_async([src], Rc, wps, S, [c_all], [torch.cuda.current_stream().cuda_stream])
+        # one eager bucket first: it sizes the group's buffers (no allocation
+        # may happen under capture) and warms the communicator
+        bucket()
+        cg.wait([torch.cuda.current_stream().cuda_stream])
+        n_rep = -(-steps // S)
+        graph_error = None
+        try:
+            g_, _ = capture(torch, dev, bucket, hook=hook)
+            c_ms = time_reps(lambda i: g_.replay(), S, n_rep, max(4, -(-warm // S)))
+            how = "hip graph"
+        except Exception as e:  # noqa: BLE001 - the eager bucket is timed instead
+            graph_error = f"{type(e).__name__}: {e}"[:300]
+            with torch.cuda.stream(torch.cuda.Stream(device=dev)):
+                c_ms = time_reps(lambda i: bucket(), S, n_rep, max(2, -(-warm // S)))
+                cg.wait([torch.cuda.current_stream().cuda_stream])
+            how = f"eager bucket (graph capture failed: {graph_error})"
+        torch.cuda.synchronize()
+        cg.wait()      # every rank's status word of the last bucket (raises the agreed code)
+        devs = [cg.device(0)]
+        if world > 1:
+            devs = [None] * world
+            dist.all_gather_object(devs, cg.device(0), group=group)
+        all_true = D.gather_symbols(d_true, gunits, world, unit=gunit, group=group) if world > 1 else d_true
+        bad = None
+        if rank == 0:
+            blocks = c_all.view(world, cblock).cpu().numpy()
+            tru = all_true.cpu().numpy().reshape(n_streams, wps)
+            bad = 0
+            for r_ in range(world):
+                first, cnt = D.shard_range(n_streams, r_, world)
+                for s_ in range(S):
+                    for j in range(cnt):
+                        off = (s_ * cnt + j) * fstride
+                        back = D.unframe_symbols(A, blocks[r_][off:off + fstride].tobytes(), wps, K)
+                        bad += int((back != tru[first + j]).sum())
+        out = {"ms_per_step": round(c_ms, 4), "step": how, "symbol_errors": bad,
+               "status": "ok (demod_group_wait: every rank's status word 0)",
+               "rank_devices": devs, "distinct_devices": len(set(devs)), "world": world,
+               "value": round(n_streams * wps * 1024 / (c_ms / 1e3) / 1e6, 1), "unit": "Msamples/s",
+               "api": api}
+        if graph_error:
+            out["graph_error"] = graph_error
+        return out
+    except Exception as e:  # noqa: BLE001 - reported in the line
+        return {"error": f"{type(e).__name__}: {e}"[:400], "api": api,
+                "group_status": cg.status() if cg is not None else None}
+    finally:
+        cg.close()
+
+
 def run_config(A, D, torch, dist, args, config, rank, world, local, use_dist, steps, warmup,
                plan="survey", method_name="auto", hop_fft=256, no_mags=False, spectrum=False,
                rescue_ab=False, parity_windows=0, n_streams_total=1024, sustain_s=0.0,
@@ -388,6 +541,36 @@ def run_config(A, D, torch, dist, args, config, rank, world, local, use_dist, st
     c_group = None
     ring_slots = 1
     graph_hook = bool(os.environ.get("BENCH_TEST_GRAPH_FAIL"))  # tests: the capture-failure path under gloo
+    ring, R = None, 1
+
+    def time_reps(fn, S_, n_rep, n_warm):
+        """ms per step of n_rep calls of fn(i) (S_ steps each) after n_warm,
+        between barriers, the max over ranks"""
+        for i in range(n_warm):
+            fn(i)
+        if world > 1:
+            dist.barrier(group=group)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(n_rep):
+            fn(i)
+        if world > 1:
+            dist.barrier(group=group)
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([el], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+            el = float(t.item())
+        return el / (n_rep * S_) * 1e3
+
+    def time_graphs(graphs, S_, n_rep):
+        return time_reps(lambda i: graphs[i % len(graphs)][0].replay(), S_, n_rep, max(4, -(-warm // S_)))
+
+    def note(msg):
+        if getattr(args, "breakdown", False):
+            print(f"bench.py: streams graph: {msg}", file=sys.stderr, flush=True)
+
     if use_dist and dev_framing and getattr(args, "graph", False) and (args.dist_backend == "nccl" or graph_hook):
         # HIP graph of S = --graph-steps steps (DESIGN.md §6). The graph's
         # branches do not run concurrently (measured: a framing kernel on a
@@ -419,8 +602,7 @@ def run_config(A, D, torch, dist, args, config, rank, world, local, use_dist, st
         # us). Every slot is a copy of the synthesised batch (the symbols of
         # every step are checked below); nothing is cached between steps:
         # the ring is >= 32x the MALL.
-        ring = d_magR = None
-        R = 1
+        d_magR = None
         if getattr(args, "ring", True) and S > 1:
             cap = float(getattr(args, "ring_gib", 8.0)) * 2 ** 30
             while 2 * R <= S and S % (2 * R) == 0 and 2 * R * W * n * 2 <= cap:
@@ -455,13 +637,10 @@ def run_config(A, D, torch, dist, args, config, rank, world, local, use_dist, st
             return None
 
         def build_bucket(kind, S_, use_ring=False):
-            if os.environ.get("BENCH_TEST_GRAPH_FAIL"):
-                # tests: a capture failure (test_self_launch_graph_failure_times_eager_bucket)
-                raise RuntimeError("graph capture refused (BENCH_TEST_GRAPH_FAIL test hook)")
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                gout = bucket_ops(kind, S_, use_ring)
-            return [(g, gout)]
+            # tests: BENCH_TEST_GRAPH_FAIL fails the capture from inside it
+            # (test_self_launch_graph_failure_times_eager_bucket)
+            return [capture(torch, dev, lambda: bucket_ops(kind, S_, use_ring),
+                            hook=bool(os.environ.get("BENCH_TEST_GRAPH_FAIL")))]
 
         def build_fork(kind):
             """round 3's step: two one-step graphs, framing + gather of the
@@ -485,50 +664,15 @@ def run_config(A, D, torch, dist, args, config, rank, world, local, use_dist, st
                 out.append((g, gout))
             return out
 
-        def time_graphs(graphs, S_, n_rep):
-            for i in range(max(4, -(-warm // S_))):
-                graphs[i % len(graphs)][0].replay()
-            if world > 1:
-                dist.barrier()
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            for i in range(n_rep):
-                graphs[i % len(graphs)][0].replay()
-            if world > 1:
-                dist.barrier()
-            torch.cuda.synchronize()
-            el = time.perf_counter() - t0
-            if world > 1:
-                t = torch.tensor([el], dtype=torch.float64, device=dev)
-                dist.all_reduce(t, op=dist.ReduceOp.MAX)
-                el = float(t.item())
-            return el / (n_rep * S_) * 1e3
-
-        def note(msg):
-            if getattr(args, "breakdown", False):
-                print(f"bench.py: streams graph: {msg}", file=sys.stderr, flush=True)
-
         def time_eager_bucket(S_, n_rep):
             """The same bucket without a graph, in this process (the fallback
             when capture or replay fails)"""
-            out = None
-            for _ in range(max(2, -(-warm // S_))):
-                out = bucket_ops("full", S_, ring is not None)
-            if world > 1:
-                dist.barrier()
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            for _ in range(n_rep):
-                out = bucket_ops("full", S_, ring is not None)
-            if world > 1:
-                dist.barrier()
-            torch.cuda.synchronize()
-            el = time.perf_counter() - t0
-            if world > 1:
-                t = torch.tensor([el], dtype=torch.float64, device=dev)
-                dist.all_reduce(t, op=dist.ReduceOp.MAX)
-                el = float(t.item())
-            return el / (n_rep * S_) * 1e3, out
+            box = [None]
+
+            def one(_i):
+                box[0] = bucket_ops("full", S_, ring is not None)
+            ms_ = time_reps(one, S_, n_rep, max(2, -(-warm // S_)))
+            return ms_, box[0]
 
         ms_per_step_eager = ms_per_step
         note(f"eager {ms_per_step:.4f} ms per step; capturing the {S}-step graph")
@@ -555,11 +699,10 @@ def run_config(A, D, torch, dist, args, config, rank, world, local, use_dist, st
             except Exception as e:  # noqa: BLE001 - the eager bucket is timed instead
                 err = f"{type(e).__name__}: {e}"[:300]
                 note(f"graph failed ({err}); timing the same bucket eagerly")
-                try:
-                    torch.cuda.synchronize()
-                except Exception:  # noqa: BLE001
-                    pass
-                ms_per_step, gathered = time_eager_bucket(S, n_rep)
+                # the capture's state was recovered (capture()); the eager
+                # bucket runs on a fresh stream
+                with torch.cuda.stream(torch.cuda.Stream(device=dev)):
+                    ms_per_step, gathered = time_eager_bucket(S, n_rep)
                 bucket = {"S": S, "gathered": gathered, "graph": False, "graph_error": err}
             st["i"] = None
         else:
@@ -568,56 +711,6 @@ def run_config(A, D, torch, dist, args, config, rank, world, local, use_dist, st
             ms_per_step = time_graphs(graphs, 1, n_rep)
             all_sym = graphs[(n_rep - 1) % 2][1]
             st["i"] = n_rep
-        if getattr(args, "c_group", False) and S > 1:
-            # the same bucket through the C ABI's RCCL group (demod_group_
-            # bucket_async: detector launches, device framing, ncclAllGather on
-            # its own communicator), captured and replayed the same way
-            # 
-            uid = None
-            if world > 1:
-                box = [A.group_unique_id() if rank == 0 else None]
-                dist.broadcast_object_list(box, src=0, group=group)
-                uid = box[0]
-            cg = A.Group(cfg, n_streams, rank=rank, world=world, uid=uid)
-            cblock = A.group_block_bytes(n_streams, world, S, wps, bits)
-            c_all = torch.zeros(cblock * world, dtype=torch.uint8, device=dev)
-            src = ring if ring is not None else d_pcm
-            Rc = R if ring is not None else 1
-
-            # one eager bucket first: it sizes the group's buffers (no
-            # allocation may happen under capture) and warms the communicator
-            cg.bucket_async([src], Rc, wps, S, [c_all], [torch.cuda.current_stream().cuda_stream])
-            torch.cuda.synchronize()
-
-            def build_c():
-                g_ = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g_):
-                    cg.bucket_async([src], Rc, wps, S, [c_all], [torch.cuda.current_stream().cuda_stream])
-                return [(g_, None)]
-            try:
-                c_ms = time_graphs(build_c(), S, -(-steps // S))
-                how = "hip graph"
-            except Exception as e:  # noqa: BLE001
-                c_ms = None
-                how = f"graph failed: {type(e).__name__}: {e}"[:200]
-            c_bad = None
-            if c_ms is not None:
-                all_true_c = D.gather_symbols(d_true, gunits, world, unit=gunit) if world > 1 else d_true
-                if rank == 0:
-                    blocks = c_all.view(world, cblock).cpu().numpy()
-                    tru = all_true_c.cpu().numpy().reshape(n_streams, wps)
-                    c_bad = 0
-                    for r_ in range(world):
-                        first, cnt = D.shard_range(n_streams, r_, world)
-                        for s_ in range(S):
-                            for j in range(cnt):
-                                off = (s_ * cnt + j) * fstride
-                                back = D.unframe_symbols(A, blocks[r_][off:off + fstride].tobytes(), wps, K)
-                                c_bad += int((back != tru[first + j]).sum())
-            cg.close()
-            c_group = {"ms_per_step": round(c_ms, 4) if c_ms is not None else None, "step": how,
-                       "symbol_errors": c_bad,
-                       "api": "demod_group_bucket_async (C ABI, its own RCCL communicator)"}
         if getattr(args, "breakdown", False):
             # where the step's time above the kernel goes
             def eager_det():
@@ -637,6 +730,17 @@ def run_config(A, D, torch, dist, args, config, rank, world, local, use_dist, st
                         time_graphs(build_bucket(kind, S, use_ring=True), S, -(-steps // S)), 4)
                     note(f"bucket {S} {kind} ring {breakdown[f'bucket_{S}step_{kind}_ring_ms']}")
             torch.cuda.synchronize()
+
+    if use_dist and dev_framing and getattr(args, "c_group", False):
+        # the same bucket through the C ABI's RCCL group (demod_group_bucket_
+        # async: detector launches, device framing, the ranks' status words
+        # and frames all-gathered on its own communicator), captured and
+        # replayed like the torch path's, with the same eager fallback; at
+        # N > 1 this is the product's own multi-GPU path
+        c_group = c_group_bucket(A, D, torch, dist, cfg, n_streams, rank, world, group, dev, wps, bits,
+                                 fstride, K, ring if ring is not None else d_pcm,
+                                 R if ring is not None else 1, max(1, int(getattr(args, "graph_steps", 1))),
+                                 steps, warm, d_true, gunits, gunit, time_reps)
 
     # correctness of the timed output: every symbol vs the transmitted one
     # (sliding windows straddle two symbols: compare the aligned ones only)
@@ -736,6 +840,19 @@ def run_config(A, D, torch, dist, args, config, rank, world, local, use_dist, st
         "d_pcm": d_pcm, "d_sym": d_sym, "d_mag": d_mag, "d_true": d_true, "cfg": cfg,
         "spectrum": d_spec is not None,
     }
+    if dev_framing and bucket is not None and bucket.get("det_graph_ms"):
+        # configs[4] on the step's own timing basis: the
+        # bucket's detector launches alone, graph-replayed (per step), and the
+        # whole graph step; the eager HIP-event figure stays beside them
+        rf = r["roofline"]
+        ach_g = alg_bytes / (bucket["det_graph_ms"] / 1e3) / 1e9
+        ach_s = alg_bytes / (ms_per_step / 1e3) / 1e9
+        rf.update({"achieved_eager_events": rf["achieved"], "frac_eager_events": rf["frac"],
+                   "achieved": round(ach_g, 1), "frac": round(ach_g / HBM_PEAK_GBPS, 4),
+                   "achieved_step": round(ach_s, 1), "frac_step": round(ach_s / HBM_PEAK_GBPS, 4),
+                   "basis": "detector_graph_ms_per_step: graph replays of the bucket's detector launches "
+                            "alone, per step (achieved_step: the whole graph step, ms_per_step)",
+                   "timed": "graph replays (the eager HIP-event figure: achieved_eager_events)"})
     if dev_framing or use_dist:
         # per-step cost above the detector kernel: the frame
         # kernel and the gather (overlapped with the next kernel), HIP events
@@ -776,7 +893,7 @@ def run_config(A, D, torch, dist, args, config, rank, world, local, use_dist, st
         if breakdown is not None:
             r["overhead"]["breakdown"] = breakdown
         if c_group is not None:
-            if c_group["ms_per_step"]:
+            if c_group.get("ms_per_step"):
                 c_group["ratio_to_torch_path"] = round(c_group["ms_per_step"] / ms_per_step, 4)
             r["overhead"]["c_group"] = c_group
     if config == "fft":
@@ -1357,6 +1474,9 @@ def main():
     ap.add_argument("--c-group", action="store_true",
                     help="streams config: also time the same bucket through the C ABI's RCCL group "
                          "(demod_group_bucket_async) and report it beside the torch path")
+    ap.add_argument("--no-c-group", action="store_true",
+                    help="N > 1: skip timing the configs[4] bucket through the C ABI's RCCL group "
+                         "(demod_group_*) beside the torch path")
     ap.add_argument("--breakdown", action="store_true",
                     help="streams config: also time the step's pieces (detector alone, graphs "
                          "without the gather / framing, 1 / S / 8 steps per graph)")
@@ -1485,6 +1605,9 @@ def main():
                 r.pop(k, None)
             torch.cuda.empty_cache()
             args.graph = args.dist_backend == "nccl" or bool(os.environ.get("BENCH_TEST_GRAPH_FAIL"))
+            # beside the torch path, the product's own multi-GPU path: the same
+            # bucket through demod_group_* on every rank
+            args.c_group = not args.no_c_group
             # >= 16 replays of the 16-step graph bucket, at N ranks and at N = 1
             # alike (2 replays left the rate within +-7 %, profiles/round4/r4g/)
             s_steps = max(args.steps, 256) if args.graph else args.steps
@@ -1496,6 +1619,8 @@ def main():
                    "unit": "Msamples/s", "ms_per_step": round(rs["ms_per_step"], 4),
                    "kernel_ms": round(rs["kernel_ms"], 4), "symbol_errors": rs["sym_err"],
                    "framing": rs["framed"], "overhead": rs.get("overhead")}
+            if ent["overhead"] and "c_group" in ent["overhead"]:
+                ent["c_group"] = ent["overhead"].pop("c_group")
             del rs
             torch.cuda.empty_cache()
             # the N = 1 reference runs the SAME step construction (graph step,
@@ -1512,6 +1637,16 @@ def main():
                                  "step (%s, gather over a one-rank group)"
                                  % ("HIP graph" if args.graph else "eager"))
                 ent["scaling_vs_n1"] = round(r1["ms_per_step"] / ent["ms_per_step"], 3)
+                c1 = (r1.get("overhead") or {}).get("c_group") or {}
+                cN = ent.get("c_group")
+                if cN is not None:
+                    cN["n1_ms_per_step"] = c1.get("ms_per_step")
+                    if c1.get("error"):
+                        cN["n1_error"] = c1["error"]
+                    if c1.get("ms_per_step") and cN.get("ms_per_step"):
+                        # the C group at N ranks against the same C group over
+                        # one rank on rank 0's GPU, the same bucket
+                        cN["scaling_vs_n1"] = round(c1["ms_per_step"] / cN["ms_per_step"], 3)
                 del r1
                 torch.cuda.empty_cache()
             dist.barrier()

@@ -392,6 +392,26 @@ int demod_group_world(const demod_group_t *g);
 int demod_group_local_ranks(const demod_group_t *g);   /* ranks this process drives */
 int demod_group_rank_shard(const demod_group_t *g, int local, int *rank, size_t *first,
                            size_t *count);
+/* The GPU ordinal of the local-th rank this process drives. */
+int demod_group_rank_device(const demod_group_t *g, int local);
+/* DEMOD_OK while the group is alive, else the code that killed it (see below). */
+int demod_group_status(const demod_group_t *g);
+
+/*
+ * Errors (no abort(), negative codes; no hang). Every call
+ * below is collective, and a rank never leaves one alone: each refusal is
+ * decided from all-gathered words, so every rank returns the same code.
+ * demod_group_push all-gathers [status, symbols == NULL, cap, per-stream
+ * counts] before anything is consumed: an argument refusal on any rank
+ * (demod_streams_push's own checks), a too-small cap or a total above INT_MAX
+ * on any rank returns that code (the lowest failing rank's) on every rank with
+ * nothing consumed. A push that fails on a rank after that point (device or
+ * allocation failure) returns its code on every rank and leaves the group
+ * dead: its communicator is aborted (ncclCommAbort), later calls return
+ * DEMOD_INVALID_STATE and the caller destroys it. A collective that fails, or
+ * does not finish within FSKD_GROUP_TIMEOUT_MS (default 120000: a peer process
+ * died), aborts the communicator the same way and returns DEMOD_DEVICE_ERROR.
+ */
 
 /*
  * One packet per stream this process owns (a local group: all n_streams; one
@@ -401,7 +421,8 @@ int demod_group_rank_shard(const demod_group_t *g, int local, int *rank, size_t 
  * return, on every rank, symbols[] holds all n_streams streams' symbols
  * (stream 0 first) and counts[0 .. n_streams-1] their counts. Returns the
  * total; if cap is too small, every rank returns DEMOD_BUFFER_TOO_SMALL
- * before anything is consumed.
+ * before anything is consumed. A local group runs its ranks concurrently
+ * (one host thread per GPU).
  */
 int demod_group_push(demod_group_t *g, const int16_t *const *pcm, const size_t *n_frames,
                      uint8_t *symbols, size_t cap, uint32_t *counts);
@@ -417,11 +438,24 @@ int demod_group_push(demod_group_t *g, const int16_t *const *pcm, const size_t *
  * [step][stream][stride]), all enqueued on streams[l] (hipStream_t; NULL
  * array = default streams), so a caller may capture it in a HIP graph (make
  * one call of the shape outside capture first: it sizes the rank's buffers).
- * Returns block bytes (demod_group_block_bytes) or a negative code.
+ * Every rank's status word is all-gathered beside the frames: a rank that
+ * fails locally (a NULL d_pcm / d_all entry, a failed launch) still posts both
+ * gathers, carrying its code, and returns that code; its peers learn it from
+ * demod_group_wait. Returns block bytes (demod_group_block_bytes) or a
+ * negative code (the shape, identical on every rank, is refused alike).
  */
 long long demod_group_bucket_async(demod_group_t *g, const int16_t *const *d_pcm, size_t ring,
                                    size_t wps, size_t steps, uint8_t *const *d_all,
                                    void *const *streams);
+
+/*
+ * After buckets (or graph replays of one) on streams[l] (NULL array: default
+ * streams): waits for them under the group's deadline, then returns the
+ * lowest failing rank's status of the last bucket (the same on every rank),
+ * DEMOD_OK, or DEMOD_DEVICE_ERROR when a collective failed or overran (the
+ * group is then dead, as above).
+ */
+int demod_group_wait(demod_group_t *g, void *const *streams);
 
 /* ---- ip.proto framing (ToReceiver{AudioData{bytes}}, delimited) ------- */
 

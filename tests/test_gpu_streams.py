@@ -59,6 +59,14 @@ def test_config5_streams_rccl_gather_world1():
     assert "%d detector launch" % lb["detector"] in ov["step"]
     # frac_p50 beside the mean-based frac
     assert 0 < line["roofline"]["frac_p50"] <= 1.5
+    # the roofline on the step's own basis: graph replays
+    # of the detector launches, the whole graph step beside it
+    rf = line["roofline"]
+    assert rf["basis"].startswith("detector_graph_ms_per_step"), rf
+    alg = rf["alg_bytes_per_launch"]
+    assert abs(rf["achieved"] - alg / (ov["detector_graph_ms_per_step"] / 1e3) / 1e9) <= 0.01 * rf["achieved"]
+    assert abs(rf["achieved_step"] - alg / (line["ms_per_step"] / 1e3) / 1e9) <= 0.01 * rf["achieved_step"]
+    assert rf["frac_step"] <= rf["frac"] + 1e-3 and "achieved_eager_events" in rf
     ps = line["parity_sample"]
     assert ps["symbol_mismatches"] == 0 and ps["max_rel_mag_err"] <= 1e-5
 
@@ -85,6 +93,37 @@ def test_config5_c_group_bucket_world1():
     print("\n" + json.dumps(cg))
     assert cg["step"] == "hip graph" and cg["symbol_errors"] == 0
     assert 0.8 <= cg["ratio_to_torch_path"] <= 1.25, cg
+    assert cg["rank_devices"] == [0] and cg["status"].startswith("ok")
+
+
+def test_config5_capture_failure_mid_capture_world1():
+    """a failure INSIDE the capture (BENCH_TEST_GRAPH_FAIL:
+    a hipMalloc while the stream captures, then an exception, for both the
+    torch bucket and the C group's): the capture is ended, the stream and the
+    runtime's sticky error are recovered, and both buckets are timed eagerly
+    on a fresh stream, every frame decoding to the transmitted symbols."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU visible")
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    env.pop("MASTER_PORT", None)
+    env["BENCH_TEST_GRAPH_FAIL"] = "1"
+    r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--config", "streams",
+                        "--force-dist", "--c-group", "--steps", "32", "--warmup", "5",
+                        "--no-cpu-baseline"], capture_output=True, timeout=400, cwd=ROOT, env=env)
+    out = r.stdout.decode()
+    assert r.returncode == 0, (out[-2000:], r.stderr.decode()[-4000:])
+    line = json.loads([ln for ln in out.splitlines() if ln.startswith("{")][-1])
+    ov = line["overhead"]
+    print("\n" + json.dumps({k: ov.get(k) for k in ("step", "graph_error", "c_group")}))
+    assert ov["step"].startswith("eager bucket (graph capture failed: RuntimeError"), ov
+    assert "hipMalloc under capture" in ov["graph_error"]
+    assert line["symbol_errors"] == 0 and line["framing"]["roundtrip_ok"]
+    cg = ov["c_group"]
+    assert "error" not in cg, cg
+    assert cg["step"].startswith("eager bucket (graph capture failed: RuntimeError"), cg
+    assert cg["symbol_errors"] == 0 and cg["ms_per_step"] > 0
 
 
 def test_config5_rank_shard_world1():
@@ -193,6 +232,12 @@ def test_self_launch_two_ranks_prints_n_gpus_2():
     c = line["rccl"]
     assert c["world_size"] == 2 and [q["rank"] for q in c["ranks"]] == [0, 1]
     assert c["distinct_devices"] == 1 and all(q["pci"] for q in c["ranks"])
+    # the C ABI group beside the torch path: RCCL refuses
+    # two ranks on one GPU, so it is a labelled error on the line and the
+    # torch entry above is kept
+    cg = s["c_group"]
+    assert cg["error"].startswith("demod_group_create"), cg
+    assert "demod_group_bucket_async" in cg["api"]
 
 
 def test_self_launch_graph_failure_times_eager_bucket():
@@ -220,6 +265,7 @@ def test_self_launch_graph_failure_times_eager_bucket():
     assert "error" not in s, s
     assert s["overhead"]["step"].startswith("eager bucket (graph capture failed: RuntimeError"), s["overhead"]
     assert "BENCH_TEST_GRAPH_FAIL" in s["overhead"]["graph_error"]
+    assert "hipMalloc under capture" in s["overhead"]["graph_error"]   # raised mid-capture
     assert s["symbol_errors"] == 0 and s["framing"]["roundtrip_ok"]
     assert s["scaling_vs_n1"] > 0 and s["n1_ms_per_step"] > 0
 

@@ -294,3 +294,83 @@ def test_group_push_and_bucket_world1(A):
     for s in range(steps):
         assert np.array_equal(allf[s * S * stride:(s + 1) * S * stride], one), s
     assert (sym == tru).all()
+
+
+def _group_with_env(A, monkeypatch, value, cfg, S, **kw):
+    monkeypatch.setenv("FSKD_GROUP_FAIL", value)   # read by demod_group_create*
+    try:
+        return A.Group(cfg, S, **kw)
+    finally:
+        monkeypatch.delenv("FSKD_GROUP_FAIL")
+
+
+@pytest.mark.parametrize("local", [False, True])
+def test_group_injected_failures_world1(A, monkeypatch, local):
+    """Injected failures (FSKD_GROUP_FAIL) through the real
+    RCCL group at world 1, both group kinds: a refusal before the push
+    returns its code and leaves the group alive with nothing consumed; a
+    failed push returns its code, kills the group (demod_group_status), and
+    every later call is refused with DEMOD_INVALID_STATE; a bucket whose rank
+    fails still posts its gathers and demod_group_wait returns the code."""
+    import numpy as np
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU visible")
+    kw = {"devices": [0]} if local else {}
+    cfg = A.make_cfg()
+    S = 3
+    rng = np.random.default_rng(11)
+    packets = [rng.integers(-20000, 20000, 2880 + 100 * s).astype(np.int16) for s in range(S)]
+    ms = A.Streams(S, cfg)
+    ref = [ms.push(packets) for _ in range(2)]
+    ms.close()
+    # refusal before the push: nothing consumed, the group stays usable
+    g = _group_with_env(A, monkeypatch, "check:0", cfg, S, **kw)
+    with pytest.raises(A.DemodError) as e:
+        g.push(packets)
+    assert e.value.code == A.DEMOD_INTERNAL_ERROR and g.status() == A.DEMOD_OK
+    g.close()
+    g = A.Group(cfg, S, **kw)
+    assert g.device(0) == 0 and g.status() == A.DEMOD_OK
+    for want in ref:   # the same symbols as demod_streams_push, push after push
+        sym, cnt = g.push(packets)
+        assert np.array_equal(sym, np.concatenate(want))
+    g.close()
+    # a failed push kills the group
+    g = _group_with_env(A, monkeypatch, "push:0", cfg, S, **kw)
+    with pytest.raises(A.DemodError) as e:
+        g.push(packets)
+    assert e.value.code == A.DEMOD_DEVICE_ERROR and g.status() == A.DEMOD_DEVICE_ERROR
+    with pytest.raises(A.DemodError) as e:
+        g.push(packets)
+    assert e.value.code == A.DEMOD_INVALID_STATE
+    dev = torch.device("cuda", 0)
+    d_pcm = torch.zeros((S * 4, 1024), dtype=torch.int16, device=dev)
+    block = A.group_block_bytes(S, 1, 2, 4, A.bits_per_symbol(2))
+    d_all = torch.zeros(block, dtype=torch.uint8, device=dev)
+    with pytest.raises(A.DemodError) as e:
+        g.bucket_async([d_pcm], 1, 4, 2, [d_all])
+    assert e.value.code == A.DEMOD_INVALID_STATE
+    g.close()
+    # a failing rank's bucket: its code returned, its gathers still posted,
+    # demod_group_wait reports it; the group stays alive
+    g = _group_with_env(A, monkeypatch, "bucket:0", cfg, S, **kw)
+    with pytest.raises(A.DemodError) as e:
+        g.bucket_async([d_pcm], 1, 4, 2, [d_all])
+    assert e.value.code == A.DEMOD_INTERNAL_ERROR
+    with pytest.raises(A.DemodError) as e:
+        g.wait()
+    assert e.value.code == A.DEMOD_INTERNAL_ERROR and g.status() == A.DEMOD_OK
+    g.close()
+    # a NULL gather target on a rank: refused, posted into the group's sink
+    with A.Group(cfg, S, **kw) as g:
+        assert g.bucket_async([d_pcm], 1, 4, 2, [d_all]) == block
+        g.wait()
+        with pytest.raises(A.DemodError) as e:
+            g.bucket_async([d_pcm], 1, 4, 2, [None])
+        assert e.value.code == A.DEMOD_BAD_ARG
+        with pytest.raises(A.DemodError) as e:
+            g.wait()
+        assert e.value.code == A.DEMOD_BAD_ARG
+        assert g.bucket_async([d_pcm], 1, 4, 2, [d_all]) == block   # alive: the next bucket is fine
+        g.wait()

@@ -75,3 +75,18 @@ def test_group_world1_push_equals_streams_push_native():
                        timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "gpu demod_group_push: world 1 equals demod_streams_push" in r.stdout
+
+
+def test_group_agreement_protocol_over_threads():
+    """demod_group_push's agreement protocol (csrc/group_flow.h, VERDICT r5
+    item 1) run over threads with injected failures (tests/native/
+    group_flow_test.cpp, ASan + UBSan): a refusal on any rank (arguments, cap,
+    NULL symbols, total > INT_MAX) returns the lowest failing rank's code on
+    every rank with no push anywhere; a failed push returns its code on every
+    rank and kills the group; a dead peer ends every other rank at the deadline
+    (DEMOD_DEVICE_ERROR), never a hang; 300 random fault plans agree."""
+    _make("group_flow_test")
+    r = subprocess.run([os.path.join(NATIVE, "group_flow_test")], capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "group flow OK" in r.stdout
