@@ -230,7 +230,25 @@ __global__ __launch_bounds__(64 * WPB) void fold_tile_kernel(GoertzelParams p)
     }
 
     const long long stride = (long long)gridDim.x * WPB;
-    for (long long t = tile_block(p.xcd_swizzle) * WPB + wave; t < n_tiles; t += stride) {
+    // one tile's loads (a buffer resource clamped to the batch's bytes)
+    auto load_tile = [&](long long tt, u32x4f (&v)[8]) {
+        const long long wb = tt * wins_per_tile;
+        long long bytes = ((p.n_windows - wb - 1) * p.hop + n) * 2;
+        if (bytes > 0x7FFFFFF0LL) bytes = 0x7FFFFFF0LL;
+        __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)(p.pcm + wb * p.hop), (short)0, (int)bytes, 0x00020000);
+#pragma unroll
+        for (int m = 0; m < 8; ++m)
+            v[m] = __builtin_amdgcn_raw_buffer_load_b128(rs, goff[m], 0, LAUX >= 0 ? LAUX : NT ? 2 : 0);
+    };
+    // PFN (LDST, K <= 2): the next tile's loads are issued as soon as this
+    // tile is in LDS, so they are in flight during this tile's arithmetic (as
+    // goertzel.hip's do_tile; round 6: K = 2 0.3050 -> see DESIGN.md §4.3)
+    constexpr bool PFN = LDST && K <= 2 && !F16;
+    u32x4f v[8];
+    const long long t_first = tile_block(p.xcd_swizzle) * WPB + wave;
+    if (PFN && t_first < n_tiles) load_tile(t_first, v);
+    for (long long t = t_first; t < n_tiles; t += stride) {
         const long long wbase = t * wins_per_tile;
         // the raw window's sum x^2 (fold_energy's fallback: rows whose folded
         // sums are all zero), from the tile in LDS (LDST) or L2
@@ -248,22 +266,19 @@ __global__ __launch_bounds__(64 * WPB) void fold_tile_kernel(GoertzelParams p)
             }
             return group_sum_f(e, log2g);
         };
-        long long bytes = ((p.n_windows - wbase - 1) * p.hop + n) * 2;
-        if (bytes > 0x7FFFFFF0LL) bytes = 0x7FFFFFF0LL;
-        __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            (void *)(p.pcm + wbase * p.hop), (short)0, (int)bytes, 0x00020000);
-        u32x4f v[8];
-#pragma unroll
-        for (int m = 0; m < 8; ++m)
-            v[m] = __builtin_amdgcn_raw_buffer_load_b128(rs, goff[m], 0, LAUX >= 0 ? LAUX : NT ? 2 : 0);
+        if (!PFN) load_tile(t, v);
         if (LDST) {
 #pragma unroll
             for (int m = 0; m < 8; ++m) wl[64 * m + lane] = v[m];
+            if (PFN && t + stride < n_tiles) load_tile(t + stride, v);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        u32x4f cur[8];
 #pragma unroll
-            for (int m = 0; m < 8; ++m) v[m] = wl[128 * win_in_tile + 16 * m + j];
+        for (int m = 0; m < 8; ++m) cur[m] = LDST ? wl[128 * win_in_tile + 16 * m + j] : v[m];
+        if (LDST) {
             __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
             __builtin_amdgcn_wave_barrier();
         }
@@ -273,7 +288,7 @@ __global__ __launch_bounds__(64 * WPB) void fold_tile_kernel(GoertzelParams p)
         for (int q = 0; q < 8; ++q) acc[q] = 0;
 #pragma unroll
         for (int m = 0; m < 8; ++m) {
-            const uint32_t d4[4] = {v[m].x, v[m].y, v[m].z, v[m].w};
+            const uint32_t d4[4] = {cur[m].x, cur[m].y, cur[m].z, cur[m].w};
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 acc[2 * q] += (int)(short)(d4[q] & 0xFFFFu);

@@ -239,8 +239,7 @@ def hip_runtime():
     libfskdemod.so binds too: one runtime per process)."""
     import ctypes
     h = ctypes.CDLL("libamdhip64.so.7")
-    for f in ("hipGetLastError", "hipMalloc", "hipFree", "hipStreamIsCapturing", "hipStreamEndCapture",
-              "hipGraphDestroy"):
+    for f in ("hipGetLastError", "hipMalloc", "hipStreamCreateWithFlags"):
         getattr(h, f).restype = ctypes.c_int
     return h
 
@@ -254,26 +253,45 @@ def capture_fail_hook():
     hip = hip_runtime()
     p = ctypes.c_void_p()
     rc = hip.hipMalloc(ctypes.byref(p), 1 << 20)
-    raise RuntimeError("graph capture refused (BENCH_TEST_GRAPH_FAIL test hook: hipMalloc under "
-                       f"capture returned {rc})")
+    raise CaptureHookError("graph capture refused (BENCH_TEST_GRAPH_FAIL test hook: hipMalloc under "
+                           f"capture returned {rc})")
 
 
-def recover_after_capture(torch, ctx, dev):
-    """After an exception inside `with ctx` (a torch.cuda.graph): end the
-    capture if it is still open or was invalidated (torch's __exit__ skips
-    restoring the stream when capture_end raises), make the default stream
-    current again and clear the runtime's sticky error, so the eager fallback
-    starts from a clean state."""
+class CaptureHookError(RuntimeError):
+    """capture_fail_hook's exception (the test hook's label survives the
+    capture_end error that replaces it when the capture was invalidated)."""
+
+
+_CAPTURE_STREAMS = []   # every capture's own HIP stream (never reused, never destroyed)
+
+
+def fresh_capture_stream(torch, dev):
+    """A brand-new HIP stream for one capture. A capture that fails inside
+    (a hipMalloc under capture, say) leaves its stream stuck in the
+    invalidated-capture state for good (HIP 7: the failed hipStreamEndCapture
+    does not reset it; profiles/round6/capture_fail_probe.log), and the next
+    capture begun on it cannot register torch's generator state, whose graph
+    then aborts the process when destroyed. torch's default capture stream
+    and its stream pool (32 streams, handed out round-robin) are both reused,
+    so each capture takes a stream of its own, never handed out again."""
     import ctypes
     hip = hip_runtime()
-    cs = getattr(ctx, "capture_stream", None)
-    if cs is not None:
-        st = ctypes.c_int(0)
-        if hip.hipStreamIsCapturing(ctypes.c_void_p(cs.cuda_stream), ctypes.byref(st)) == 0 and st.value:
-            gr = ctypes.c_void_p()
-            hip.hipStreamEndCapture(ctypes.c_void_p(cs.cuda_stream), ctypes.byref(gr))
-            if gr.value:
-                hip.hipGraphDestroy(gr)
+    s = ctypes.c_void_p()
+    rc = hip.hipStreamCreateWithFlags(ctypes.byref(s), ctypes.c_uint(1))   # hipStreamNonBlocking
+    if rc != 0:
+        raise RuntimeError(f"hipStreamCreateWithFlags: {rc}")
+    _CAPTURE_STREAMS.append(s.value)
+    return torch.cuda.ExternalStream(s.value, device=dev)
+
+
+def recover_after_capture(torch, dev):
+    """After an exception inside a capture (on its own stream: fresh_capture_
+    stream): torch's __exit__ skips restoring the current stream when
+    capture_end raises, so the default stream is made current again and the
+    runtime's sticky error is cleared; the capture's stream is abandoned. The
+    eager fallback then starts from a clean state (VERDICT r5 item 2;
+    profiles/round6/capture_fail_probe.log)."""
+    hip = hip_runtime()
     torch.cuda.set_stream(torch.cuda.default_stream(dev))
     hip.hipGetLastError()
     try:
@@ -283,19 +301,30 @@ def recover_after_capture(torch, ctx, dev):
         torch.cuda.synchronize()
 
 
-def capture(torch, dev, fn, hook=False):
-    """A HIP graph of fn() (returns (graph, fn's result)); on any failure
-    inside the capture the state is recovered (recover_after_capture) before
-    the exception propagates."""
+def capture(torch, dev, fn, hook=False, hook_first=False):
+    """A HIP graph of fn() on a capture stream of its own (returns (graph,
+    fn's result)); on any failure inside the capture the state is recovered
+    (recover_after_capture) before the exception propagates."""
     g = torch.cuda.CUDAGraph()
-    ctx = torch.cuda.graph(g)
+    ctx = torch.cuda.graph(g, stream=fresh_capture_stream(torch, dev))
+    hooked = []
     try:
         with ctx:
-            out = fn()
+            # hook_first: before fn's work (a gloo rehearsal: gloo's host
+            # copies of device tensors cannot run under capture)
+            out = None if (hook and hook_first) else fn()
             if hook:
-                capture_fail_hook()
-    except Exception:
-        recover_after_capture(torch, ctx, dev)
+                try:
+                    capture_fail_hook()
+                except CaptureHookError as e:
+                    hooked.append(str(e))
+                    raise
+    except Exception as e:
+        recover_after_capture(torch, dev)
+        if hooked and not isinstance(e, CaptureHookError):
+            # the invalidated capture's own error replaced the hook's
+            raise RuntimeError(f"{hooked[0]}; then capture_end: {type(e).__name__}: "
+                               f"{str(e).splitlines()[0]}") from e
         raise
     return g, out
 
@@ -640,7 +669,8 @@ def run_config(A, D, torch, dist, args, config, rank, world, local, use_dist, st
             # tests: BENCH_TEST_GRAPH_FAIL fails the capture from inside it
             # (test_self_launch_graph_failure_times_eager_bucket)
             return [capture(torch, dev, lambda: bucket_ops(kind, S_, use_ring),
-                            hook=bool(os.environ.get("BENCH_TEST_GRAPH_FAIL")))]
+                            hook=bool(os.environ.get("BENCH_TEST_GRAPH_FAIL")),
+                            hook_first=args.dist_backend == "gloo")]
 
         def build_fork(kind):
             """round 3's step: two one-step graphs, framing + gather of the

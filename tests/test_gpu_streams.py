@@ -119,6 +119,7 @@ def test_config5_capture_failure_mid_capture_world1():
     print("\n" + json.dumps({k: ov.get(k) for k in ("step", "graph_error", "c_group")}))
     assert ov["step"].startswith("eager bucket (graph capture failed: RuntimeError"), ov
     assert "hipMalloc under capture" in ov["graph_error"]
+    assert "capture_end" in ov["graph_error"]   # the capture was invalidated: torch's capture_end failed too
     assert line["symbol_errors"] == 0 and line["framing"]["roundtrip_ok"]
     cg = ov["c_group"]
     assert "error" not in cg, cg
