@@ -243,7 +243,8 @@ __global__ __launch_bounds__(64 * WPB) void fold_tile_kernel(GoertzelParams p)
     };
     // PFN (LDST, K <= 2): the next tile's loads are issued as soon as this
     // tile is in LDS, so they are in flight during this tile's arithmetic (as
-    // goertzel.hip's do_tile; round 6: K = 2 0.3050 -> see DESIGN.md §4.3)
+    // goertzel.hip's do_tile; round 6, configs[1] at K = 2: 0.3050 -> 0.3034
+    // ms per step, the plain bank 0.2966; profiles/round6/fold_k2_ab.log)
     constexpr bool PFN = LDST && K <= 2 && !F16;
     u32x4f v[8];
     const long long t_first = tile_block(p.xcd_swizzle) * WPB + wave;

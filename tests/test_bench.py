@@ -182,3 +182,20 @@ def test_extras_watchdog_after_the_line_only_exits():
     r = _watchdog_run("e = bench.extras_watchdog(lambda: {'value': 1.5}, 0, 0.5); e.printed = True; "
                       "print('{\"value\": 2.0}', flush=True); time.sleep(30)")
     assert r.returncode == 3 and r.stdout.strip().splitlines() == ['{"value": 2.0}']
+
+
+def test_implied_magnitude_bounds_per_shipped_config():
+    """the magnitude bound the derived error model implies
+    on an aligned window, per shipped configuration. configs[2] (fold F16) and
+    configs[3] (the FFT) are proven within north_star's 1e-5; configs[1] under
+    AUTO (the plain bank) is not (~7e-5: its bar is measured, parity_all), and
+    DEMOD_METHOD_FOLDED proves it on the same plan."""
+    A = bench.load_pkg()[0]
+    b = bench.implied_mag_bounds(A)
+    for key in ("configs[2]", "configs[3]_fsk2_hop256", "configs[3]_fsk8_hop256",
+                "configs[1]_method_folded"):
+        assert b[key]["within_1e-5"] and b[key]["bound"] <= 1e-5, (key, b[key])
+    assert b["configs[1]"]["detector"] == "goertzel" and not b["configs[1]"]["within_1e-5"]
+    assert 5e-5 < b["configs[1]"]["bound"] < 1e-4
+    assert b["configs[1]_method_folded"]["detector"] == "folded"
+    assert "MEASURED" in b["note"]
