@@ -219,6 +219,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "demod_streams_pending": (ctypes.c_int, [_P, _SZ]),
         "demod_streams_max_symbols": (ctypes.c_longlong, [_P, _P]),
         "demod_streams_push": (ctypes.c_int, [_P, _P, _P, _P, _P, _SZ, _P]),
+        "demod_streams_push_packets": (ctypes.c_int, [_P, _P, _P, _P, _P, ctypes.c_int, _P, _P, _SZ,
+                                                      _P]),
         "demod_synth_fsk": (ctypes.c_int, [ctypes.POINTER(DemodCfg), ctypes.c_uint64,
                                            ctypes.c_uint64, _SZ, ctypes.c_int, ctypes.c_int,
                                            _P, _P, _P]),
@@ -262,7 +264,7 @@ def header_exports(path: str = HEADER_PATH) -> list:
     skip = {"defined", "sizeof"}
     decl = []
     for m in re.finditer(r"^[^#\n][^;{}]*?\b([a-z_][a-z0-9_]*)\s*\([^;{}]*\)\s*;", src, flags=re.M):
-        if m.group(1) not in skip:
+        if m.group(1) not in skip and not m.group(0).lstrip().startswith("typedef"):
             decl.append(m.group(1))
     return sorted(set(decl)) if decl else sorted(set(names) - skip)
 
@@ -615,6 +617,45 @@ class Streams:
         if not mags:
             return out_s
         return out_s, [mag[e[i]:e[i + 1]] for i in range(S)]
+
+
+# demod_decode_fn: opus_decode's signature (opus.h:462)
+DECODE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32,
+                             ctypes.c_void_p, ctypes.c_int, ctypes.c_int)
+
+
+def push_packets(streams: "Streams", decode, decoders: Sequence[int], packets: Sequence[Optional[bytes]],
+                 frame_size: int, mags: bool = False, cap: Optional[int] = None):
+    """demod_streams_push_packets: one encoded packet per stream (bytes, or
+    None / b"" for none), decoded by `decode` (a DECODE_FN, or the address of
+    a native demod_decode_fn such as opus_decode) with decoders[i] (a state
+    pointer) into PCM, then pushed. Returns the per-stream symbol arrays (and
+    magnitude arrays)."""
+    lib = streams._lib
+    S = streams.n_streams
+    if len(packets) != S or len(decoders) != S:
+        raise DemodError(DEMOD_BAD_ARG, "one packet and one decoder per stream")
+    bufs = [ctypes.create_string_buffer(bytes(p), max(len(p), 1)) if p else None for p in packets]
+    pk = (ctypes.c_void_p * S)(*[ctypes.addressof(b) if b is not None else None for b in bufs])
+    lens = (ctypes.c_int32 * S)(*[len(p) if p else 0 for p in packets])
+    decs = (ctypes.c_void_p * S)(*decoders)
+    if cap is None:
+        frames = np.full(S, frame_size, dtype=np.uintp)
+        cap = int(lib.demod_streams_max_symbols(streams._h, frames.ctypes.data))
+    sym = np.empty(max(cap, 1), dtype=np.uint8)
+    mag = np.empty((max(cap, 1), streams.k), dtype=np.float32) if mags else None
+    counts = np.zeros(S, dtype=np.uint32)
+    fn = ctypes.cast(decode, ctypes.c_void_p) if not isinstance(decode, int) else ctypes.c_void_p(decode)
+    rc = lib.demod_streams_push_packets(streams._h, fn, decs, pk, lens, int(frame_size), _ptr(sym),
+                                        _ptr(mag), cap, counts.ctypes.data)
+    del bufs
+    if rc < 0:
+        raise DemodError(rc, "demod_streams_push_packets")
+    e = [0] + np.cumsum(counts, dtype=np.int64).tolist()
+    out_s = [sym[e[i]:e[i + 1]] for i in range(S)]
+    if not mags:
+        return out_s
+    return out_s, [mag[e[i]:e[i + 1]] for i in range(S)]
 
 
 def synth_fsk(cfg: DemodCfg, seed: int, n_windows: int, amplitude: int, sigma: int,

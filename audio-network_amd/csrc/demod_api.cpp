@@ -977,6 +977,9 @@ struct demod_streams {
     std::vector<size_t> have;             // per push: carry lengths before it
     std::vector<uint8_t> sym;             // per push: batch symbols / magnitudes
     std::vector<float> mag;
+    std::vector<int16_t> dec;             // push_packets: [stream][frame_size x channels] decoded PCM
+    std::vector<size_t> dec_frames;
+    std::vector<const int16_t *> dec_ptr;
     StagePool pool;                       // staging threads of large pushes
     // FSKD_STREAMS_MAPPED=1 (measurement switch, read at create): the push
     // stages into mapped pinned memory that the detector reads in place over
@@ -1273,6 +1276,56 @@ int demod_streams_push(demod_streams_t *ms, const int16_t *const *pcm, const siz
         ms->skip[s] -= std::min(ms->skip[s], n_frames[s]);
     }
     return (int)W;
+}
+
+int demod_streams_push_packets(demod_streams_t *ms, demod_decode_fn decode, void *const *decoders,
+                               const uint8_t *const *packets, const int32_t *lens, int frame_size,
+                               uint8_t *symbols, float *mags, size_t cap, uint32_t *counts)
+{
+    if (!ms || !decode || !decoders || !lens || !counts) return DEMOD_BAD_ARG;
+    if (frame_size < 1 || frame_size > (1 << 20)) return DEMOD_BAD_ARG;
+    const size_t S = ms->carry.size(), ch = ms->cfg.channels, per = (size_t)frame_size * ch;
+    for (size_t s = 0; s < S; ++s)
+        if (lens[s] < 0 || (lens[s] > 0 && (!packets || !packets[s]))) return DEMOD_BAD_ARG;
+    try {
+        ms->dec.resize(S * per);
+        ms->dec_frames.assign(S, 0);
+        ms->dec_ptr.assign(S, nullptr);
+    } catch (...) {
+        return DEMOD_ALLOC_FAIL;
+    }
+    // every stream's packet decoded by its own decoder (playback.cpp:118,
+    // opus_decode into the PCM buffer), on the handle's staging threads: the
+    // decoders are independent, so are the streams. A zero-length packet is
+    // no packet (playback.cpp:105 skips it): the stream pushes 0 frames.
+    std::vector<int> err(S, 0);
+    auto dec_one = [&](size_t s) {
+        if (lens[s] == 0) return;
+        int16_t *out = ms->dec.data() + s * per;
+        const int got = decode(decoders[s], packets[s], lens[s], out, frame_size, 0);
+        if (got < 0) err[s] = got;
+        else if (got > frame_size) err[s] = DEMOD_INTERNAL_ERROR;   // the decoder overran its frame_size
+        else {
+            ms->dec_frames[s] = (size_t)got;
+            ms->dec_ptr[s] = out;
+        }
+    };
+    size_t T = std::min<size_t>(kPushThreads, S);
+    if (S < 8) T = 1;
+    if (T >= 2) {
+        const std::function<void(size_t, size_t)> range = [&dec_one](size_t a, size_t e) {
+            for (size_t s = a; s < e; ++s) dec_one(s);
+        };
+        ms->pool.run(T, S, range);
+    } else {
+        for (size_t s = 0; s < S; ++s) dec_one(s);
+    }
+    // the lowest stream's decode error: nothing pushed, no carry consumed
+    // (the decoders' own states have advanced, as the reference's on a
+    // failed opus_decode)
+    for (size_t s = 0; s < S; ++s)
+        if (err[s]) return err[s];
+    return demod_streams_push(ms, ms->dec_ptr.data(), ms->dec_frames.data(), symbols, mags, cap, counts);
 }
 
 int demod_synth_fsk(const demod_cfg_t *cfg, uint64_t seed, uint64_t w0, size_t n_windows,

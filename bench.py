@@ -419,9 +419,12 @@ def c_group_bucket(A, D, torch, dist, cfg, n_streams, rank, world, group, dev, w
 def run_config(A, D, torch, dist, args, config, rank, world, local, use_dist, steps, warmup,
                plan="survey", method_name="auto", hop_fft=256, no_mags=False, spectrum=False,
                rescue_ab=False, parity_windows=0, n_streams_total=1024, sustain_s=0.0,
-               parity_every=0, group=None):
-    """Allocate, synthesise, warm up and time one workload; returns a dict."""
-    freqs = A.FSK8_FREQS if config == "fsk8" else A.FSK2_FREQS
+               parity_every=0, group=None, fft_plan="fsk2"):
+    """Allocate, synthesise, warm up and time one workload; returns a dict.
+    fft_plan: configs[3]'s tone plan (fsk2, or fsk8: the plan-independent
+    work, every post-pass block of the FFT's tones-only kernel that a
+    full 8-tone plan touches)."""
+    freqs = A.FSK8_FREQS if (config == "fsk8" or (config == "fft" and fft_plan == "fsk8")) else A.FSK2_FREQS
     if config == "fsk8" and plan == "odd":
         freqs = tuple(46.875 * (32 + 9 * i) for i in range(8))
     K = len(freqs)
@@ -1131,7 +1134,8 @@ def torch_index(flat, idx, hop, n):
 def summary(r) -> dict:
     """The extra-config entry of the bench line."""
     out = {"workload": (f"configs[2]: 8-FSK Goertzel, {r['W']} x 1024 windows" if r["config"] == "fsk8"
-                        else f"configs[3]: sliding 1024-pt FFT, hop {r['hop']}, {r['n_eval']} windows"
+                        else f"configs[3]: sliding 1024-pt FFT, hop {r['hop']}, {r['n_eval']} windows, "
+                        f"{r['K']}-tone plan {list(r['freqs'])}"
                         + (", full |X[b]|^2 spectrum stored (513 floats per window)"
                            if r.get("spectrum") else "")),
            "detector": r["detector"], "ms_per_step": round(r["ms_per_step"], 4),
@@ -1550,7 +1554,7 @@ def main():
                          "without the gather / framing, 1 / S / 8 steps per graph)")
     ap.add_argument("--extras-only", default="",
                     help="comma-separated subset of the default line's extras (measurement calls): "
-                         "fsk8, fft_hop256, fft_hop256_spectrum, host_e2e, error_model, rescue_worst, "
+                         "fsk8, fft_hop256, fft_hop256_fsk8, fft_hop256_spectrum, host_e2e, error_model, rescue_worst, "
                          "quiet_cost, streams")
     ap.add_argument("--extras-timeout", type=float, default=240.0,
                     help="N > 1: seconds the configs[4] extra may take before a watchdog prints "
@@ -1610,8 +1614,9 @@ def main():
 
         def want(key):  # --extras-only: a measurement call's subset of the extras
             return only is None or key in only
-        for key, cfgname, spec in (("fsk8", "fsk8", False), ("fft_hop256", "fft", False),
-                                   ("fft_hop256_spectrum", "fft", True)):
+        for key, cfgname, spec, fplan in (("fsk8", "fsk8", False, "fsk2"), ("fft_hop256", "fft", False, "fsk2"),
+                                          ("fft_hop256_fsk8", "fft", False, "fsk8"),
+                                          ("fft_hop256_spectrum", "fft", True, "fsk2")):
             if not want(key):
                 continue
             # >= 100 timed steps (>= 25 event-timed launches): at the driver's
@@ -1619,7 +1624,7 @@ def main():
             # launch moved 8-FSK's mean by 3 % (profiles/round4/r4z/: p50
             # 0.3126, mean 0.3197 ms)
             rr = run_config(A, D, torch, dist, args, cfgname, rank, world, local, False,
-                            max(args.steps, 100), args.warmup, hop_fft=256, spectrum=spec,
+                            max(args.steps, 100), args.warmup, hop_fft=256, spectrum=spec, fft_plan=fplan,
                             rescue_ab=not spec and not args.no_rescue_ab,
                             parity_windows=16384 if (cfgname == "fft" and not spec) else 0,
                             parity_every=0 if spec or args.no_cpu_baseline else 1)

@@ -363,6 +363,26 @@ long long demod_streams_max_symbols(const demod_streams_t *ms, const size_t *n_f
 int demod_streams_push(demod_streams_t *ms, const int16_t *const *pcm, const size_t *n_frames,
                        uint8_t *symbols, float *mags, size_t cap, uint32_t *counts);
 
+/*
+ * The packet front-end of many streams (SURVEY §8 f2's decoder-agnostic half):
+ * one encoded packet per stream, each decoded by `decode` with its stream's
+ * decoder state, then demodulated as by demod_streams_push (per-stream carry,
+ * lead-in, one batch). demod_decode_fn has opus_decode's signature
+ * (libopus/src/opus.h:462; opus_decode itself, cast, is one), as the
+ * reference calls it per packet (playback.cpp:115-122): it writes at most
+ * frame_size frames of `channels` interleaved int16 to pcm and returns the
+ * frames decoded or a negative code. decoders[i] is stream i's state (used by
+ * one thread at a time: streams decode concurrently on the handle's staging
+ * threads). lens[i] == 0: no packet for stream i this push (playback.cpp:105).
+ * A decoder's negative code (the lowest stream's) is returned with nothing
+ * pushed. Otherwise as demod_streams_push.
+ */
+typedef int (*demod_decode_fn)(void *decoder, const unsigned char *data, int32_t len, int16_t *pcm,
+                               int frame_size, int decode_fec);
+int demod_streams_push_packets(demod_streams_t *ms, demod_decode_fn decode, void *const *decoders,
+                               const uint8_t *const *packets, const int32_t *lens, int frame_size,
+                               uint8_t *symbols, float *mags, size_t cap, uint32_t *counts);
+
 /* ---- many streams over many GPUs (config 5), RCCL ---------------------- */
 /*
  * A group of `world` ranks, one per GPU, demodulating n_streams streams of one

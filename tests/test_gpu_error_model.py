@@ -191,3 +191,54 @@ def test_fft_kernel_equals_emulation(A, O, torch):
             del os.environ["FSKD_NO_RESCUE"]
         else:
             os.environ["FSKD_NO_RESCUE"] = old
+
+
+FFT_TONE_PLANS = {
+    "fsk2": [32, 64],
+    "fsk8": [32 + 8 * i for i in range(8)],
+    "all": [3 + 31 * i for i in range(16)],
+}
+
+
+@pytest.mark.parametrize("hop", [1024, 256])
+@pytest.mark.parametrize("plan", sorted(FFT_TONE_PLANS))
+def test_fft_tones_only_kernel_equals_emulation(A, O, torch, plan, hop):
+    """the SHIPPED tones-only FFT instantiation (the device
+    batch with magnitudes and no spectrum: PICK 2, the pair-block post-pass
+    mask fft_pmask, OVL at hop < n; the configs[3] kernel) equals
+    fp32emu.fft_spectrum at the plan's tone bins bit for bit (rescue off), so
+    the CPU proof of the FFT bound (tests/test_error_bound.py over the
+    emulation) covers the code the bench times. Nearest reference FFT:
+    kiss_fft.c:569-589 (tests/test_gpu_parity.py pins the spectrum to it)."""
+    import numpy as np
+    import fp32emu as E
+    bins = FFT_TONE_PLANS[plan]
+    freqs = tuple(EM.BIN * b for b in bins)
+    cfg = A.make_cfg(hop=hop, freqs=freqs, method=A.METHOD_FFT)
+    info = A.plan_info(cfg)
+    if plan != "all":
+        assert bin(info["fft_pmask"] & 0xFF).count("1") < 8   # the post-pass is masked
+    old = os.environ.get("FSKD_NO_RESCUE")
+    os.environ["FSKD_NO_RESCUE"] = "1"
+    try:
+        d = A.Demodulator(cfg)
+    finally:
+        if old is None:
+            del os.environ["FSKD_NO_RESCUE"]
+        else:
+            os.environ["FSKD_NO_RESCUE"] = old
+    with d:
+        for fi, fam in enumerate(("fsk_s400", "two_tone_equal", "random_full", "near_nyquist_tone")):
+            W = 1024 + 3
+            blocks = -(-((W - 1) * hop + 1024) // 1024)
+            x = EM.family(fam, freqs, 1024, blocks, 500 + fi)[:(W - 1) * hop + 1024]
+            xt = torch.from_numpy(x).cuda()
+            sym = torch.empty(W, dtype=torch.uint8, device="cuda")
+            mag = torch.empty((W, len(bins)), dtype=torch.float32, device="cuda")
+            d.batch_async(xt, W, sym, mag)
+            torch.cuda.synchronize()
+            got = mag.cpu().numpy()
+            emu = E.fft_spectrum(x, hop, W)[:, bins]
+            diff = np.flatnonzero((got.view(np.uint32) != emu.astype(np.float32).view(np.uint32)).any(axis=1))
+            assert diff.size == 0, (plan, hop, fam, diff.size, diff[:4].tolist(), got[diff[:1]].tolist(),
+                                    emu[diff[:1]].tolist())

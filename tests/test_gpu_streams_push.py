@@ -374,3 +374,58 @@ def test_group_injected_failures_world1(A, monkeypatch, local):
         assert e.value.code == A.DEMOD_BAD_ARG
         assert g.bucket_async([d_pcm], 1, 4, 2, [d_all]) == block   # alive: the next bucket is fine
         g.wait()
+
+
+def _passthrough(A, channels, fail_on=None, calls=None):
+    """A PCM pass-through demod_decode_fn (opus_decode's signature): the
+    packet's bytes are interleaved int16 frames."""
+    import ctypes
+
+    def dec(state, data, ln, pcm, frame_size, fec):
+        if calls is not None:
+            calls.append(int(state or 0))
+        if fail_on is not None and int(state or 0) == fail_on:
+            return A.DEMOD_INVALID_PACKET
+        frames = ln // (2 * channels)
+        if frames > frame_size:
+            return A.DEMOD_BUFFER_TOO_SMALL
+        ctypes.memmove(pcm, data, frames * 2 * channels)
+        return frames
+    return A.DECODE_FN(dec)
+
+
+@pytest.mark.parametrize("channels", [1, 2])
+def test_push_packets_passthrough_equals_push(A, torch, channels):
+    """demod_streams_push_packets with a PCM pass-through
+    decoder (opus_decode's signature) equals demod_streams_push byte for byte
+    over rounds of ragged packets with lead-in, empty packets (no packet, as
+    playback.cpp:105) and 12 streams (staging threads decode concurrently);
+    a decoder error returns its code with nothing consumed."""
+    import numpy as np
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU visible")
+    S = 12
+    cfg = A.make_cfg(channels=channels, channel_mode=A.CH_DOWNMIX if channels == 2 else A.CH_LEFT,
+                     lead_in=312)
+    rng = np.random.default_rng(40 + channels)
+    a, b = A.Streams(S, cfg), A.Streams(S, cfg)
+    fn = _passthrough(A, channels)
+    for rnd in range(6):
+        pk = [rng.integers(-20000, 20000, channels * (2880 - 97 * s - 13 * rnd)).astype(np.int16)
+              for s in range(S)]
+        pk[(rnd * 5) % S] = np.zeros(0, np.int16)          # no packet for one stream
+        want = a.push(pk, mags=True)
+        got = A.push_packets(b, fn, [1 + s for s in range(S)], [p.tobytes() for p in pk], 2880,
+                             mags=True)
+        for s in range(S):
+            assert np.array_equal(want[0][s], got[0][s]), (rnd, s)
+            assert np.array_equal(want[1][s].view(np.uint32), got[1][s].view(np.uint32)), (rnd, s)
+    pend = [b.pending(s) for s in range(S)]
+    bad = _passthrough(A, channels, fail_on=1 + 7)
+    pk = [rng.integers(-20000, 20000, channels * 2880).astype(np.int16).tobytes() for _ in range(S)]
+    with pytest.raises(A.DemodError) as e:
+        A.push_packets(b, bad, [1 + s for s in range(S)], pk, 2880)
+    assert e.value.code == A.DEMOD_INVALID_PACKET
+    assert [b.pending(s) for s in range(S)] == pend        # nothing consumed
+    a.close()
+    b.close()
