@@ -17,10 +17,12 @@
 //      |X[512 - k]|^2.
 // LDS traffic per window: 4 KiB written + 4 KiB read for the transpose (plus
 // 2 KiB of bin powers when the full spectrum is stored) — against 12 + 12 KiB
-// for a 64-lane radix-8 Stockham layout (scripts/fft_r0.hip), whose LDS writes
+// for a 64-lane radix-8 Stockham layout (scripts/fft_r0.hip, in git history
+// at 8b49018), whose LDS writes
 // bound it (guide: ds_write aggregates 38-51 TB/s). Every twiddle product is
 // fused into the butterfly that consumes it (fft1024_quad_kernel below); the
-// round-1 kernel with separate products is scripts/fft_quad_r1b.hip.
+// round-1 kernel with separate products is scripts/fft_quad_r1b.hip (git
+// history, 8b49018).
 #include <algorithm>
 #include <cstdlib>
 #include <type_traits>

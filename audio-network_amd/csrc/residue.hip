@@ -150,7 +150,7 @@ __device__ __forceinline__ void residue_even_classes_asm(const f2 (&p02)[2], con
 // [4 classes][QP sample pairs][64 lanes] float4 (4 QP KiB).
 constexpr int kResidueQP = 2;  // shipped: two sample pairs per LDS round
 
-// Tunables (defaults = shipped, chosen with scripts/probe.hip):
+// Tunables (defaults = shipped, chosen with scripts/probe.hip, in git history at 8b49018):
 //   ASM   butterflies as residue_classes_asm (else the plain-C residue_classes),
 //   ROTV  rotation constants in VGPRs (8 per tone) instead of the LDS table,
 //   MINW  > 0: ask for MINW waves per SIMD (VGPR budget 512 / MINW),
