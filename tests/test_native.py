@@ -90,3 +90,20 @@ def test_group_agreement_protocol_over_threads():
                        timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "group flow OK" in r.stdout
+
+
+def test_rescue_bounds_checking_build_compiles(tmp_path):
+    """the bounds-checking build of the rescue launch
+    (FSKD_BOUNDS_DEBUG: RS_CHECK reports and clamps an out-of-range index,
+    the instrument that found round 5's dense-run fault) stays buildable for
+    gfx950."""
+    import shutil
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    if not os.path.exists(hipcc):
+        pytest.skip("no hipcc")
+    csrc = os.path.join(os.path.dirname(HERE), "audio-network_amd", "csrc")
+    r = subprocess.run([hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC",
+                        "-mcode-object-version=5", "-I" + os.path.join(os.path.dirname(HERE), "include"),
+                        "-DFSKD_BOUNDS_DEBUG", "-c", os.path.join(csrc, "rescue.hip"),
+                        "-o", str(tmp_path / "rescue_dbg.o")], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
