@@ -541,6 +541,14 @@ def run_config(A, D, torch, dist, args, config, rank, world, local, use_dist, st
     for _ in range(warm):
         step()
     flush()
+    settle = None
+    if not use_dist:
+        # round 6: the transient does not always end by launch 64 (a closing
+        # run timed 20 steps at 0.3045 ms whose 6 s sustained rate was 0.2956,
+        # profiles/round6/r6close/): further untimed warmup in chunks until
+        # the per-step time has settled (settle_warmup)
+        n_more, settle = settle_warmup(torch, step)
+        warm += n_more
     timed = [i % EV_EVERY == 0 for i in range(steps)]
     evs = [mk(3) if timed[i] else None for i in range(steps)]
     gevs = [mk(2) if timed[i] else None for i in range(steps)] if use_dist else None
@@ -852,7 +860,7 @@ def run_config(A, D, torch, dist, args, config, rank, world, local, use_dist, st
     r = {
         "config": config, "freqs": freqs, "K": K, "n": n, "hop": hop, "W": W, "n_eval": n_eval,
         "total_windows": total_windows, "ms_per_step": ms_per_step, "kernel_ms": kernel_ms,
-        "kts": kts, "sym_err": sym_err, "framed": framed, "warm": warm,
+        "kts": kts, "sym_err": sym_err, "framed": framed, "warm": warm, "settle": settle,
         "detector": {A.METHOD_GOERTZEL: "goertzel", A.METHOD_FOLDED: "folded",
                      A.METHOD_RESIDUE: "residue",
                      A.METHOD_FFT: "fft1024"}.get(demod.method, str(demod.method)),
@@ -1022,6 +1030,25 @@ def run_config(A, D, torch, dist, args, config, rank, world, local, use_dist, st
         del sl
     demod.close()
     return r
+
+
+def settle_warmup(torch, fn, chunk=16, max_chunks=32, tol=0.01):
+    """Untimed warmup past the clock transient: chunks of `chunk` steps, each
+    timed (synchronised), until two consecutive chunks agree within tol and
+    the last is within 3 % of the fastest chunk seen (at most max_chunks,
+    ~0.15 s at configs[1]). Returns (steps run, per-chunk ms per step)."""
+    times = []
+    for _ in range(max_chunks):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(chunk):
+            fn()
+        torch.cuda.synchronize()
+        times.append((time.perf_counter() - t0) / chunk * 1e3)
+        if (len(times) >= 2 and abs(times[-1] - times[-2]) <= tol * times[-1]
+                and times[-1] <= 1.03 * min(times)):
+            break
+    return len(times) * chunk, [round(t, 4) for t in times]
 
 
 def time_steps(torch, fn, steps, warm) -> float:
@@ -1800,6 +1827,7 @@ def headline_line(args, r, world, extras) -> dict:
         "steps": args.steps,
         "warmup": args.warmup,
         "warmup_effective": r["warm"],
+        "warmup_settle_ms_per_step": r.get("settle"),
         "ms_per_step": round(r["ms_per_step"], 4),
         "higher_is_better": True,
         "scaling": "strong" if config == "streams" else "weak",
