@@ -199,3 +199,49 @@ def test_implied_magnitude_bounds_per_shipped_config():
     assert 5e-5 < b["configs[1]"]["bound"] < 1e-4
     assert b["configs[1]_method_folded"]["detector"] == "folded"
     assert "MEASURED" in b["note"]
+
+
+def test_settle_warmup_waits_out_a_transient(monkeypatch):
+    """bench.settle_warmup (round 6): untimed chunks until two consecutive
+    chunks agree within 1 % and the last is within 3 % of the fastest; a
+    transient (slow chunks after fast ones) is waited out, a steady device
+    stops after two chunks, and the cap bounds a device that never settles.
+    A fake clock advances by each step's scheduled time (deterministic)."""
+    clock = [0.0]
+
+    class FakeCuda:
+        @staticmethod
+        def synchronize():
+            pass
+
+    class FakeTorch:
+        cuda = FakeCuda
+
+    class FakeTime:
+        @staticmethod
+        def perf_counter():
+            return clock[0]
+
+    monkeypatch.setattr(bench, "time", FakeTime)
+
+    def make(schedule):
+        it = iter(schedule)
+
+        def fn():
+            clock[0] += next(it, schedule[-1]) * 1e-3
+        return fn
+    chunk = 4
+    n, times = bench.settle_warmup(FakeTorch, make([2.0] * 400), chunk=chunk)
+    assert n == 2 * chunk and times == [2.0, 2.0]
+    # fast, then a transient 30 % slower for 5 chunks, then back
+    sched = [2.0] * chunk + [2.6] * (5 * chunk) + [2.0] * 400
+    n, times = bench.settle_warmup(FakeTorch, make(sched), chunk=chunk)
+    assert n == 8 * chunk and times[-2:] == [2.0, 2.0], times
+    # a ramp down from a high start settles once it flattens at the floor
+    sched = [3.0] * chunk + [2.5] * chunk + [2.05] * chunk + [2.0] * 400
+    n, times = bench.settle_warmup(FakeTorch, make(sched), chunk=chunk)
+    assert times[-1] == 2.0 and n == 5 * chunk, times
+    # never settles: alternating chunks, capped
+    alt = ([2.0] * chunk + [3.0] * chunk) * 50
+    n, times = bench.settle_warmup(FakeTorch, make(alt), chunk=chunk, max_chunks=6)
+    assert n == 6 * chunk and len(times) == 6
