@@ -542,12 +542,20 @@ def run_config(A, D, torch, dist, args, config, rank, world, local, use_dist, st
         step()
     flush()
     settle = None
-    if not use_dist:
+    if not dev_framing:
         # round 6: the transient does not always end by launch 64 (a closing
         # run timed 20 steps at 0.3045 ms whose 6 s sustained rate was 0.2956,
         # profiles/round6/r6close/): further untimed warmup in chunks until
-        # the per-step time has settled (settle_warmup)
-        n_more, settle = settle_warmup(torch, step)
+        # the per-step time has settled (settle_warmup). With the gather
+        # (use_dist) every step holds a collective, so the ranks agree on
+        # each chunk (all settled, or go on) and run the same number of steps
+        def agree(ok):
+            if world == 1:
+                return ok
+            t = torch.tensor([0.0 if ok else 1.0], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+            return float(t.item()) == 0.0
+        n_more, settle = settle_warmup(torch, step, agree=agree, flush=flush if use_dist else None)
         warm += n_more
     timed = [i % EV_EVERY == 0 for i in range(steps)]
     evs = [mk(3) if timed[i] else None for i in range(steps)]
@@ -1032,21 +1040,28 @@ def run_config(A, D, torch, dist, args, config, rank, world, local, use_dist, st
     return r
 
 
-def settle_warmup(torch, fn, chunk=16, max_chunks=32, tol=0.01):
+def settle_warmup(torch, fn, chunk=16, max_chunks=32, tol=0.01, agree=None, flush=None):
     """Untimed warmup past the clock transient: chunks of `chunk` steps, each
     timed (synchronised), until two consecutive chunks agree within tol and
     the last is within 3 % of the fastest chunk seen (at most max_chunks,
-    ~0.15 s at configs[1]). Returns (steps run, per-chunk ms per step)."""
+    ~0.15 s at configs[1]). agree(settled) -> bool makes the stop decision
+    common to every rank (the steps hold collectives); flush() ends a chunk's
+    pending gather. Returns (steps run, per-chunk ms per step)."""
     times = []
     for _ in range(max_chunks):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(chunk):
             fn()
+        if flush is not None:
+            flush()
         torch.cuda.synchronize()
         times.append((time.perf_counter() - t0) / chunk * 1e3)
-        if (len(times) >= 2 and abs(times[-1] - times[-2]) <= tol * times[-1]
-                and times[-1] <= 1.03 * min(times)):
+        ok = (len(times) >= 2 and abs(times[-1] - times[-2]) <= tol * times[-1]
+              and times[-1] <= 1.03 * min(times))
+        if agree is not None:
+            ok = agree(ok)
+        if ok:
             break
     return len(times) * chunk, [round(t, 4) for t in times]
 
