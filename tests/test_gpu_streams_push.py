@@ -429,3 +429,45 @@ def test_push_packets_passthrough_equals_push(A, torch, channels):
     assert [b.pending(s) for s in range(S)] == pend        # nothing consumed
     a.close()
     b.close()
+
+
+def test_push_packets_argument_and_decoder_errors(A, torch):
+    """demod_streams_push_packets' refusals: a negative length, a NULL
+    packet with a length, frame_size outside [1, 2^20], a decoder that
+    claims more frames than frame_size (DEMOD_INTERNAL_ERROR) — each with
+    nothing consumed; every packet empty (no decode call) pushes nothing."""
+    import ctypes
+    import numpy as np
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU visible")
+    S = 3
+    ms = A.Streams(S, A.make_cfg())
+    lib = ms._lib
+    calls = []
+    ok = _passthrough(A, 1, calls=calls)
+    decs = (ctypes.c_void_p * S)(1, 2, 3)
+    counts = np.zeros(S, np.uint32)
+    sym = np.zeros(64, np.uint8)
+    buf = (ctypes.c_uint8 * 64)()
+    pk = (ctypes.c_void_p * S)(ctypes.addressof(buf), None, ctypes.addressof(buf))
+
+    def push(lens, frame_size=2880, fn=ok, packets=pk):
+        ln = (ctypes.c_int32 * S)(*lens)
+        return lib.demod_streams_push_packets(ms._h, ctypes.cast(fn, ctypes.c_void_p), decs, packets, ln,
+                                              frame_size, sym.ctypes.data, None, sym.size,
+                                              counts.ctypes.data)
+    assert push([4, -1, 0]) == A.DEMOD_BAD_ARG
+    assert push([4, 4, 0]) == A.DEMOD_BAD_ARG          # stream 1 has no packet pointer
+    assert push([4, 0, 0], frame_size=0) == A.DEMOD_BAD_ARG
+    assert push([4, 0, 0], frame_size=(1 << 20) + 1) == A.DEMOD_BAD_ARG
+    assert calls == []                                   # refused before any decode
+
+    def liar(state, data, ln, pcm, frame_size, fec):
+        return frame_size + 1
+    bad = A.DECODE_FN(liar)
+    assert push([4, 0, 4], frame_size=2, fn=bad) == A.DEMOD_INTERNAL_ERROR
+    assert [ms.pending(s) for s in range(S)] == [0, 0, 0]
+    assert push([0, 0, 0], packets=None) == 0 and calls == [] and counts.sum() == 0
+    assert push([64, 0, 64]) == 0 and sorted(calls) == [1, 3]     # 32 frames each: no window yet
+    assert [ms.pending(s) for s in range(S)] == [32, 0, 32]
+    ms.close()
