@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Summarise the SQ/GRBM passes of scripts/gpu_pmc_sq.sh (gpurun_out/sq_*/):
+"""Summarise the SQ/GRBM passes of scripts/gpu_pmc_sq.sh (removed in round 6; git show 8b49018:scripts/gpu_pmc_sq.sh) (gpurun_out/sq_*/):
 per-dispatch means of the kernel each pass profiled, and the derived issue
 fractions, into profiles/round1/pmc_sq_kernels.json.
 
