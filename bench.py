@@ -1587,7 +1587,8 @@ def main():
                          "of one launch over an S-slot input ring")
     ap.add_argument("--c-group", action="store_true",
                     help="streams config: also time the same bucket through the C ABI's RCCL group "
-                         "(demod_group_bucket_async) and report it beside the torch path")
+                         "(demod_group_bucket_async) and report it beside the torch path (always on "
+                         "for the N > 1 configs[4] extra unless --no-c-group)")
     ap.add_argument("--no-c-group", action="store_true",
                     help="N > 1: skip timing the configs[4] bucket through the C ABI's RCCL group "
                          "(demod_group_*) beside the torch path")
