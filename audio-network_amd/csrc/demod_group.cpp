@@ -331,8 +331,19 @@ struct PushOps {
 // the ranks' common result (they agree by construction; a disagreement is
 // reported as DEMOD_INTERNAL_ERROR).
 template <class F>
-long long each_rank(demod_group_t *g, F fn)
+long long each_rank(demod_group_t *g, F fn_)
 {
+    // no exception leaves a rank's thread or the C ABI: a host allocation
+    // that fails inside the flow ends that rank with DEMOD_ALLOC_FAIL (its
+    // peers then meet the missing rank at their deadline and abort)
+    auto fn = [&](size_t l) -> long long {
+        try {
+            return fn_(l);
+        } catch (...) {
+            kill_rank(g, g->ranks[l], DEMOD_ALLOC_FAIL);
+            return DEMOD_ALLOC_FAIL;
+        }
+    };
     const size_t L = g->ranks.size();
     std::vector<long long> rc(L, DEMOD_OK);
     std::vector<std::thread> th;
