@@ -195,3 +195,75 @@ def test_bucket_gather_blocks(A, O, world, n_streams):
                 off = (s * cnt + j) * fstride
                 back = D.unframe_symbols(A, blocks[r][off:off + fstride].tobytes(), wps, k)
                 assert (back == tru[first + j]).all(), (s, r, j)
+
+
+def _settle_worker(rank, world, port, q):
+    try:
+        sys.path.insert(0, ROOT)
+        import torch
+        import torch.distributed as dist
+        import bench
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        clock = [0.0]
+
+        class FakeCuda:
+            @staticmethod
+            def synchronize():
+                pass
+
+        class FakeTorch:
+            cuda = FakeCuda
+
+        class FakeTime:
+            @staticmethod
+            def perf_counter():
+                return clock[0]
+        bench.time = FakeTime
+        # rank r's device ramps down from a transient for 3 r chunks of 4
+        # steps (3.0, 2.85, ... ms per step), then runs at 2.0
+        sched = [3.0 - 0.15 * c for c in range(3 * rank) for _ in range(4)] + [2.0] * 1000
+        it = iter(sched)
+        steps = [0]
+
+        def fn():
+            steps[0] += 1
+            clock[0] += next(it) * 1e-3
+
+        def agree(ok):
+            t = torch.tensor([0.0 if ok else 1.0])
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            return float(t.item()) == 0.0
+        n, times = bench.settle_warmup(FakeTorch, fn, chunk=4, agree=agree)
+        q.put((rank, n, steps[0], times))
+        dist.destroy_process_group()
+    except BaseException:
+        import traceback
+        q.put(("error", traceback.format_exc()))
+        raise
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_settle_warmup_agreed_across_ranks(world):
+    """bench.py's settle warmup at N > 1 (round 6): every step holds a
+    collective, so the ranks must run the same number of warmup steps. Each
+    rank's (fake) device settles after a different number of chunks; with
+    the agreement (gloo all-reduce of each rank's verdict, as bench.py does
+    on the device) every rank runs the slowest rank's count."""
+    pytest.importorskip("torch")
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_settle_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=120)
+    assert all(r[0] != "error" for r in res), res
+    counts = {r[1] for r in res} | {r[2] for r in res}
+    assert len(counts) == 1, res                      # the same steps on every rank
+    slowest = 3 * (world - 1) + 2                      # chunks until the last rank settles
+    assert counts == {4 * slowest}, res
