@@ -243,8 +243,11 @@ __global__ __launch_bounds__(64 * WPB) void fold_tile_kernel(GoertzelParams p)
     };
     // PFN (LDST, K <= 2): the next tile's loads are issued as soon as this
     // tile is in LDS, so they are in flight during this tile's arithmetic (as
-    // goertzel.hip's do_tile; round 6, configs[1] at K = 2: 0.3050 -> 0.3034
-    // ms per step, the plain bank 0.2966; profiles/round6/fold_k2_ab.log)
+    // goertzel.hip's do_tile) when a wave takes more than one tile. With the
+    // shipped one-tile-per-wave grid (tile_grid) it never issues; what it
+    // changes there is the register allocation (114 VGPRs, 4 waves/SIMD,
+    // instead of 84 / 5), measured 0.5 % faster at K = 2 (0.3033 vs 0.3048 ms,
+    // interleaved; the plain bank 0.2967; profiles/round6/fold_k2_ab.log)
     constexpr bool PFN = LDST && K <= 2 && !F16;
     u32x4f v[8];
     const long long t_first = tile_block(p.xcd_swizzle) * WPB + wave;
